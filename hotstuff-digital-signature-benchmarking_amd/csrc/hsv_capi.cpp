@@ -1,0 +1,312 @@
+// C ABI of libhsv.so (declared in include/hsv.h): device contexts, staging
+// buffers, sharding across GPUs, and the reference-shaped entry points.
+//
+// Host-buffer calls stage inputs into pinned memory, copy them to HBM on a
+// per-device stream, launch the verification kernel and copy the flag bytes
+// back.  Batches above kShardMin items are split into contiguous ranges, one
+// per visible GPU, each driven by its own host thread; the per-item flags are
+// written straight into the caller's output (the "host gather").
+// There is no CPU verification path: without a GPU every call returns
+// HSV_ERR_NO_DEVICE.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "hsv.h"
+#include "hsv_internal.h"
+
+namespace {
+
+thread_local std::string t_last_error = "";
+
+int fail(int code, const std::string &msg) {
+  t_last_error = msg;
+  return code;
+}
+
+int hip_fail(const char *where, hipError_t e) {
+  return fail(HSV_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+constexpr size_t kAlign = 256;
+constexpr size_t kChunk = size_t(1) << 22;     // items per launch (512 MiB of inputs max)
+constexpr size_t kShardMin = size_t(1) << 16;  // shard host batches across GPUs above this
+
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct DevCtx {
+  int device = 0;
+  int cus = 0;
+  hipStream_t stream = nullptr;
+  uint8_t *d_buf = nullptr;
+  size_t d_cap = 0;
+  uint8_t *h_buf = nullptr;
+  size_t h_cap = 0;
+  std::mutex mu;
+};
+
+struct Global {
+  std::mutex mu;
+  bool inited = false;
+  int ndev = 0;
+  std::vector<DevCtx *> ctx;
+  std::atomic<int> variant{0};
+};
+
+Global &G() {
+  static Global g;
+  return g;
+}
+
+int ensure_init() {
+  Global &g = G();
+  std::lock_guard<std::mutex> lk(g.mu);
+  if (g.inited) return g.ndev > 0 ? HSV_OK : fail(HSV_ERR_NO_DEVICE, "no HIP device visible");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  g.ndev = n;
+  for (int i = 0; i < n; ++i) {
+    DevCtx *c = new DevCtx();
+    c->device = i;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, i) == hipSuccess) c->cus = prop.multiProcessorCount;
+    g.ctx.push_back(c);
+  }
+  if (const char *v = std::getenv("HSV_VARIANT")) g.variant = std::atoi(v);
+  g.inited = true;
+  return n > 0 ? HSV_OK : fail(HSV_ERR_NO_DEVICE, "no HIP device visible");
+}
+
+int ctx_prepare(DevCtx &c, size_t dev_bytes, size_t host_bytes) {
+  hipError_t e = hipSetDevice(c.device);
+  if (e != hipSuccess) return hip_fail("hipSetDevice", e);
+  if (!c.stream) {
+    e = hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail("hipStreamCreate", e);
+  }
+  if (dev_bytes > c.d_cap) {
+    if (c.d_buf) (void)hipFree(c.d_buf);
+    c.d_buf = nullptr;
+    c.d_cap = 0;
+    const size_t cap = round_up(dev_bytes, size_t(1) << 20);
+    e = hipMalloc(&c.d_buf, cap);
+    if (e != hipSuccess) return hip_fail("hipMalloc", e);
+    c.d_cap = cap;
+  }
+  if (host_bytes > c.h_cap) {
+    if (c.h_buf) (void)hipHostFree(c.h_buf);
+    c.h_buf = nullptr;
+    c.h_cap = 0;
+    const size_t cap = round_up(host_bytes, size_t(1) << 20);
+    e = hipHostMalloc(&c.h_buf, cap, hipHostMallocDefault);
+    if (e != hipSuccess) return hip_fail("hipHostMalloc", e);
+    c.h_cap = cap;
+  }
+  return HSV_OK;
+}
+
+// Host records: item i at pk + i*pk_stride, sig + i*sig_stride, msg + i*msg_stride
+// (msg_stride 0 = shared).  Runs [0, n) on one device, chunk by chunk.
+int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t *sig,
+                  size_t sig_stride, const uint8_t *msg, size_t msg_stride, size_t n,
+                  uint8_t *flags_out) {
+  std::lock_guard<std::mutex> lk(c.mu);
+  const size_t chunk = std::min(n, kChunk);
+  const size_t pk_off = 0;
+  const size_t sig_off = round_up(chunk * 32, kAlign);
+  const size_t msg_off = sig_off + round_up(chunk * 64, kAlign);
+  const size_t msg_bytes = msg_stride ? chunk * 32 : 32;
+  const size_t flag_off = msg_off + round_up(msg_bytes, kAlign);
+  const size_t total = flag_off + round_up(chunk, kAlign);
+  int rc = ctx_prepare(c, total, total);
+  if (rc != HSV_OK) return rc;
+  const int variant = G().variant.load();
+  for (size_t base = 0; base < n; base += chunk) {
+    const size_t m = std::min(chunk, n - base);
+    uint8_t *h = c.h_buf;
+    // pack into the dense layout the kernel reads (pk 32 | sig 64 | msg 32)
+    if (pk_stride == 32) std::memcpy(h + pk_off, pk + base * 32, m * 32);
+    else for (size_t i = 0; i < m; ++i) std::memcpy(h + pk_off + 32 * i, pk + (base + i) * pk_stride, 32);
+    if (sig_stride == 64) std::memcpy(h + sig_off, sig + base * 64, m * 64);
+    else for (size_t i = 0; i < m; ++i) std::memcpy(h + sig_off + 64 * i, sig + (base + i) * sig_stride, 64);
+    if (msg_stride == 0) std::memcpy(h + msg_off, msg, 32);
+    else if (msg_stride == 32) std::memcpy(h + msg_off, msg + base * 32, m * 32);
+    else for (size_t i = 0; i < m; ++i) std::memcpy(h + msg_off + 32 * i, msg + (base + i) * msg_stride, 32);
+    const size_t in_bytes = msg_off + (msg_stride ? m * 32 : 32);
+    hipError_t e = hipMemcpyAsync(c.d_buf, h, in_bytes, hipMemcpyHostToDevice, c.stream);
+    if (e != hipSuccess) return hip_fail("hipMemcpyAsync H2D", e);
+    e = hsv_launch_verify(variant, c.d_buf + pk_off, 32, c.d_buf + sig_off, 64, c.d_buf + msg_off,
+                          msg_stride ? 32 : 0, (uint32_t)m, c.d_buf + flag_off, nullptr, c.stream);
+    if (e != hipSuccess) return hip_fail("verify kernel launch", e);
+    e = hipMemcpyAsync(h + flag_off, c.d_buf + flag_off, m, hipMemcpyDeviceToHost, c.stream);
+    if (e != hipSuccess) return hip_fail("hipMemcpyAsync D2H", e);
+    e = hipStreamSynchronize(c.stream);
+    if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
+    std::memcpy(flags_out + base, h + flag_off, m);
+  }
+  return HSV_OK;
+}
+
+int run_host(const uint8_t *pk, size_t pk_stride, const uint8_t *sig, size_t sig_stride,
+             const uint8_t *msg, size_t msg_stride, size_t n, uint8_t *flags_out) {
+  if (n == 0) return HSV_OK;
+  if (!pk || !sig || !msg || !flags_out) return fail(HSV_ERR_INVALID_ARG, "null pointer");
+  int rc = ensure_init();
+  if (rc != HSV_OK) return rc;
+  Global &g = G();
+  const int ndev = g.ndev;
+  if (ndev == 1 || n < kShardMin) return run_on_device(*g.ctx[0], pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out);
+  // contiguous shards, one host thread per GPU
+  std::vector<int> rcs(ndev, HSV_OK);
+  std::vector<std::string> errs(ndev);
+  std::vector<std::thread> th;
+  for (int d = 0; d < ndev; ++d) {
+    const size_t lo = n * d / ndev, hi = n * (d + 1) / ndev;
+    th.emplace_back([&, d, lo, hi]() {
+      if (hi > lo)
+        rcs[d] = run_on_device(*g.ctx[d], pk + lo * pk_stride, pk_stride, sig + lo * sig_stride,
+                               sig_stride, msg + lo * msg_stride, msg_stride, hi - lo,
+                               flags_out + lo);
+      if (rcs[d] != HSV_OK) errs[d] = t_last_error;
+    });
+  }
+  for (auto &t : th) t.join();
+  for (int d = 0; d < ndev; ++d)
+    if (rcs[d] != HSV_OK) return fail(rcs[d], "device " + std::to_string(d) + ": " + errs[d]);
+  return HSV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hsv_init(int device) {
+  int rc = ensure_init();
+  if (rc != HSV_OK) return rc;
+  Global &g = G();
+  if (device >= g.ndev) return fail(HSV_ERR_INVALID_ARG, "device index out of range");
+  return device < 0 ? g.ndev : 1;
+}
+
+void hsv_shutdown(void) {
+  Global &g = G();
+  std::lock_guard<std::mutex> lk(g.mu);
+  for (DevCtx *c : g.ctx) {
+    std::lock_guard<std::mutex> lk2(c->mu);
+    if (hipSetDevice(c->device) == hipSuccess) {
+      if (c->stream) (void)hipStreamDestroy(c->stream);
+      if (c->d_buf) (void)hipFree(c->d_buf);
+      if (c->h_buf) (void)hipHostFree(c->h_buf);
+    }
+    c->stream = nullptr;
+    c->d_buf = c->h_buf = nullptr;
+    c->d_cap = c->h_cap = 0;
+  }
+}
+
+int hsv_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+const char *hsv_last_error(void) { return t_last_error.c_str(); }
+
+const char *hsv_version(void) { return "hsv 0.1.0 (gfx950)"; }
+
+// Measurement/test hook (not in hsv.h): pick the kernel variant.
+int hsv_set_variant(int v) {
+  if (v < 0 || v >= hsv_num_variants()) return fail(HSV_ERR_INVALID_ARG, "bad variant");
+  G().variant = v;
+  return HSV_OK;
+}
+
+int hsv_get_variant(void) { return G().variant.load(); }
+
+int hsv_verify(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, size_t msg_stride,
+               size_t n, uint8_t *flags_out) {
+  if (msg_stride != 0 && msg_stride != 32) return fail(HSV_ERR_INVALID_ARG, "msg_stride must be 0 or 32");
+  return run_host(pk, 32, sig, 64, msg, msg_stride, n, flags_out);
+}
+
+int hsv_verify_strict(const uint8_t digest[32], const uint8_t pk[32], const uint8_t sig[64]) {
+  uint8_t f = 0;
+  int rc = run_host(pk, 32, sig, 64, digest, 0, 1, &f);
+  if (rc != HSV_OK) return rc;
+  return (f & HSV_STRICT_OK) ? 1 : 0;
+}
+
+static int batch_verdict(const std::vector<uint8_t> &flags) {
+  for (uint8_t f : flags)
+    if ((f & (HSV_PARSE_OK | HSV_EQ_OK)) != (HSV_PARSE_OK | HSV_EQ_OK)) return 0;
+  return 1;
+}
+
+int hsv_verify_batch(const uint8_t digest[32], const uint8_t *pk, const uint8_t *sig, size_t n) {
+  if (n == 0) return 1;  // dalek verify_batch over zero items is Ok
+  std::vector<uint8_t> flags(n);
+  int rc = run_host(pk, 32, sig, 64, digest, 0, n, flags.data());
+  if (rc != HSV_OK) return rc;
+  return batch_verdict(flags);
+}
+
+int hsv_verify_batch_packed(const uint8_t digest[32], const uint8_t *votes, size_t n) {
+  if (n == 0) return 1;
+  if (!votes) return fail(HSV_ERR_INVALID_ARG, "null votes");
+  std::vector<uint8_t> flags(n);
+  int rc = run_host(votes, 96, votes + 32, 96, digest, 0, n, flags.data());
+  if (rc != HSV_OK) return rc;
+  return batch_verdict(flags);
+}
+
+int hsv_verify_device_bits(const uint8_t *d_pk, size_t pk_stride, const uint8_t *d_sig,
+                           size_t sig_stride, const uint8_t *d_msg, size_t msg_stride, size_t n,
+                           uint8_t *d_flags, uint32_t *d_strict_bits, void *stream) {
+  if (n == 0) return HSV_OK;
+  if (!d_pk || !d_sig || !d_msg) return fail(HSV_ERR_INVALID_ARG, "null input pointer");
+  if (!d_flags && !d_strict_bits) return fail(HSV_ERR_INVALID_ARG, "no output");
+  const uintptr_t mis = (reinterpret_cast<uintptr_t>(d_pk) | reinterpret_cast<uintptr_t>(d_sig) |
+                         reinterpret_cast<uintptr_t>(d_msg) | pk_stride | sig_stride | msg_stride) & 15u;
+  if (mis) return fail(HSV_ERR_ALIGN, "device pointers and strides must be multiples of 16");
+  if (pk_stride < 32 || sig_stride < 64 || (msg_stride != 0 && msg_stride < 32))
+    return fail(HSV_ERR_INVALID_ARG, "record strides overlap");
+  int rc = ensure_init();
+  if (rc != HSV_OK) return rc;
+  const int variant = G().variant.load();
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  for (size_t base = 0; base < n; base += kChunk) {
+    const size_t m = std::min(kChunk, n - base);
+    hipError_t e = hsv_launch_verify(
+        variant, d_pk + base * pk_stride, pk_stride, d_sig + base * sig_stride, sig_stride,
+        d_msg + base * msg_stride, msg_stride, (uint32_t)m, d_flags ? d_flags + base : nullptr,
+        d_strict_bits ? d_strict_bits + base / 32 : nullptr, s);
+    if (e != hipSuccess) return hip_fail("verify kernel launch", e);
+  }
+  return HSV_OK;
+}
+
+int hsv_verify_device(const uint8_t *d_pk, size_t pk_stride, const uint8_t *d_sig,
+                      size_t sig_stride, const uint8_t *d_msg, size_t msg_stride, size_t n,
+                      uint8_t *d_flags, void *stream) {
+  if (!d_flags && n) return fail(HSV_ERR_INVALID_ARG, "null d_flags");
+  return hsv_verify_device_bits(d_pk, pk_stride, d_sig, sig_stride, d_msg, msg_stride, n, d_flags,
+                                nullptr, stream);
+}
+
+double hsv_measure_mad_peak(void) {
+  if (ensure_init() != HSV_OK) return -1.0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return -1.0;
+  return hsv_launch_mad_peak(prop.multiProcessorCount);
+}
+
+}  // extern "C"

@@ -1,0 +1,168 @@
+// gfx950 kernels of the Ed25519 batch verifier.
+//
+//  hsv_verify_kernel   one verification per lane (see hsv_verify_core.hpp);
+//                      the [1..256]B Niels table (24 KiB) is staged in LDS
+//                      once per workgroup; inputs are read with 16-byte loads
+//                      straight from the caller's layout (strided records).
+//  hsv_mad_peak_kernel issue-rate probe of v_mad_u64_u32 for the roofline
+//                      denominator (bench.py reports against it).
+#include <hip/hip_runtime.h>
+
+#include "hsv_internal.h"
+#include "hsv_verify_core.hpp"
+
+namespace hsv {
+
+__device__ const uint32_t g_btable[256 * 24] = {
+#include "hsv_btable.inc"
+};
+
+struct LdsBTab {
+  const uint4 *base;
+  __device__ __forceinline__ ge_niels load(uint32_t idx) const {
+    const uint4 *e = base + idx * 6u;
+    ge_niels n;
+    const uint4 q0 = e[0], q1 = e[1], q2 = e[2], q3 = e[3], q4 = e[4], q5 = e[5];
+    n.ypx.v[0] = q0.x; n.ypx.v[1] = q0.y; n.ypx.v[2] = q0.z; n.ypx.v[3] = q0.w;
+    n.ypx.v[4] = q1.x; n.ypx.v[5] = q1.y; n.ypx.v[6] = q1.z; n.ypx.v[7] = q1.w;
+    n.ymx.v[0] = q2.x; n.ymx.v[1] = q2.y; n.ymx.v[2] = q2.z; n.ymx.v[3] = q2.w;
+    n.ymx.v[4] = q3.x; n.ymx.v[5] = q3.y; n.ymx.v[6] = q3.z; n.ymx.v[7] = q3.w;
+    n.xy2d.v[0] = q4.x; n.xy2d.v[1] = q4.y; n.xy2d.v[2] = q4.z; n.xy2d.v[3] = q4.w;
+    n.xy2d.v[4] = q5.x; n.xy2d.v[5] = q5.y; n.xy2d.v[6] = q5.z; n.xy2d.v[7] = q5.w;
+    return n;
+  }
+};
+
+constexpr int kBlock = 256;
+
+// One verification per lane.  WA/WB: window widths (hsv_verify_core.hpp);
+// WAVES: waves per SIMD requested from the register allocator (256 regs at 2,
+// 512 at 1).  The B table needs 2^(WB-1) entries x 96 B of LDS.
+template <int WA, int WB, int WAVES>
+__global__ void __launch_bounds__(kBlock, WAVES)
+hsv_verify_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
+                  const uint8_t *__restrict__ sig, uint64_t sig_stride,
+                  const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
+                  uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits) {
+  constexpr int kEntries = 1 << (WB - 1);
+  __shared__ uint4 lds_b[kEntries * 6];
+  {
+    const uint4 *src = reinterpret_cast<const uint4 *>(g_btable);
+    for (int i = threadIdx.x; i < kEntries * 6; i += kBlock) lds_b[i] = src[i];
+  }
+  __syncthreads();
+
+  const uint32_t idx = blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = idx < n;
+  const uint64_t li = valid ? idx : (uint64_t)(n - 1);
+
+  uint32_t pkw[8], sigw[16], msgw[8];
+  {
+    const uint4 *p = reinterpret_cast<const uint4 *>(pk + li * pk_stride);
+    const uint4 *s = reinterpret_cast<const uint4 *>(sig + li * sig_stride);
+    const uint4 *m = reinterpret_cast<const uint4 *>(msg + li * msg_stride);
+    const uint4 p0 = p[0], p1 = p[1];
+    const uint4 s0 = s[0], s1 = s[1], s2 = s[2], s3 = s[3];
+    const uint4 m0 = m[0], m1 = m[1];
+    pkw[0] = p0.x; pkw[1] = p0.y; pkw[2] = p0.z; pkw[3] = p0.w;
+    pkw[4] = p1.x; pkw[5] = p1.y; pkw[6] = p1.z; pkw[7] = p1.w;
+    sigw[0] = s0.x; sigw[1] = s0.y; sigw[2] = s0.z; sigw[3] = s0.w;
+    sigw[4] = s1.x; sigw[5] = s1.y; sigw[6] = s1.z; sigw[7] = s1.w;
+    sigw[8] = s2.x; sigw[9] = s2.y; sigw[10] = s2.z; sigw[11] = s2.w;
+    sigw[12] = s3.x; sigw[13] = s3.y; sigw[14] = s3.z; sigw[15] = s3.w;
+    msgw[0] = m0.x; msgw[1] = m0.y; msgw[2] = m0.z; msgw[3] = m0.w;
+    msgw[4] = m1.x; msgw[5] = m1.y; msgw[6] = m1.z; msgw[7] = m1.w;
+  }
+
+  LdsBTab bt{lds_b};
+  const uint32_t f = verify_one<WA, WB>(pkw, sigw, msgw, bt);
+
+  if (valid && flags_out) flags_out[idx] = (uint8_t)f;
+  if (strict_bits) {
+    const uint64_t mask = __ballot(valid && (f & kStrictOk));
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave_base = idx - lane;  // multiple of 64
+    const uint32_t nwords = (n + 31u) / 32u;
+    if (lane == 0) {
+      const uint32_t w0 = wave_base / 32u;
+      if (w0 < nwords) strict_bits[w0] = (uint32_t)mask;
+      if (w0 + 1 < nwords) strict_bits[w0 + 1] = (uint32_t)(mask >> 32);
+    }
+  }
+}
+
+// ---- v_mad_u64_u32 issue-rate probe -------------------------------------
+constexpr int kPeakChains = 8;
+constexpr int kPeakIters = 4096;
+
+__global__ void __launch_bounds__(256) hsv_mad_peak_kernel(uint32_t *sink, uint32_t seed) {
+  const uint32_t t = threadIdx.x + blockIdx.x * blockDim.x + seed;
+  uint64_t x[kPeakChains];
+  const uint32_t a = t | 1u, b = t * 3u + 7u;
+#pragma unroll
+  for (int c = 0; c < kPeakChains; ++c) x[c] = t + c;
+  for (int it = 0; it < kPeakIters; ++it) {
+#pragma unroll
+    for (int c = 0; c < kPeakChains; ++c)
+      asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(x[c]) : "v"(a), "v"(b) : "vcc");
+  }
+  uint32_t r = 0;
+#pragma unroll
+  for (int c = 0; c < kPeakChains; ++c) r ^= (uint32_t)(x[c] ^ (x[c] >> 32));
+  if (r == 0x9e3779b9u) sink[0] = r;
+}
+
+}  // namespace hsv
+
+// Kernel variants, selectable for measurement (hsv_set_variant / HSV_VARIANT).
+//   0: WA=2 WB=8  2 waves/SIMD (table of 2 cached points in registers)
+//   1: WA=3 WB=9  1 wave/SIMD
+//   2: WA=4 WB=8  1 wave/SIMD
+//   3: WA=3 WB=9  2 waves/SIMD (register-capped; spills if it does not fit)
+extern "C" int hsv_num_variants(void) { return 4; }
+
+extern "C" hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t pk_stride,
+                                        const uint8_t *sig, uint64_t sig_stride,
+                                        const uint8_t *msg, uint64_t msg_stride, uint32_t n,
+                                        uint8_t *flags_out, uint32_t *strict_bits,
+                                        hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const uint32_t grid = (n + hsv::kBlock - 1) / hsv::kBlock;
+#define HSV_LAUNCH(WA, WB, WV)                                                                \
+  hipLaunchKernelGGL((hsv::hsv_verify_kernel<WA, WB, WV>), dim3(grid), dim3(hsv::kBlock), 0, \
+                     stream, pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out,   \
+                     strict_bits)
+  switch (variant) {
+    case 0: HSV_LAUNCH(2, 8, 2); break;
+    case 1: HSV_LAUNCH(3, 9, 1); break;
+    case 2: HSV_LAUNCH(4, 8, 1); break;
+    case 3: HSV_LAUNCH(3, 9, 2); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef HSV_LAUNCH
+  return hipGetLastError();
+}
+
+extern "C" double hsv_launch_mad_peak(int device_cus) {
+  uint32_t *sink = nullptr;
+  if (hipMalloc(&sink, 64) != hipSuccess) return -1.0;
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  const int grid = device_cus * 8;
+  hipLaunchKernelGGL(hsv::hsv_mad_peak_kernel, dim3(grid), dim3(256), 0, 0, sink, 1u);
+  (void)hipDeviceSynchronize();
+  (void)hipEventRecord(e0, 0);
+  const int reps = 5;
+  for (int r = 0; r < reps; ++r)
+    hipLaunchKernelGGL(hsv::hsv_mad_peak_kernel, dim3(grid), dim3(256), 0, 0, sink, (uint32_t)r);
+  (void)hipEventRecord(e1, 0);
+  (void)hipEventSynchronize(e1);
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(sink);
+  const double macs = (double)reps * grid * 256.0 * hsv::kPeakIters * hsv::kPeakChains;
+  return ms > 0.f ? macs / (ms * 1e-3) : -1.0;
+}

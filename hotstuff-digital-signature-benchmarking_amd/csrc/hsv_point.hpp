@@ -1,0 +1,198 @@
+// Edwards25519 group operations for the verification kernels.
+//
+// Curve: -x^2 + y^2 = 1 + d x^2 y^2 over GF(2^255-19).
+// Representations:
+//   ge_ext    (X:Y:Z:T), x = X/Z, y = Y/Z, T = XY/Z           (accumulator)
+//   ge_cached (Y+X, Y-X, 2Z, 2dT)                            (variable-base table)
+//   ge_niels  (y+x, y-x, 2dxy), affine                       (fixed-base B table)
+// Formulas: Hisil-Wong-Carter-Dawson 2008 ("dbl-2008-hwcd", "add-2008-hwcd-3"),
+// both complete for a = -1 because d is a non-square, so the identity and
+// torsion points need no special cases (no divergence between lanes).
+//
+// Restated from curve25519-dalek 3.x:
+//   CompressedEdwardsY::decompress  -> ge_decompress
+//   EdwardsPoint::ct_eq (X1 Z2 == X2 Z1 && Y1 Z2 == Y2 Z1) -> ge_eq_affine
+//   EdwardsPoint::is_small_order ([8]P == O) -> y_is_small_order (equivalent:
+//   P is in E[8] iff its canonical y is one of the five y values of E[8]).
+#pragma once
+#include "hsv_field.hpp"
+
+namespace hsv {
+
+struct ge_ext {
+  fe X, Y, Z, T;
+};
+struct ge_cached {
+  fe YpX, YmX, Z2, T2d;
+};
+struct ge_niels {
+  fe ypx, ymx, xy2d;
+};
+
+HSV_INL ge_ext ge_identity() {
+  ge_ext r;
+  r.X = fe_small(0);
+  r.Y = fe_small(1);
+  r.Z = fe_small(1);
+  r.T = fe_small(0);
+  return r;
+}
+
+HSV_INL ge_cached ge_cached_identity() {
+  ge_cached r;
+  r.YpX = fe_small(1);
+  r.YmX = fe_small(1);
+  r.Z2 = fe_small(2);
+  r.T2d = fe_small(0);
+  return r;
+}
+
+HSV_INL ge_cached ge_to_cached(const ge_ext &p) {
+  ge_cached r;
+  r.YpX = fe_add(p.Y, p.X);
+  r.YmX = fe_sub(p.Y, p.X);
+  r.Z2 = fe_add(p.Z, p.Z);
+  r.T2d = fe_mul(p.T, fe_d2());
+  return r;
+}
+
+// 2P.  with_t = false skips T3 (saves one multiply when the next op is a doubling).
+template <bool with_t>
+HSV_INL ge_ext ge_dbl(const ge_ext &p) {
+  fe A = fe_sq(p.X);
+  fe B = fe_sq(p.Y);
+  fe C = fe_sq(p.Z);
+  C = fe_add(C, C);
+  fe H = fe_add(A, B);
+  fe xy = fe_add(p.X, p.Y);
+  fe E = fe_sub(H, fe_sq(xy));
+  fe G = fe_sub(A, B);
+  fe F = fe_add(C, G);
+  ge_ext r;
+  r.X = fe_mul(E, F);
+  r.Y = fe_mul(G, H);
+  r.Z = fe_mul(F, G);
+  if (with_t) r.T = fe_mul(E, H);
+  else r.T = fe_small(0);
+  return r;
+}
+
+// P + Q with Q cached.
+template <bool with_t>
+HSV_INL ge_ext ge_add_cached(const ge_ext &p, const ge_cached &q) {
+  fe A = fe_mul(fe_sub(p.Y, p.X), q.YmX);
+  fe B = fe_mul(fe_add(p.Y, p.X), q.YpX);
+  fe C = fe_mul(p.T, q.T2d);
+  fe D = fe_mul(p.Z, q.Z2);
+  fe E = fe_sub(B, A);
+  fe F = fe_sub(D, C);
+  fe G = fe_add(D, C);
+  fe H = fe_add(B, A);
+  ge_ext r;
+  r.X = fe_mul(E, F);
+  r.Y = fe_mul(G, H);
+  r.Z = fe_mul(F, G);
+  if (with_t) r.T = fe_mul(E, H);
+  else r.T = fe_small(0);
+  return r;
+}
+
+// P + Q with Q affine Niels (Z2 = 1).
+template <bool with_t>
+HSV_INL ge_ext ge_add_niels(const ge_ext &p, const ge_niels &q) {
+  fe A = fe_mul(fe_sub(p.Y, p.X), q.ymx);
+  fe B = fe_mul(fe_add(p.Y, p.X), q.ypx);
+  fe C = fe_mul(p.T, q.xy2d);
+  fe D = fe_add(p.Z, p.Z);
+  fe E = fe_sub(B, A);
+  fe F = fe_sub(D, C);
+  fe G = fe_add(D, C);
+  fe H = fe_add(B, A);
+  ge_ext r;
+  r.X = fe_mul(E, F);
+  r.Y = fe_mul(G, H);
+  r.Z = fe_mul(F, G);
+  if (with_t) r.T = fe_mul(E, H);
+  else r.T = fe_small(0);
+  return r;
+}
+
+// -Q for a cached point: swap Y+X / Y-X, negate 2dT.
+HSV_INL ge_cached ge_cached_cneg(const ge_cached &q, uint32_t neg) {
+  ge_cached r;
+  r.YpX = fe_select(q.YpX, q.YmX, neg);
+  r.YmX = fe_select(q.YmX, q.YpX, neg);
+  r.Z2 = q.Z2;
+  r.T2d = fe_select(q.T2d, fe_neg(q.T2d), neg);
+  return r;
+}
+
+HSV_INL ge_niels ge_niels_cneg(const ge_niels &q, uint32_t neg) {
+  ge_niels r;
+  r.ypx = fe_select(q.ypx, q.ymx, neg);
+  r.ymx = fe_select(q.ymx, q.ypx, neg);
+  r.xy2d = fe_select(q.xy2d, fe_neg(q.xy2d), neg);
+  return r;
+}
+
+// curve25519-dalek FieldElement::sqrt_ratio_i: returns was_nonzero_square
+// (true also for u == 0) and the non-negative root r.
+HSV_INL uint32_t fe_sqrt_ratio_i(const fe &u, const fe &v, fe &r_out) {
+  fe v3 = fe_mul(fe_sq(v), v);
+  fe v7 = fe_mul(fe_sq(v3), v);
+  fe r = fe_mul(fe_mul(u, v3), fe_pow22523(fe_mul(u, v7)));
+  fe check = fe_mul(v, fe_sq(r));
+  fe neg_u = fe_neg(u);
+  uint32_t correct = fe_eq(check, u);
+  uint32_t flipped = fe_eq(check, neg_u);
+  uint32_t flipped_i = fe_eq(check, fe_mul(neg_u, fe_sqrtm1()));
+  fe r_prime = fe_mul(r, fe_sqrtm1());
+  r = fe_select(r, r_prime, flipped | flipped_i);
+  r = fe_canon(r);
+  r = fe_select(r, fe_neg(r), r.v[0] & 1u);
+  r_out = fe_canon(r);
+  return correct | flipped;
+}
+
+// CompressedEdwardsY::decompress.  enc = 32 bytes as 8 little-endian words.
+// Returns 1 on success with the affine point (x, y); y keeps the (possibly
+// non-canonical) masked input value, x is canonical.
+HSV_INL uint32_t ge_decompress(const uint32_t enc[8], fe &x, fe &y) {
+  y = fe_from_words_masked(enc);
+  fe yy = fe_sq(y);
+  fe u = fe_sub(yy, fe_small(1));
+  fe v = fe_add(fe_mul(yy, fe_d()), fe_small(1));
+  uint32_t ok = fe_sqrt_ratio_i(u, v, x);
+  uint32_t sign = enc[7] >> 31;
+  x = fe_select(x, fe_neg(x), sign);  // -0 == 0 is accepted (no rejection)
+  return ok;
+}
+
+// [8]P == O  <=>  canonical y in {0, 1, p-1, y8, p-y8}  (the y values of E[8])
+HSV_INL uint32_t y_is_small_order(const fe &y) {
+  fe c = fe_canon(y);
+  const fe y8 = fe_const(0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du, 0xfa53202au,
+                         0xc6cc392cu, 0x77fdc74eu, 0x7a03ac92u);
+  const fe py8 = fe_const(0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u, 0x05acdfd5u,
+                          0x3933c6d3u, 0x880238b1u, 0x05fc536du);
+  const fe pm1 = fe_const(0xffffffecu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu,
+                          0xffffffffu, 0xffffffffu, 0x7fffffffu);
+  return fe_eq_canon_const(c, fe_small(0)) | fe_eq_canon_const(c, fe_small(1)) |
+         fe_eq_canon_const(c, pm1) | fe_eq_canon_const(c, y8) | fe_eq_canon_const(c, py8);
+}
+
+// Projective point == affine point (x, y): X == x Z and Y == y Z.
+HSV_INL uint32_t ge_eq_affine(const ge_ext &p, const fe &x, const fe &y) {
+  return fe_eq(p.X, fe_mul(x, p.Z)) & fe_eq(p.Y, fe_mul(y, p.Z));
+}
+
+// Compress (x, y) = (X/Z, Y/Z) -> 32 bytes as 8 words (host-side signing).
+HSV_INL void ge_compress(const ge_ext &p, uint32_t out[8]) {
+  fe zi = fe_invert(p.Z);
+  fe x = fe_canon(fe_mul(p.X, zi));
+  fe y = fe_canon(fe_mul(p.Y, zi));
+  for (int i = 0; i < 8; ++i) out[i] = y.v[i];
+  out[7] |= (x.v[0] & 1u) << 31;
+}
+
+}  // namespace hsv

@@ -1,0 +1,120 @@
+"""ctypes binding of libhsv.so (the C ABI declared in include/hsv.h).
+
+The shared library is built in-tree (``make`` in the package root, or
+``__graft_entry__.build()``) and is loaded from this directory only.  If it
+is missing, every entry point raises :class:`HsvLibraryError` -- there is no
+CPU fallback for verification.
+
+PyTorch, when importable, is imported *before* the library so that the HIP
+runtime (``libamdhip64.so.7``) already mapped by torch is the one libhsv
+binds to: one runtime per process, so device pointers from torch tensors can
+be passed to ``hsv_verify_device``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhsv.so")
+
+# flag bits (include/hsv.h)
+STRICT_OK = 0x01
+EQ_OK = 0x02
+PARSE_OK = 0x04
+SMALL_A = 0x08
+SMALL_R = 0x10
+S_OK = 0x20
+A_OK = 0x40
+R_OK = 0x80
+
+HSV_OK = 0
+ERRORS = {
+    -1: "HSV_ERR_NO_DEVICE",
+    -2: "HSV_ERR_HIP",
+    -3: "HSV_ERR_INVALID_ARG",
+    -4: "HSV_ERR_ALLOC",
+    -5: "HSV_ERR_ALIGN",
+}
+
+
+class HsvLibraryError(RuntimeError):
+    """libhsv.so missing, or an infrastructure error (never a signature rejection)."""
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def _declare(lib):
+    c_u8p = ctypes.c_void_p
+    sz = ctypes.c_size_t
+    sig = {
+        "hsv_init": (ctypes.c_int, [ctypes.c_int]),
+        "hsv_shutdown": (None, []),
+        "hsv_device_count": (ctypes.c_int, []),
+        "hsv_last_error": (ctypes.c_char_p, []),
+        "hsv_version": (ctypes.c_char_p, []),
+        "hsv_verify": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, sz, sz, c_u8p]),
+        "hsv_verify_strict": (ctypes.c_int, [c_u8p, c_u8p, c_u8p]),
+        "hsv_verify_batch": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, sz]),
+        "hsv_verify_batch_packed": (ctypes.c_int, [c_u8p, c_u8p, sz]),
+        "hsv_verify_device": (ctypes.c_int, [c_u8p, sz, c_u8p, sz, c_u8p, sz, sz, c_u8p, ctypes.c_void_p]),
+        "hsv_verify_device_bits": (ctypes.c_int, [c_u8p, sz, c_u8p, sz, c_u8p, sz, sz, c_u8p, c_u8p,
+                                                  ctypes.c_void_p]),
+        "hsv_public_key": (ctypes.c_int, [c_u8p, c_u8p]),
+        "hsv_sign": (ctypes.c_int, [c_u8p, c_u8p, sz, c_u8p]),
+        "hsv_sign_many": (ctypes.c_int, [c_u8p, c_u8p, sz, sz, c_u8p, c_u8p, ctypes.c_int]),
+        "hsv_measure_mad_peak": (ctypes.c_double, []),
+        "hsv_set_variant": (ctypes.c_int, [ctypes.c_int]),
+        "hsv_get_variant": (ctypes.c_int, []),
+        "hsv_num_variants": (ctypes.c_int, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def load(require: bool = True):
+    """Return the loaded CDLL (cached).  Raises HsvLibraryError if absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            if require:
+                raise HsvLibraryError(
+                    f"{LIB_PATH} not built: run `make` in {os.path.dirname(_HERE)} "
+                    "or __graft_entry__.build(); there is no CPU fallback")
+            return None
+        if os.environ.get("HSV_NO_TORCH") != "1":
+            try:
+                import torch  # noqa: F401  (share torch's HIP runtime)
+            except Exception:  # pragma: no cover - torch absent is fine
+                pass
+        lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        _declare(lib)
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str) -> int:
+    if rc < 0:
+        lib = load()
+        msg = lib.hsv_last_error().decode(errors="replace")
+        raise HsvLibraryError(f"{what}: {ERRORS.get(rc, rc)}: {msg}")
+    return rc
+
+
+def last_error() -> str:
+    return load().hsv_last_error().decode(errors="replace")
+
+
+def device_count() -> int:
+    return load().hsv_device_count()
+
+
+def version() -> str:
+    return load().hsv_version().decode()

@@ -1,0 +1,98 @@
+"""Array-level entry points over the C ABI (throughput path).
+
+* :func:`verify_flags`   host numpy arrays -> per-item flag bytes (hsv_verify)
+* :func:`verify_device`  device-resident torch tensors, stream-ordered
+                          (hsv_verify_device[_bits]); no synchronisation
+* :func:`sign_many`      bulk RFC 8032 signing on host threads (input synthesis)
+
+Record layout is the reference's byte layout: pk 32 B, sig 64 B (R || s),
+msg 32 B (a consensus Digest).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+
+def _ptr(a: np.ndarray):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def verify_flags(pk: np.ndarray, sig: np.ndarray, msg: np.ndarray) -> np.ndarray:
+    """pk (n,32) u8, sig (n,64) u8, msg (n,32) u8 or (32,) shared -> flags (n,) u8."""
+    pk = np.ascontiguousarray(pk, dtype=np.uint8).reshape(-1, 32)
+    sig = np.ascontiguousarray(sig, dtype=np.uint8).reshape(-1, 64)
+    n = pk.shape[0]
+    if sig.shape[0] != n:
+        raise ValueError("pk/sig length mismatch")
+    msg = np.ascontiguousarray(msg, dtype=np.uint8)
+    if msg.size == 32 and (msg.ndim == 1 or n != 1):
+        stride = 0
+    else:
+        msg = msg.reshape(-1, 32)
+        if msg.shape[0] != n:
+            raise ValueError("msg length mismatch")
+        stride = 32
+    out = np.zeros(n, dtype=np.uint8)
+    if n == 0:
+        return out
+    lib = _lib.load()
+    _lib.check(lib.hsv_verify(_ptr(pk), _ptr(sig), _ptr(msg), stride, n, _ptr(out)), "hsv_verify")
+    return out
+
+
+def verify_device(pk, sig, msg, flags=None, strict_bits=None, stream=None) -> None:
+    """Enqueue verification of device tensors (uint8, contiguous rows).
+
+    pk: (n,32), sig: (n,64), msg: (n,32) or (32,) shared; flags: (n,) uint8
+    and/or strict_bits: (ceil(n/32),) int32 outputs.  ``stream`` is a raw
+    hipStream_t handle (int) -- default: torch's current stream.
+    """
+    import torch
+
+    n = pk.shape[0]
+    if stream is None:
+        stream = torch.cuda.current_stream(pk.device).cuda_stream
+    msg_stride = 0 if msg.dim() == 1 else msg.stride(0)
+    lib = _lib.load()
+    rc = lib.hsv_verify_device_bits(
+        ctypes.c_void_p(pk.data_ptr()), pk.stride(0), ctypes.c_void_p(sig.data_ptr()), sig.stride(0),
+        ctypes.c_void_p(msg.data_ptr()), msg_stride, n,
+        ctypes.c_void_p(flags.data_ptr()) if flags is not None else None,
+        ctypes.c_void_p(strict_bits.data_ptr()) if strict_bits is not None else None,
+        ctypes.c_void_p(stream))
+    _lib.check(rc, "hsv_verify_device_bits")
+
+
+def sign_many(seeds: np.ndarray, msgs: np.ndarray, nthreads: int = 0):
+    """seeds (n,32), msgs (n,L) -> (pk (n,32), sig (n,64)) via host threads."""
+    seeds = np.ascontiguousarray(seeds, dtype=np.uint8).reshape(-1, 32)
+    n = seeds.shape[0]
+    msgs = np.ascontiguousarray(msgs, dtype=np.uint8).reshape(n, -1)
+    pk = np.zeros((n, 32), dtype=np.uint8)
+    sig = np.zeros((n, 64), dtype=np.uint8)
+    if n:
+        lib = _lib.load()
+        _lib.check(lib.hsv_sign_many(_ptr(seeds), _ptr(msgs), msgs.shape[1], n, _ptr(pk), _ptr(sig),
+                                     nthreads), "hsv_sign_many")
+    return pk, sig
+
+
+def measure_mad_peak() -> float:
+    """Measured v_mad_u64_u32 rate of the current device (MAC/s)."""
+    return float(_lib.load().hsv_measure_mad_peak())
+
+
+def set_variant(v: int) -> None:
+    _lib.check(_lib.load().hsv_set_variant(v), "hsv_set_variant")
+
+
+def get_variant() -> int:
+    return _lib.load().hsv_get_variant()
+
+
+def num_variants() -> int:
+    return _lib.load().hsv_num_variants()

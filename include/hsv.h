@@ -1,0 +1,124 @@
+/*
+ * hsv.h -- C ABI of the MI355X Ed25519 batch verifier (libhsv.so).
+ *
+ * Drop-in boundary for the reference's hot path, the `crypto` crate of
+ * mwaurawakati/hotstuff-digital-signature-benchmarking:
+ *
+ *   crypto::Signature::verify        crypto/src/lib.rs:204-208  -> hsv_verify_strict
+ *   crypto::Signature::verify_batch  crypto/src/lib.rs:210-223  -> hsv_verify_batch
+ *                                                                   hsv_verify_batch_packed
+ *   (batched strict API)                     -> hsv_verify
+ *   crypto::Signature::new           crypto/src/lib.rs:185-191  -> hsv_sign
+ *   crypto::generate_keypair         crypto/src/lib.rs:167-175  -> hsv_public_key
+ *
+ * Plain pointers and sizes only.  All inputs are borrowed for the duration of
+ * the call; the library never retains a caller pointer.  Every entry point is
+ * thread-safe (the reference calls verify from tokio worker threads,
+ * node/src/main.rs:16).  A return value < 0 is an infrastructure error (no
+ * GPU, HIP failure, bad argument) and NEVER encodes a signature rejection;
+ * there is no CPU fallback for verification -- callers decide what to do.
+ *
+ * Byte layouts are the reference's: PublicKey = 32 bytes (crypto/src/lib.rs:66),
+ * Signature = part1 (R, 32 B) || part2 (s, 32 B) as produced by flatten()
+ * (lib.rs:197-202), Digest = 32 bytes (lib.rs:22).
+ */
+#ifndef HSV_H_
+#define HSV_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- per-signature flag byte (hsv_verify / hsv_verify_device) ---------- */
+#define HSV_STRICT_OK 0x01u /* == ed25519-dalek PublicKey::verify_strict Ok   */
+#define HSV_EQ_OK 0x02u     /* PARSE_OK and [s]B == R + [k]A (cofactorless)    */
+#define HSV_PARSE_OK 0x04u  /* S_OK and A_OK and R_OK                          */
+#define HSV_SMALL_A 0x08u   /* A decodes and [8]A == O                         */
+#define HSV_SMALL_R 0x10u   /* R decodes and [8]R == O                         */
+#define HSV_S_OK 0x20u      /* s < l (canonical)                               */
+#define HSV_A_OK 0x40u      /* A decompresses                                  */
+#define HSV_R_OK 0x80u      /* R decompresses                                  */
+/* verify_batch item accepted  <=>  (flags & (HSV_PARSE_OK|HSV_EQ_OK)) == both  */
+
+/* ---- return codes ------------------------------------------------------- */
+#define HSV_OK 0
+#define HSV_ERR_NO_DEVICE (-1)
+#define HSV_ERR_HIP (-2)
+#define HSV_ERR_INVALID_ARG (-3)
+#define HSV_ERR_ALLOC (-4)
+#define HSV_ERR_ALIGN (-5)
+
+/* ---- lifecycle ---------------------------------------------------------- */
+/* Optional: contexts are created lazily on first use.  device = -1 selects
+ * every visible GPU (large host-buffer batches are then sharded across them
+ * by contiguous range).  Returns the number of devices initialised or < 0. */
+int hsv_init(int device);
+/* Release all device buffers, streams and pinned staging memory. */
+void hsv_shutdown(void);
+/* Number of visible HIP devices (0 when none). */
+int hsv_device_count(void);
+/* Human-readable description of the last error on the calling thread. */
+const char *hsv_last_error(void);
+/* Library version string. */
+const char *hsv_version(void);
+
+/* ---- verification, host buffers (synchronous) --------------------------- */
+/* Verify n independent triples.  pk: n*32 B, sig: n*64 B (R||s),
+ * msg: n*32 B when msg_stride == 32, or one shared 32-B digest when
+ * msg_stride == 0 (the QC case).  flags_out: n bytes (HSV_* bits above).
+ * n == 0 is valid and does nothing. */
+int hsv_verify(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, size_t msg_stride,
+               size_t n, uint8_t *flags_out);
+
+/* crypto::Signature::verify (crypto/src/lib.rs:204-208):
+ * returns 1 = Ok, 0 = Err(CryptoError), < 0 = infrastructure error. */
+int hsv_verify_strict(const uint8_t digest[32], const uint8_t pk[32], const uint8_t sig[64]);
+
+/* crypto::Signature::verify_batch (crypto/src/lib.rs:210-223), votes as
+ * parallel arrays pk[n*32], sig[n*64] over one shared digest:
+ * returns 1 = Ok, 0 = Err, < 0 = infrastructure error.  n == 0 -> 1 (Ok). */
+int hsv_verify_batch(const uint8_t digest[32], const uint8_t *pk, const uint8_t *sig, size_t n);
+
+/* Same, votes packed as n 96-byte records pk(32)||R(32)||s(32). */
+int hsv_verify_batch_packed(const uint8_t digest[32], const uint8_t *votes, size_t n);
+
+/* ---- verification, device-resident buffers (stream-ordered, async) ------ */
+/* Inputs already in HBM of the current device.  Record i reads
+ * pk + i*pk_stride (32 B), sig + i*sig_stride (64 B), msg + i*msg_stride
+ * (32 B; msg_stride may be 0).  Pointers and strides must be multiples of 16.
+ * Writes n flag bytes to d_flags.  stream: a hipStream_t (NULL = default).
+ * Does not synchronise. */
+int hsv_verify_device(const uint8_t *d_pk, size_t pk_stride, const uint8_t *d_sig,
+                      size_t sig_stride, const uint8_t *d_msg, size_t msg_stride, size_t n,
+                      uint8_t *d_flags, void *stream);
+
+/* As hsv_verify_device, additionally packing STRICT_OK bits into
+ * d_strict_bits[(n+31)/32] (bit i of word i/32 = item i).  Either output
+ * pointer may be NULL. */
+int hsv_verify_device_bits(const uint8_t *d_pk, size_t pk_stride, const uint8_t *d_sig,
+                           size_t sig_stride, const uint8_t *d_msg, size_t msg_stride, size_t n,
+                           uint8_t *d_flags, uint32_t *d_strict_bits, void *stream);
+
+/* ---- signing (host CPU; not on the hot path) ---------------------------- */
+/* Public key for a 32-byte secret seed (dalek Keypair from SecretKey). */
+int hsv_public_key(const uint8_t seed[32], uint8_t pk_out[32]);
+/* RFC 8032 deterministic signature (Signature::new). */
+int hsv_sign(const uint8_t seed[32], const uint8_t *msg, size_t msg_len, uint8_t sig_out[64]);
+/* Bulk: n seeds (n*32 B), n messages of msg_len bytes each; writes n public
+ * keys and n signatures.  nthreads <= 0 picks the hardware concurrency. */
+int hsv_sign_many(const uint8_t *seeds, const uint8_t *msgs, size_t msg_len, size_t n,
+                  uint8_t *pk_out, uint8_t *sig_out, int nthreads);
+
+/* ---- measurement helpers ------------------------------------------------ */
+/* Measured issue rate of v_mad_u64_u32 on the current device, in
+ * multiply-accumulates per second (the roofline denominator). */
+double hsv_measure_mad_peak(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HSV_H_ */

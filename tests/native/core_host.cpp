@@ -1,0 +1,127 @@
+// Host (CPU) build of the kernel's per-lane verification core, for unit tests
+// in this GPU-less container.  This is test infrastructure: the product
+// library never runs this code on the CPU.
+//
+// Reads lines "pk_hex sig_hex msg_hex" (32/64/32 bytes) on stdin and prints
+// the flag byte per line in hex.  With "--selftest-field" it instead prints
+// field/scalar/SHA results for random-ish inputs so Python can compare.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <cstdint>
+#include <string>
+#include <iostream>
+
+#include "hsv_verify_core.hpp"
+
+using namespace hsv;
+
+static const uint32_t kBTable[256 * 24] = {
+#include "hsv_btable.inc"
+};
+
+struct HostBTab {
+  ge_niels load(uint32_t idx) const {
+    ge_niels n;
+    const uint32_t *e = kBTable + 24 * idx;
+    for (int i = 0; i < 8; ++i) {
+      n.ypx.v[i] = e[i];
+      n.ymx.v[i] = e[8 + i];
+      n.xy2d.v[i] = e[16 + i];
+    }
+    return n;
+  }
+};
+
+static bool parse_hex(const std::string &s, uint8_t *out, size_t n) {
+  if (s.size() != 2 * n) return false;
+  for (size_t i = 0; i < n; ++i) {
+    unsigned v;
+    if (sscanf(s.c_str() + 2 * i, "%2x", &v) != 1) return false;
+    out[i] = (uint8_t)v;
+  }
+  return true;
+}
+
+static void to_words(const uint8_t *b, uint32_t *w, int n) {
+  for (int i = 0; i < n; ++i)
+    w[i] = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) |
+           ((uint32_t)b[4 * i + 3] << 24);
+}
+
+static void print_fe(const fe &a) {
+  fe c = fe_canon(a);
+  for (int i = 7; i >= 0; --i) printf("%08x", c.v[i]);
+}
+
+int main(int argc, char **argv) {
+  if (argc > 1 && strcmp(argv[1], "--field") == 0) {
+    // lines: op a_hex b_hex (big-endian hex of 256-bit values)
+    std::string op, as, bs;
+    while (std::cin >> op >> as >> bs) {
+      uint8_t ab[32], bb[32];
+      // big-endian hex -> little-endian bytes
+      uint8_t tmp[32];
+      parse_hex(as, tmp, 32);
+      for (int i = 0; i < 32; ++i) ab[i] = tmp[31 - i];
+      parse_hex(bs, tmp, 32);
+      for (int i = 0; i < 32; ++i) bb[i] = tmp[31 - i];
+      fe a, b;
+      to_words(ab, a.v, 8);
+      to_words(bb, b.v, 8);
+      fe r;
+      if (op == "mul") r = fe_mul(a, b);
+      else if (op == "sq") r = fe_sq(a);
+      else if (op == "add") r = fe_add(a, b);
+      else if (op == "sub") r = fe_sub(a, b);
+      else if (op == "inv") r = fe_invert(a);
+      else if (op == "pow") r = fe_pow22523(a);
+      else r = fe_canon(a);
+      print_fe(r);
+      printf("\n");
+    }
+    return 0;
+  }
+  if (argc > 1 && strcmp(argv[1], "--hashk") == 0) {
+    // lines: R A M hex -> k (big-endian hex)
+    std::string rs, as, ms;
+    while (std::cin >> rs >> as >> ms) {
+      uint8_t r[32], a[32], m[32];
+      parse_hex(rs, r, 32);
+      parse_hex(as, a, 32);
+      parse_hex(ms, m, 32);
+      uint32_t rw[8], aw[8], mw[8], h[16];
+      to_words(r, rw, 8);
+      to_words(a, aw, 8);
+      to_words(m, mw, 8);
+      sha512_96(rw, aw, mw, h);
+      sc k = sc_reduce512(h);
+      for (int i = 7; i >= 0; --i) printf("%08x", k.v[i]);
+      printf("\n");
+    }
+    return 0;
+  }
+  HostBTab bt;
+  int variant = (argc > 2 && strcmp(argv[1], "--variant") == 0) ? atoi(argv[2]) : 1;
+  std::string ps, ss, ms;
+  while (std::cin >> ps >> ss >> ms) {
+    uint8_t pk[32], sig[64], msg[32];
+    if (!parse_hex(ps, pk, 32) || !parse_hex(ss, sig, 64) || !parse_hex(ms, msg, 32)) {
+      printf("ERR\n");
+      continue;
+    }
+    uint32_t pw[8], sw[16], mw[8];
+    to_words(pk, pw, 8);
+    to_words(sig, sw, 16);
+    to_words(msg, mw, 8);
+    uint32_t f;
+    switch (variant) {
+      case 0: f = verify_one<2, 8>(pw, sw, mw, bt); break;
+      case 2: f = verify_one<4, 8>(pw, sw, mw, bt); break;
+      case 4: f = verify_one<3, 6>(pw, sw, mw, bt); break;
+      default: f = verify_one<3, 9>(pw, sw, mw, bt); break;
+    }
+    printf("%02x\n", f);
+  }
+  return 0;
+}
