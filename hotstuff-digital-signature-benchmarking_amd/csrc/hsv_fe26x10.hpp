@@ -1,0 +1,346 @@
+// GF(2^255 - 19), representation B: 10 limbs in radix 2^25.5.
+//
+// Limb i holds bits [off(i), off(i) + bits(i)) with bits = 26, 25, 26, 25, ...
+// and off = 0, 26, 51, 77, 102, 128, 153, 179, 204, 230 (25.5 * 10 = 255).
+//
+// Multiplication: column k of f*g is  sum_i f_i * G(k-i)  where the partner
+// limb is pre-scaled so the mod-p fold happens inside the product:
+//   * 19 when i + j >= 10   (2^255 == 19),
+//   * 2  when i and j are both odd (off(i) + off(j) = off(i+j) + 1).
+// Each column is a chain of 10 v_mad_u64_u32 accumulating in place into a
+// 64-bit register pair -- no carries inside the product, no extra adds.  One
+// carry chain per multiply (ref10 order, two interleaved chains) normalises
+// the 10 column sums.  Squaring uses the 55 distinct products.
+//
+// Operand classes (limb-wise upper bounds, R = 2^26 for even limbs / 2^25 for
+// odd limbs):
+//   R   output of mul / sq / carry / canon / from_words   (<= 1.004 R)
+//   S2  fe_add(R, R)                                      (<= 2.01 R)
+//   D   fe_sub(R-or-S2 minuend, R subtrahend) = a + 2p - b (<= 3.01 R, 4.01 R for an S2 minuend)
+// Rules (checked on the host with -DHSV_CHECK_BOUNDS):
+//   fe_sub(a, b)  b must be <= 2p limb-wise (class R)
+//   fe_mul(f, g)  g <= 3.368 R (19*g must fit 32 bits); column sums < 2^64,
+//                 which holds whenever class(f) * class(g) < 32
+//   fe_sq(f)      f <= 3.368 R
+//   fe_carry(x)   any x with limbs < 2^31 -> class R
+// Included by hsv_field.hpp when HSV_FE_RADIX == 26 (the default).
+#pragma once
+
+#if defined(HSV_CHECK_BOUNDS) && !defined(__HIP_DEVICE_COMPILE__)
+#include <cstdio>
+#include <cstdlib>
+#define HSV_BOUND(cond, what)                                           \
+  do {                                                                  \
+    if (!(cond)) {                                                      \
+      std::fprintf(stderr, "hsv bound violated: %s (%s:%d)\n", what,    \
+                   __FILE__, __LINE__);                                 \
+      std::abort();                                                     \
+    }                                                                   \
+  } while (0)
+#else
+#define HSV_BOUND(cond, what) ((void)0)
+#endif
+
+namespace hsv {
+
+struct fe {
+  uint32_t v[10];
+};
+
+constexpr int kFeLimbs = 10;
+
+HSV_INL constexpr int fe26_bits(int i) { return (i & 1) ? 25 : 26; }
+HSV_INL constexpr int fe26_off(int i) { return (i * 51 + 1) / 2; }
+HSV_INL constexpr uint32_t fe26_mask(int i) { return (i & 1) ? 0x1ffffffu : 0x3ffffffu; }
+// limbs of 2p: 2 * (2^26 - 19), 2 * (2^25 - 1), 2 * (2^26 - 1), ...
+HSV_INL constexpr uint32_t fe26_2p(int i) { return i == 0 ? 0x7ffffdau : ((i & 1) ? 0x3fffffeu : 0x7fffffeu); }
+// largest limb value g may hold in fe_mul (so that 19 * g fits 32 bits)
+HSV_INL constexpr uint32_t fe26_gmax(int i) { return (i & 1) ? 113025455u : 226050910u; }
+
+HSV_INL fe fe_small(uint32_t x) {
+  fe r;
+  r.v[0] = x;
+  HSV_UNROLL
+  for (int i = 1; i < 10; ++i) r.v[i] = 0;
+  return r;
+}
+
+// 8 little-endian words -> element; bit 255 masked (FieldElement::from_bytes).
+// The value may be >= p (non-canonical y is accepted and reduced implicitly).
+HSV_INL fe fe_from_words_masked(const uint32_t w[8]) {
+  fe r;
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) {
+    const int off = fe26_off(i), wi = off >> 5, sh = off & 31;
+    const uint32_t lo = w[wi];
+    const uint32_t hi = (wi + 1 < 8) ? w[wi + 1] : 0u;
+    const uint32_t x = sh ? ((lo >> sh) | (hi << ((32 - sh) & 31))) : lo;
+    r.v[i] = x & fe26_mask(i);
+  }
+  return r;
+}
+
+HSV_INL fe fe_add(const fe &a, const fe &b) {
+  fe r;
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) {
+    HSV_BOUND((uint64_t)a.v[i] + b.v[i] < (1ull << 32), "fe_add overflow");
+    r.v[i] = a.v[i] + b.v[i];
+  }
+  return r;
+}
+
+// a - b computed as a + 2p - b; b must be class R (<= 2p limb-wise).
+HSV_INL fe fe_sub(const fe &a, const fe &b) {
+  fe r;
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) {
+    HSV_BOUND(b.v[i] <= fe26_2p(i), "fe_sub subtrahend not reduced");
+    HSV_BOUND((uint64_t)a.v[i] + fe26_2p(i) < (1ull << 32), "fe_sub overflow");
+    r.v[i] = a.v[i] + fe26_2p(i) - b.v[i];
+  }
+  return r;
+}
+
+HSV_INL fe fe_neg(const fe &a) { return fe_sub(fe_small(0), a); }
+
+// --- carries ------------------------------------------------------------
+template <int I>
+HSV_INL void fe26_carry_step(uint32_t h[10]) {
+  const uint32_t c = h[I] >> fe26_bits(I);
+  h[I] &= fe26_mask(I);
+  h[I + 1] += c;
+}
+
+HSV_INL void fe26_carry_wrap(uint32_t h[10]) {
+  const uint32_t c = h[9] >> 25;
+  h[9] &= 0x1ffffffu;
+  h[0] += c * 19u;
+}
+
+// Any limbs < 2^31 -> class R (ref10 order: two interleaved chains).
+HSV_INL fe fe_carry(const fe &a) {
+  uint32_t h[10];
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) h[i] = a.v[i];
+  fe26_carry_step<0>(h);
+  fe26_carry_step<4>(h);
+  fe26_carry_step<1>(h);
+  fe26_carry_step<5>(h);
+  fe26_carry_step<2>(h);
+  fe26_carry_step<6>(h);
+  fe26_carry_step<3>(h);
+  fe26_carry_step<7>(h);
+  fe26_carry_step<4>(h);
+  fe26_carry_step<8>(h);
+  fe26_carry_wrap(h);
+  fe26_carry_step<0>(h);
+  fe r;
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) r.v[i] = h[i];
+  return r;
+}
+
+// 64-bit column sums -> class R.
+template <int I>
+HSV_INL void fe26_carry64_step(uint64_t h[10]) {
+  const uint64_t c = h[I] >> fe26_bits(I);
+  h[I] &= fe26_mask(I);
+  h[I + 1] += c;
+}
+
+HSV_INL fe fe26_carry64(uint64_t h[10]) {
+  fe26_carry64_step<0>(h);
+  fe26_carry64_step<4>(h);
+  fe26_carry64_step<1>(h);
+  fe26_carry64_step<5>(h);
+  fe26_carry64_step<2>(h);
+  fe26_carry64_step<6>(h);
+  fe26_carry64_step<3>(h);
+  fe26_carry64_step<7>(h);
+  fe26_carry64_step<4>(h);
+  fe26_carry64_step<8>(h);
+  {
+    const uint64_t c = h[9] >> 25;
+    h[9] &= 0x1ffffffu;
+    h[0] += c * 19u;
+  }
+  fe26_carry64_step<0>(h);
+  fe r;
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) r.v[i] = (uint32_t)h[i];
+  return r;
+}
+
+#if defined(HSV_CHECK_BOUNDS) && !defined(__HIP_DEVICE_COMPILE__)
+// exact column sums in 128-bit arithmetic: each must stay below 2^64
+HSV_INL void fe26_check_columns(const fe &f, const fe &g) {
+  for (int k = 0; k < 10; ++k) {
+    unsigned __int128 acc = 0;
+    for (int i = 0; i < 10; ++i) {
+      int j = k - i;
+      unsigned m = 1;
+      if (j < 0) { j += 10; m *= 19; }
+      if ((i & 1) && (j & 1)) m *= 2;
+      acc += (unsigned __int128)f.v[i] * g.v[j] * m;
+    }
+    HSV_BOUND((acc >> 64) == 0, "fe_mul column overflow");
+  }
+}
+#endif
+
+HSV_INL fe fe_mul(const fe &f, const fe &g) {
+  HSV_SCHED_FENCE();
+#if defined(HSV_CHECK_BOUNDS) && !defined(__HIP_DEVICE_COMPILE__)
+  for (int i = 0; i < 10; ++i) HSV_BOUND(g.v[i] <= fe26_gmax(i), "fe_mul g operand too large");
+  fe26_check_columns(f, g);
+#endif
+  uint32_t g19[10], f2[10];
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) {
+    g19[i] = g.v[i] * 19u;
+    f2[i] = (i & 1) ? f.v[i] * 2u : f.v[i];
+  }
+  uint64_t h[10];
+  HSV_UNROLL
+  for (int k = 0; k < 10; ++k) {
+    uint64_t acc = 0;
+    HSV_UNROLL
+    for (int i = 0; i < 10; ++i) {
+      int j = k - i;
+      const bool wrap = j < 0;
+      if (wrap) j += 10;
+      const uint32_t a = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+      const uint32_t b = wrap ? g19[j] : g.v[j];
+      acc += (uint64_t)a * b;
+    }
+    h[k] = acc;
+  }
+  fe r = fe26_carry64(h);
+  HSV_SCHED_FENCE();
+  return r;
+}
+
+HSV_INL fe fe_sq(const fe &f) {
+  HSV_SCHED_FENCE();
+#if defined(HSV_CHECK_BOUNDS) && !defined(__HIP_DEVICE_COMPILE__)
+  for (int i = 0; i < 10; ++i) HSV_BOUND(f.v[i] <= fe26_gmax(i), "fe_sq operand too large");
+  fe26_check_columns(f, f);
+#endif
+  uint32_t f2[10], f19[10], f38[10];
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) {
+    f2[i] = f.v[i] * 2u;
+    f19[i] = f.v[i] * 19u;
+    f38[i] = (i & 1) ? f.v[i] * 38u : 0u;  // only odd limbs are scaled by 38
+  }
+  uint64_t h[10];
+  HSV_UNROLL
+  for (int k = 0; k < 10; ++k) {
+    uint64_t acc = 0;
+    HSV_UNROLL
+    for (int i = 0; i < 10; ++i) {
+      HSV_UNROLL
+      for (int j = i; j < 10; ++j) {
+        if ((i + j) % 10 != k) continue;
+        const bool odd = (i & 1) && (j & 1);
+        const bool wrap = i + j >= 10;
+        const int m = (i != j ? 2 : 1) * (odd ? 2 : 1) * (wrap ? 19 : 1);
+        uint32_t a, b;
+        if (m == 1) { a = f.v[i]; b = f.v[j]; }
+        else if (m == 2) { a = f2[i]; b = f.v[j]; }
+        else if (m == 4) { a = f2[i]; b = f2[j]; }
+        else if (m == 19) { a = f.v[i]; b = f19[j]; }
+        else if (m == 38) {
+          if (i == j) { a = f.v[i]; b = f38[j]; }
+          else { a = f2[i]; b = f19[j]; }
+        } else { a = f2[i]; b = f38[j]; }  // m == 76
+        acc += (uint64_t)a * b;
+      }
+    }
+    h[k] = acc;
+  }
+  fe r = fe26_carry64(h);
+  HSV_SCHED_FENCE();
+  return r;
+}
+
+// Unique representative in [0, p), limbs exact.
+HSV_INL fe fe_canon(const fe &a) {
+  uint32_t h[10];
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) h[i] = a.v[i];
+  // three sequential passes: limbs exact, value < 2^255
+  HSV_UNROLL
+  for (int pass = 0; pass < 3; ++pass) {
+    fe26_carry_step<0>(h);
+    fe26_carry_step<1>(h);
+    fe26_carry_step<2>(h);
+    fe26_carry_step<3>(h);
+    fe26_carry_step<4>(h);
+    fe26_carry_step<5>(h);
+    fe26_carry_step<6>(h);
+    fe26_carry_step<7>(h);
+    fe26_carry_step<8>(h);
+    fe26_carry_wrap(h);
+  }
+  // q = [h >= p] = [h + 19 >= 2^255]
+  uint32_t q = (h[0] + 19u) >> 26;
+  HSV_UNROLL
+  for (int i = 1; i < 10; ++i) q = (h[i] + q) >> fe26_bits(i);
+  h[0] += 19u * q;
+  fe26_carry_step<0>(h);
+  fe26_carry_step<1>(h);
+  fe26_carry_step<2>(h);
+  fe26_carry_step<3>(h);
+  fe26_carry_step<4>(h);
+  fe26_carry_step<5>(h);
+  fe26_carry_step<6>(h);
+  fe26_carry_step<7>(h);
+  fe26_carry_step<8>(h);
+  h[9] &= 0x1ffffffu;  // drops 2^255 (subtracting p = 2^255 - 19 after the +19q)
+  fe r;
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) r.v[i] = h[i];
+  return r;
+}
+
+// canonical encoding as 8 little-endian words
+HSV_INL void fe_pack(const fe &a, uint32_t w[8]) {
+  const fe c = fe_canon(a);
+  HSV_UNROLL
+  for (int j = 0; j < 8; ++j) w[j] = 0;
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) {
+    const int off = fe26_off(i), wi = off >> 5, sh = off & 31;
+    w[wi] |= c.v[i] << sh;
+    if (sh + fe26_bits(i) > 32 && wi + 1 < 8) w[wi + 1] |= c.v[i] >> (32 - sh);
+  }
+}
+
+HSV_INL uint32_t fe_canon_low_bit(const fe &a) { return fe_canon(a).v[0] & 1u; }
+
+HSV_INL uint32_t fe_is_zero(const fe &a) {
+  const fe c = fe_canon(a);
+  uint32_t acc = 0;
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) acc |= c.v[i];
+  return acc == 0;
+}
+
+HSV_INL uint32_t fe_eq(const fe &a, const fe &b) {
+  const fe x = fe_canon(a), y = fe_canon(b);
+  uint32_t acc = 0;
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) acc |= x.v[i] ^ y.v[i];
+  return acc == 0;
+}
+
+HSV_INL fe fe_select(const fe &a, const fe &b, uint32_t take_b) {
+  fe r;
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) r.v[i] = take_b ? b.v[i] : a.v[i];
+  return r;
+}
+
+}  // namespace hsv

@@ -21,14 +21,16 @@ struct LdsBTab {
   const uint4 *base;
   __device__ __forceinline__ ge_niels load(uint32_t idx) const {
     const uint4 *e = base + idx * 6u;
+    uint32_t w[24];
+    HSV_UNROLL
+    for (int q = 0; q < 6; ++q) {
+      const uint4 v = e[q];
+      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
     ge_niels n;
-    const uint4 q0 = e[0], q1 = e[1], q2 = e[2], q3 = e[3], q4 = e[4], q5 = e[5];
-    n.ypx.v[0] = q0.x; n.ypx.v[1] = q0.y; n.ypx.v[2] = q0.z; n.ypx.v[3] = q0.w;
-    n.ypx.v[4] = q1.x; n.ypx.v[5] = q1.y; n.ypx.v[6] = q1.z; n.ypx.v[7] = q1.w;
-    n.ymx.v[0] = q2.x; n.ymx.v[1] = q2.y; n.ymx.v[2] = q2.z; n.ymx.v[3] = q2.w;
-    n.ymx.v[4] = q3.x; n.ymx.v[5] = q3.y; n.ymx.v[6] = q3.z; n.ymx.v[7] = q3.w;
-    n.xy2d.v[0] = q4.x; n.xy2d.v[1] = q4.y; n.xy2d.v[2] = q4.z; n.xy2d.v[3] = q4.w;
-    n.xy2d.v[4] = q5.x; n.xy2d.v[5] = q5.y; n.xy2d.v[6] = q5.z; n.xy2d.v[7] = q5.w;
+    n.ypx = fe_from_words_masked(w);
+    n.ymx = fe_from_words_masked(w + 8);
+    n.xy2d = fe_from_words_masked(w + 16);
     return n;
   }
 };

@@ -57,6 +57,8 @@ HSV_INL ge_cached ge_to_cached(const ge_ext &p) {
 }
 
 // 2P.  with_t = false skips T3 (saves one multiply when the next op is a doubling).
+// Operand classes (hsv_fe26x10.hpp): X, Y, Z in R.  H, C in S2, G in D,
+// E = H - S in 4R (used only as the unscaled f operand), F carried to R.
 template <bool with_t>
 HSV_INL ge_ext ge_dbl(const ge_ext &p) {
   fe A = fe_sq(p.X);
@@ -67,7 +69,7 @@ HSV_INL ge_ext ge_dbl(const ge_ext &p) {
   fe xy = fe_add(p.X, p.Y);
   fe E = fe_sub(H, fe_sq(xy));
   fe G = fe_sub(A, B);
-  fe F = fe_add(C, G);
+  fe F = fe_carry(fe_add(C, G));
   ge_ext r;
   r.X = fe_mul(E, F);
   r.Y = fe_mul(G, H);
@@ -77,7 +79,8 @@ HSV_INL ge_ext ge_dbl(const ge_ext &p) {
   return r;
 }
 
-// P + Q with Q cached.
+// P + Q with Q cached.  P in R; Q.YpX / Q.YmX in S2 / D (swapped when
+// negated), Q.Z2 in S2, Q.T2d in R (2R when negated).  E, F in D; G, H in S2.
 template <bool with_t>
 HSV_INL ge_ext ge_add_cached(const ge_ext &p, const ge_cached &q) {
   fe A = fe_mul(fe_sub(p.Y, p.X), q.YmX);
@@ -103,7 +106,7 @@ HSV_INL ge_ext ge_add_niels(const ge_ext &p, const ge_niels &q) {
   fe A = fe_mul(fe_sub(p.Y, p.X), q.ymx);
   fe B = fe_mul(fe_add(p.Y, p.X), q.ypx);
   fe C = fe_mul(p.T, q.xy2d);
-  fe D = fe_add(p.Z, p.Z);
+  fe D = fe_carry(fe_add(p.Z, p.Z));  // minuend and subtrahend below: keep it in R
   fe E = fe_sub(B, A);
   fe F = fe_sub(D, C);
   fe G = fe_add(D, C);
@@ -148,37 +151,47 @@ HSV_INL uint32_t fe_sqrt_ratio_i(const fe &u, const fe &v, fe &r_out) {
   uint32_t flipped_i = fe_eq(check, fe_mul(neg_u, fe_sqrtm1()));
   fe r_prime = fe_mul(r, fe_sqrtm1());
   r = fe_select(r, r_prime, flipped | flipped_i);
-  r = fe_canon(r);
-  r = fe_select(r, fe_neg(r), r.v[0] & 1u);
-  r_out = fe_canon(r);
+  const uint32_t neg = fe_is_negative(r);
+  r_out = fe_canon(fe_select(r, fe_neg(r), neg));
   return correct | flipped;
 }
 
 // CompressedEdwardsY::decompress.  enc = 32 bytes as 8 little-endian words.
 // Returns 1 on success with the affine point (x, y); y keeps the (possibly
-// non-canonical) masked input value, x is canonical.
+// non-canonical) masked input value (class R), x is canonical.
 HSV_INL uint32_t ge_decompress(const uint32_t enc[8], fe &x, fe &y) {
   y = fe_from_words_masked(enc);
   fe yy = fe_sq(y);
-  fe u = fe_sub(yy, fe_small(1));
+  fe u = fe_carry(fe_sub(yy, fe_small(1)));  // negated inside sqrt_ratio_i: keep in R
   fe v = fe_add(fe_mul(yy, fe_d()), fe_small(1));
   uint32_t ok = fe_sqrt_ratio_i(u, v, x);
   uint32_t sign = enc[7] >> 31;
-  x = fe_select(x, fe_neg(x), sign);  // -0 == 0 is accepted (no rejection)
+  x = fe_canon(fe_select(x, fe_neg(x), sign));  // -0 == 0 is accepted (no rejection)
   return ok;
 }
 
 // [8]P == O  <=>  canonical y in {0, 1, p-1, y8, p-y8}  (the y values of E[8])
 HSV_INL uint32_t y_is_small_order(const fe &y) {
-  fe c = fe_canon(y);
-  const fe y8 = fe_const(0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du, 0xfa53202au,
-                         0xc6cc392cu, 0x77fdc74eu, 0x7a03ac92u);
-  const fe py8 = fe_const(0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u, 0x05acdfd5u,
-                          0x3933c6d3u, 0x880238b1u, 0x05fc536du);
-  const fe pm1 = fe_const(0xffffffecu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu,
-                          0xffffffffu, 0xffffffffu, 0x7fffffffu);
-  return fe_eq_canon_const(c, fe_small(0)) | fe_eq_canon_const(c, fe_small(1)) |
-         fe_eq_canon_const(c, pm1) | fe_eq_canon_const(c, y8) | fe_eq_canon_const(c, py8);
+  uint32_t c[8];
+  fe_pack(y, c);
+  const uint32_t y8[8] = {0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du,
+                          0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0x7a03ac92u};
+  const uint32_t py8[8] = {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u,
+                           0x05acdfd5u, 0x3933c6d3u, 0x880238b1u, 0x05fc536du};
+  uint32_t hi = 0;  // OR of words 1..7
+  HSV_UNROLL
+  for (int i = 1; i < 8; ++i) hi |= c[i];
+  const uint32_t is0 = (hi == 0) & (c[0] == 0u);
+  const uint32_t is1 = (hi == 0) & (c[0] == 1u);
+  uint32_t pm1 = (c[0] == 0xffffffecu) & (c[7] == 0x7fffffffu);
+  uint32_t e8 = 1u, ep8 = 1u;
+  HSV_UNROLL
+  for (int i = 0; i < 8; ++i) {
+    if (i >= 1 && i <= 6) pm1 &= (c[i] == 0xffffffffu);
+    e8 &= (c[i] == y8[i]);
+    ep8 &= (c[i] == py8[i]);
+  }
+  return is0 | is1 | pm1 | e8 | ep8;
 }
 
 // Projective point == affine point (x, y): X == x Z and Y == y Z.
@@ -188,11 +201,10 @@ HSV_INL uint32_t ge_eq_affine(const ge_ext &p, const fe &x, const fe &y) {
 
 // Compress (x, y) = (X/Z, Y/Z) -> 32 bytes as 8 words (host-side signing).
 HSV_INL void ge_compress(const ge_ext &p, uint32_t out[8]) {
-  fe zi = fe_invert(p.Z);
-  fe x = fe_canon(fe_mul(p.X, zi));
-  fe y = fe_canon(fe_mul(p.Y, zi));
-  for (int i = 0; i < 8; ++i) out[i] = y.v[i];
-  out[7] |= (x.v[0] & 1u) << 31;
+  const fe zi = fe_invert(p.Z);
+  const uint32_t xneg = fe_is_negative(fe_mul(p.X, zi));
+  fe_pack(fe_mul(p.Y, zi), out);
+  out[7] |= xneg << 31;
 }
 
 }  // namespace hsv

@@ -163,6 +163,7 @@ int hsv_sign_many(const uint8_t *seeds, const uint8_t *msgs, size_t msg_len, siz
   if (!seeds || (!msgs && msg_len) || !sig_out) return HSV_ERR_INVALID_ARG;
   (void)fixed_base_table();
   unsigned nt = nthreads > 0 ? (unsigned)nthreads : std::thread::hardware_concurrency();
+  if (nthreads <= 0 && nt > 16) nt = 16;  // default: one GPU box's CPU share
   if (nt == 0) nt = 1;
   if ((size_t)nt > n) nt = (unsigned)n;
   std::vector<std::thread> th;

@@ -169,7 +169,7 @@ HSV_INL uint32_t verify_one(const uint32_t pk[8], const uint32_t sig[16], const 
   ge_cached tab[G::TS];
   {
     ge_ext p1;
-    p1.X = fe_neg(ax);
+    p1.X = fe_carry(fe_neg(ax));
     p1.Y = ay;
     p1.Z = fe_small(1);
     p1.T = fe_mul(p1.X, ay);

@@ -243,6 +243,13 @@ class SignatureService:
             if not fut.done():
                 fut.set_result(Signature.new(digest, self._secret))
 
+    async def close(self) -> None:
+        self._task.cancel()
+        try:
+            await self._task
+        except asyncio.CancelledError:
+            pass
+
     async def request_signature(self, digest: Digest) -> Signature:
         fut = asyncio.get_event_loop().create_future()
         await self._queue.put((digest, fut))

@@ -1,0 +1,147 @@
+"""Synthetic workloads for the BASELINE.json configs (no network, no datasets).
+
+C1  QC, 4-node committee: 3 votes over one digest
+C2  QC, n = 100: 67 votes over one digest
+C3  n = 1000: QC of 667 votes + TC of 667 timeouts, 5 % corrupted
+C4  2^20 independent (pk, digest, sig) triples, 5 % corrupted
+C5  2^24 triples sharded across GPUs (each rank builds its own shard)
+
+Keys are derived from seeded 32-byte secrets; messages are 32-byte digests
+shaped like the reference's (QC digest = SHA-512(hash || round_le)[..32],
+consensus/src/messages.rs:201-207; TC vote digest = SHA-512(round_le ||
+high_qc_round_le)[..32], messages.rs:307-311).  Corruptions are spread evenly
+over the kinds SURVEY 8(d) lists for C3/C4 (mixed-order keys are exercised by
+the golden vectors instead, since building them needs point arithmetic).
+"""
+from __future__ import annotations
+
+import hashlib
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from .verifier import sign_many
+
+L = 2**252 + 27742317777372353535851937790883648493
+
+# encodings of the 8 small-order points plus non-canonical aliases (13 in all)
+SMALL_ORDER_ENCODINGS = [bytes.fromhex(h) for h in (
+    "0100000000000000000000000000000000000000000000000000000000000000",
+    "eeffffffffffffffffffffffffffffffffffffffffffffffffffffffffffff7f",
+    "0100000000000000000000000000000000000000000000000000000000000080",
+    "26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05",
+    "0000000000000000000000000000000000000000000000000000000000000000",
+    "edffffffffffffffffffffffffffffffffffffffffffffffffffffffffffff7f",
+    "c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac037a",
+    "ecffffffffffffffffffffffffffffffffffffffffffffffffffffffffffff7f",
+    "ecffffffffffffffffffffffffffffffffffffffffffffffffffffffffffffff",
+    "c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac03fa",
+    "0000000000000000000000000000000000000000000000000000000000000080",
+    "edffffffffffffffffffffffffffffffffffffffffffffffffffffffffffffff",
+    "26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc85",
+)]
+# y = 2: (y^2 - 1) / (d y^2 + 1) is not a square -> does not decompress
+UNDECODABLE = bytes.fromhex("0200000000000000000000000000000000000000000000000000000000000000")
+
+CORRUPTIONS = ("flip_R", "flip_s", "s_plus_l", "wrong_digest", "undecodable_R", "small_order_R",
+               "small_order_A", "s_bit255")
+
+
+@dataclass
+class Workload:
+    pk: np.ndarray        # (n, 32) uint8
+    sig: np.ndarray       # (n, 64) uint8
+    msg: np.ndarray       # (n, 32) uint8, or (32,) for one shared digest
+    honest: np.ndarray    # (n,) bool: untouched honest signature
+    kind: np.ndarray = field(default=None)  # (n,) int8: -1 honest, else CORRUPTIONS index
+
+    @property
+    def n(self) -> int:
+        return self.pk.shape[0]
+
+
+def qc_digest(block_hash: bytes, round_: int) -> bytes:
+    return hashlib.sha512(block_hash + int(round_).to_bytes(8, "little")).digest()[:32]
+
+
+def tc_vote_digest(round_: int, high_qc_round: int) -> bytes:
+    return hashlib.sha512(int(round_).to_bytes(8, "little") + int(high_qc_round).to_bytes(8, "little")).digest()[:32]
+
+
+def corrupt(w: Workload, frac: float, rng: np.random.Generator) -> None:
+    """Corrupt round(frac * n) items in place, kinds spread evenly (seeded)."""
+    n = w.n
+    m = int(round(n * frac))
+    if m == 0:
+        return
+    idx = rng.choice(n, size=m, replace=False)
+    shared = w.msg.ndim == 1
+    if shared and m:
+        w.msg = np.repeat(w.msg[None, :], n, axis=0)
+    for j, i in enumerate(idx):
+        kind = j % len(CORRUPTIONS)
+        name = CORRUPTIONS[kind]
+        w.kind[i] = kind
+        w.honest[i] = False
+        if name == "flip_R":
+            b = int(rng.integers(0, 255))
+            w.sig[i, b // 8] ^= np.uint8(1 << (b % 8))
+        elif name == "flip_s":
+            b = int(rng.integers(0, 253))
+            w.sig[i, 32 + b // 8] ^= np.uint8(1 << (b % 8))
+        elif name == "s_plus_l":
+            s = int.from_bytes(bytes(w.sig[i, 32:]), "little") + L
+            w.sig[i, 32:] = np.frombuffer((s % 2**256).to_bytes(32, "little"), np.uint8)
+        elif name == "wrong_digest":
+            b = int(rng.integers(0, 256))
+            w.msg[i, b // 8] ^= np.uint8(1 << (b % 8))
+        elif name == "undecodable_R":
+            w.sig[i, :32] = np.frombuffer(UNDECODABLE, np.uint8)
+        elif name == "small_order_R":
+            w.sig[i, :32] = np.frombuffer(SMALL_ORDER_ENCODINGS[int(rng.integers(0, 13))], np.uint8)
+        elif name == "small_order_A":
+            w.pk[i] = np.frombuffer(SMALL_ORDER_ENCODINGS[int(rng.integers(0, 13))], np.uint8)
+        elif name == "s_bit255":
+            w.sig[i, 63] |= np.uint8(0x80)
+
+
+def independent_triples(n: int, seed: int, corrupt_frac: float = 0.05, nthreads: int = 0) -> Workload:
+    """C4 / C5 shard: n independent keys, digests and signatures."""
+    rng = np.random.default_rng(seed)
+    seeds = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    msgs = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    pk, sig = sign_many(seeds, msgs, nthreads)
+    w = Workload(pk, sig, msgs, np.ones(n, bool), np.full(n, -1, np.int8))
+    corrupt(w, corrupt_frac, rng)
+    return w
+
+
+def committee_seeds(n: int, seed: int = 0) -> np.ndarray:
+    rng = np.random.default_rng(1_000_003 + seed)
+    return rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+
+
+def qc_votes(committee: int, seed: int = 0, corrupt_frac: float = 0.0, round_: int = 1) -> Workload:
+    """A QC of 2f+1 = 2*committee//3 + 1 votes over one digest (C1/C2/C3)."""
+    quorum = 2 * committee // 3 + 1
+    seeds = committee_seeds(committee, seed)[:quorum]
+    digest = qc_digest(hashlib.sha512(b"block" + seed.to_bytes(4, "little")).digest()[:32], round_)
+    msgs = np.repeat(np.frombuffer(digest, np.uint8)[None, :], quorum, axis=0)
+    pk, sig = sign_many(seeds, msgs)
+    w = Workload(pk, sig, np.frombuffer(digest, np.uint8).copy(), np.ones(quorum, bool),
+                 np.full(quorum, -1, np.int8))
+    corrupt(w, corrupt_frac, np.random.default_rng(seed + 17))
+    return w
+
+
+def tc_votes(committee: int, seed: int = 0, corrupt_frac: float = 0.0, round_: int = 1000) -> Workload:
+    """A TC of 2f+1 timeouts, per-vote digests over high_qc_round in [round-10, round-1] (C3)."""
+    quorum = 2 * committee // 3 + 1
+    seeds = committee_seeds(committee, seed)[:quorum]
+    rng = np.random.default_rng(seed + 29)
+    hqc = rng.integers(round_ - 10, round_, size=quorum)
+    msgs = np.stack([np.frombuffer(tc_vote_digest(round_, int(h)), np.uint8) for h in hqc])
+    pk, sig = sign_many(seeds, msgs)
+    w = Workload(pk, sig, msgs, np.ones(quorum, bool), np.full(quorum, -1, np.int8))
+    corrupt(w, corrupt_frac, rng)
+    return w

@@ -108,7 +108,7 @@ int hsv_public_key(const uint8_t seed[32], uint8_t pk_out[32]);
 /* RFC 8032 deterministic signature (Signature::new). */
 int hsv_sign(const uint8_t seed[32], const uint8_t *msg, size_t msg_len, uint8_t sig_out[64]);
 /* Bulk: n seeds (n*32 B), n messages of msg_len bytes each; writes n public
- * keys and n signatures.  nthreads <= 0 picks the hardware concurrency. */
+ * keys and n signatures.  nthreads <= 0 picks min(hardware concurrency, 16). */
 int hsv_sign_many(const uint8_t *seeds, const uint8_t *msgs, size_t msg_len, size_t n,
                   uint8_t *pk_out, uint8_t *sig_out, int nthreads);
 

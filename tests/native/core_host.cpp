@@ -22,13 +22,11 @@ static const uint32_t kBTable[256 * 24] = {
 
 struct HostBTab {
   ge_niels load(uint32_t idx) const {
-    ge_niels n;
     const uint32_t *e = kBTable + 24 * idx;
-    for (int i = 0; i < 8; ++i) {
-      n.ypx.v[i] = e[i];
-      n.ymx.v[i] = e[8 + i];
-      n.xy2d.v[i] = e[16 + i];
-    }
+    ge_niels n;
+    n.ypx = fe_from_words_masked(e);
+    n.ymx = fe_from_words_masked(e + 8);
+    n.xy2d = fe_from_words_masked(e + 16);
     return n;
   }
 };
@@ -50,8 +48,9 @@ static void to_words(const uint8_t *b, uint32_t *w, int n) {
 }
 
 static void print_fe(const fe &a) {
-  fe c = fe_canon(a);
-  for (int i = 7; i >= 0; --i) printf("%08x", c.v[i]);
+  uint32_t w[8];
+  fe_pack(a, w);
+  for (int i = 7; i >= 0; --i) printf("%08x", w[i]);
 }
 
 int main(int argc, char **argv) {
@@ -66,9 +65,10 @@ int main(int argc, char **argv) {
       for (int i = 0; i < 32; ++i) ab[i] = tmp[31 - i];
       parse_hex(bs, tmp, 32);
       for (int i = 0; i < 32; ++i) bb[i] = tmp[31 - i];
-      fe a, b;
-      to_words(ab, a.v, 8);
-      to_words(bb, b.v, 8);
+      uint32_t aw[8], bw[8];
+      to_words(ab, aw, 8);
+      to_words(bb, bw, 8);
+      const fe a = fe_from_words_masked(aw), b = fe_from_words_masked(bw);
       fe r;
       if (op == "mul") r = fe_mul(a, b);
       else if (op == "sq") r = fe_sq(a);

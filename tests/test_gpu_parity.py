@@ -1,0 +1,259 @@
+"""GPU parity: the HIP path through the C ABI vs the oracle, bit-exact.
+
+Every comparison is on all 8 flag bits (include/hsv.h), not only the verdict.
+Sizes: golden fixtures (2193 records), the BASELINE configs C1-C3 exactly,
+2^15 random records against the C oracle, and the full C4 size (2^20) through
+the device-resident API, checked with size-independent properties plus an
+oracle-checked sample.
+"""
+import asyncio
+import threading
+
+import numpy as np
+import pytest
+
+import ed25519_ref as o
+from conftest import oracle_flags
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def api(hsv):
+    from hsverify import crypto, synth, verifier
+    return crypto, verifier, synth
+
+
+def test_golden_every_variant(api, golden):
+    _, verifier, _ = api
+    default = verifier.get_variant()
+    try:
+        for v in range(verifier.num_variants()):
+            verifier.set_variant(v)
+            got = verifier.verify_flags(golden["pk"], golden["sig"], golden["msg"])
+            bad = np.nonzero(got != golden["flags"])[0]
+            assert bad.size == 0, (v, [(golden["cases"][i], int(got[i]), int(golden["flags"][i])) for i in bad[:8]])
+    finally:
+        verifier.set_variant(default)
+
+
+# ---- the reference's own tests (crypto/src/tests/crypto_tests.rs) ---------
+def _keys(crypto):
+    return [crypto.generate_keypair(lambda n, s=s: s) for s in o.reference_key_seeds()]
+
+
+def test_verify_valid_signature(api):
+    crypto, _, _ = api
+    public_key, secret_key = _keys(crypto).pop()
+    digest = crypto.Digest(o.test_digest(b"Hello, world!"))
+    signature = crypto.Signature.new(digest, secret_key)
+    assert signature.verify(digest, public_key).is_ok()
+
+
+def test_verify_invalid_signature(api):
+    crypto, _, _ = api
+    public_key, secret_key = _keys(crypto).pop()
+    digest = crypto.Digest(o.test_digest(b"Hello, world!"))
+    signature = crypto.Signature.new(digest, secret_key)
+    bad = crypto.Digest(o.test_digest(b"Bad message!"))
+    assert signature.verify(bad, public_key).is_err()
+
+
+def test_verify_valid_batch(api):
+    crypto, _, _ = api
+    digest = crypto.Digest(o.test_digest(b"Hello, world!"))
+    keys = _keys(crypto)
+    signatures = []
+    for _ in range(3):
+        public_key, secret_key = keys.pop()
+        signatures.append((public_key, crypto.Signature.new(digest, secret_key)))
+    assert crypto.Signature.verify_batch(digest, signatures).is_ok()
+
+
+def test_verify_invalid_batch(api):
+    crypto, _, _ = api
+    digest = crypto.Digest(o.test_digest(b"Hello, world!"))
+    keys = _keys(crypto)
+    signatures = []
+    for _ in range(2):
+        public_key, secret_key = keys.pop()
+        signatures.append((public_key, crypto.Signature.new(digest, secret_key)))
+    public_key, _ = keys.pop()
+    signatures.append((public_key, crypto.Signature.default()))
+    assert crypto.Signature.verify_batch(digest, signatures).is_err()
+
+
+def test_signature_service(api):
+    crypto, _, _ = api
+    public_key, secret_key = _keys(crypto).pop()
+    digest = crypto.Digest(o.test_digest(b"Hello, world!"))
+
+    async def run():
+        service = crypto.SignatureService(secret_key)
+        try:
+            return await service.request_signature(digest)
+        finally:
+            await service.close()
+
+    loop = asyncio.new_event_loop()
+    signature = loop.run_until_complete(run())
+    loop.close()
+    assert signature.verify(digest, public_key).is_ok()
+
+
+def test_reference_fixture_file(api, reference_fixtures):
+    """Committed fixtures incl. consensus qc() (messages_tests.rs verify_valid_qc)."""
+    crypto, _, _ = api
+    for name, v in reference_fixtures["fixtures"].items():
+        d = crypto.Digest(bytes.fromhex(v["digest"]))
+        if v["op"] == "verify":
+            sig = bytes.fromhex(v["sig"])
+            r = crypto.Signature(sig[:32], sig[32:]).verify(d, crypto.PublicKey(bytes.fromhex(v["pk"])))
+        else:
+            votes = [(crypto.PublicKey(bytes.fromhex(p)), crypto.Signature(bytes.fromhex(s)[:32], bytes.fromhex(s)[32:]))
+                     for p, s in v["votes"]]
+            r = crypto.Signature.verify_batch(d, votes)
+        assert r.is_ok() == v["expect_ok"], name
+
+
+# ---- BASELINE configs C1-C3 ---------------------------------------------------
+@pytest.mark.parametrize("committee", [4, 100, 1000])
+def test_qc_configs(api, oracle_lib, committee):
+    crypto, verifier, synth = api
+    w = synth.qc_votes(committee, seed=committee)
+    votes = [(crypto.PublicKey(bytes(p)), crypto.Signature(bytes(s[:32]), bytes(s[32:]))) for p, s in zip(w.pk, w.sig)]
+    d = crypto.Digest(bytes(w.msg))
+    assert crypto.Signature.verify_batch(d, votes).is_ok()
+    # one bad vote anywhere makes the QC Err
+    bad = list(votes)
+    i = len(bad) // 2
+    s = bytearray(bad[i][1].flatten())
+    s[40] ^= 4
+    bad[i] = (bad[i][0], crypto.Signature(bytes(s[:32]), bytes(s[32:])))
+    assert crypto.Signature.verify_batch(d, bad).is_err()
+
+
+def test_c3_committee_1000_qc_and_tc_bit_exact(api, oracle_lib):
+    _, verifier, synth = api
+    for make in (synth.qc_votes, synth.tc_votes):
+        w = make(1000, seed=5, corrupt_frac=0.05)
+        msg = w.msg if w.msg.ndim == 2 else np.repeat(w.msg[None], w.n, 0)
+        got = verifier.verify_flags(w.pk, w.sig, msg)
+        exp = oracle_flags(oracle_lib, w.pk, w.sig, msg)
+        assert (got == exp).all()
+        assert (got[w.honest] & o.STRICT_OK).all()
+        assert not (got[~w.honest] & o.STRICT_OK).any()
+
+
+def test_random_batch_vs_c_oracle(api, oracle_lib):
+    _, verifier, synth = api
+    w = synth.independent_triples(1 << 15, seed=99, corrupt_frac=0.2)
+    got = verifier.verify_flags(w.pk, w.sig, w.msg)
+    exp = oracle_flags(oracle_lib, w.pk, w.sig, w.msg)
+    assert (got == exp).all()
+
+
+# ---- ragged sizes, shared digests, layouts ------------------------------------
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 256, 257, 1000])
+def test_ragged_sizes(api, golden, n):
+    _, verifier, _ = api
+    idx = np.arange(n) % len(golden["flags"])
+    got = verifier.verify_flags(golden["pk"][idx], golden["sig"][idx], golden["msg"][idx])
+    assert (got == golden["flags"][idx]).all()
+
+
+def test_shared_digest_matches_per_item(api, oracle_lib):
+    _, verifier, synth = api
+    w = synth.qc_votes(100, seed=3)          # one shared digest
+    assert w.msg.shape == (32,)
+    for i in range(0, w.n, 7):               # corrupt signatures, keep the digest shared
+        w.sig[i, (i * 13) % 64] ^= 1 << (i % 8)
+    shared = verifier.verify_flags(w.pk, w.sig, w.msg)
+    per_item = verifier.verify_flags(w.pk, w.sig, np.repeat(w.msg[None], w.n, 0))
+    assert (shared == per_item).all()
+    assert (shared == oracle_flags(oracle_lib, w.pk, w.sig, w.msg)).all()
+
+
+def test_packed_votes_layout(api, hsv):
+    crypto, verifier, synth = api
+    w = synth.qc_votes(100, seed=8)
+    packed = np.concatenate([w.pk, w.sig], axis=1).tobytes()
+    assert hsv.hsv_verify_batch_packed(bytes(w.msg), packed, w.n) == 1
+    assert hsv.hsv_verify_batch(bytes(w.msg), w.pk.tobytes(), w.sig.tobytes(), w.n) == 1
+    assert hsv.hsv_verify_batch(bytes(w.msg), None, None, 0) == 1
+
+
+def test_concurrent_host_calls(api, golden):
+    _, verifier, _ = api
+    results = [None] * 6
+
+    def work(k):
+        sl = slice(k * 300, k * 300 + 300)
+        results[k] = verifier.verify_flags(golden["pk"][sl], golden["sig"][sl], golden["msg"][sl])
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(6)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for k in range(6):
+        sl = slice(k * 300, k * 300 + 300)
+        assert (results[k] == golden["flags"][sl]).all()
+
+
+def test_device_api_flags_bits_and_strides(api, golden):
+    import torch
+    _, verifier, _ = api
+    dev = torch.device("cuda:0")
+    n = 1000
+    idx = np.arange(n) % len(golden["flags"])
+    exp = golden["flags"][idx]
+    pk = torch.from_numpy(golden["pk"][idx].copy()).to(dev)
+    sig = torch.from_numpy(golden["sig"][idx].copy()).to(dev)
+    msg = torch.from_numpy(golden["msg"][idx].copy()).to(dev)
+    flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+    bits = torch.zeros((n + 31) // 32, dtype=torch.int32, device=dev)
+    verifier.verify_device(pk, sig, msg, flags, bits)
+    torch.cuda.synchronize()
+    f = flags.cpu().numpy()
+    assert (f == exp).all()
+    b = bits.cpu().numpy().view(np.uint32)
+    unpacked = np.array([(b[i // 32] >> (i % 32)) & 1 for i in range(n)], np.uint8)
+    assert (unpacked == (exp & o.STRICT_OK)).all()
+    # packed 128-byte records (pk | sig | msg) read in place through strides
+    rec = torch.cat([pk, sig, msg], dim=1).contiguous()
+    flags2 = torch.zeros(n, dtype=torch.uint8, device=dev)
+    verifier.verify_device(rec[:, 0:32], rec[:, 32:96], rec[:, 96:128], flags2)
+    torch.cuda.synchronize()
+    assert (flags2.cpu().numpy() == exp).all()
+
+
+# ---- full C4 size: properties + oracle sample ----------------------------------
+def test_c4_full_size_properties(api, oracle_lib):
+    import torch
+    _, verifier, synth = api
+    n = 1 << 20
+    w = synth.independent_triples(n, seed=2024, corrupt_frac=0.05)
+    dev = torch.device("cuda:0")
+    pk, sig, msg = (torch.from_numpy(a).to(dev) for a in (w.pk, w.sig, w.msg))
+    flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+    verifier.verify_device(pk, sig, msg, flags)
+    torch.cuda.synchronize()
+    f = flags.cpu().numpy()
+    # honest signatures are all accepted; every corruption kind is rejected
+    assert (f[w.honest] & o.STRICT_OK).all()
+    assert not (f[~w.honest] & o.STRICT_OK).any()
+    kinds = {name: f[w.kind == k] for k, name in enumerate(synth.CORRUPTIONS)}
+    assert not (kinds["s_plus_l"] & o.S_OK).any() and not (kinds["s_bit255"] & o.S_OK).any()
+    assert not (kinds["undecodable_R"] & o.R_OK).any()
+    assert (kinds["small_order_R"] & o.SMALL_R).all() and (kinds["small_order_A"] & o.SMALL_A).all()
+    # idempotent: a second launch gives identical bytes
+    flags2 = torch.zeros_like(flags)
+    verifier.verify_device(pk, sig, msg, flags2)
+    torch.cuda.synchronize()
+    assert torch.equal(flags, flags2)
+    # oracle-checked sample across the whole range
+    rng = np.random.default_rng(1)
+    sample = np.sort(rng.choice(n, 8192, replace=False))
+    exp = oracle_flags(oracle_lib, w.pk[sample], w.sig[sample], w.msg[sample])
+    assert (f[sample] == exp).all()

@@ -1,0 +1,95 @@
+"""The kernel's per-lane arithmetic, compiled for the host, against the oracle.
+
+tests/native/core_host.cpp includes the same csrc/hsv_*.hpp headers the gfx950
+kernel is built from and runs them with g++ (test infrastructure; the product
+library never verifies on the CPU).  This pins field / scalar / SHA-512 /
+window-geometry logic in this GPU-less container before a GPU run.
+"""
+import os
+import random
+import subprocess
+
+import numpy as np
+import pytest
+
+import ed25519_ref as o
+from conftest import PKG, ROOT
+
+BIN = os.path.join(ROOT, "build", "core_host")
+
+
+@pytest.fixture(scope="module")
+def core_host():
+    os.makedirs(os.path.dirname(BIN), exist_ok=True)
+    src = os.path.join(ROOT, "tests", "native", "core_host.cpp")
+    # -DHSV_CHECK_BOUNDS: every field multiply asserts its operand classes and
+    # that all 64-bit column sums are exact (checked in 128-bit arithmetic)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wno-unknown-pragmas", "-DHSV_CHECK_BOUNDS",
+                    "-I", os.path.join(PKG, "csrc"), src, "-o", BIN], check=True)
+    return BIN
+
+
+def _run(binary, args, lines):
+    r = subprocess.run([binary] + args, input="\n".join(lines) + "\n", capture_output=True, text=True, check=True)
+    return r.stdout.split()
+
+
+def test_field_ops_match_python(core_host):
+    rnd = random.Random(5)
+    lines, exp = [], []
+    # operands enter through fe_from_words_masked (bit 255 dropped), so the domain is [0, 2^255)
+    specials = [0, 1, 2, o.P - 1, o.P, o.P + 1, 2**255 - 1, 2**255 - 20, 19, 38, 2**26 - 1, 2**51]
+    vals = specials + [rnd.randrange(2**255) for _ in range(120)]
+    for a in vals:
+        b = vals[rnd.randrange(len(vals))]
+        for op, v in (("mul", a * b), ("sq", a * a), ("add", a + b), ("sub", a - b), ("canon", a)):
+            lines.append(f"{op} {a:064x} {b:064x}")
+            exp.append(v % o.P)
+        lines.append(f"pow {a:064x} {b:064x}")
+        exp.append(pow(a, (o.P - 5) // 8, o.P))
+        if a % o.P:
+            lines.append(f"inv {a:064x} {b:064x}")
+            exp.append(pow(a, o.P - 2, o.P))
+    got = _run(core_host, ["--field"], lines)
+    bad = [lines[i] for i in range(len(exp)) if int(got[i], 16) != exp[i]]
+    assert not bad, bad[:5]
+
+
+def test_challenge_scalar_matches_python(core_host):
+    rnd = random.Random(6)
+    lines, exp = [], []
+    for _ in range(200):
+        r, a, m = rnd.randbytes(32), rnd.randbytes(32), rnd.randbytes(32)
+        lines.append(f"{r.hex()} {a.hex()} {m.hex()}")
+        exp.append(o.scalar_from_hash(o.sha512(r + a + m)))
+    # extreme hashes are covered by construction of Barrett; also all-ones inputs
+    lines.append(f"{'ff'*32} {'ff'*32} {'ff'*32}")
+    exp.append(o.scalar_from_hash(o.sha512(b"\xff" * 96)))
+    got = _run(core_host, ["--hashk"], lines)
+    assert [int(g, 16) for g in got] == exp
+
+
+@pytest.fixture(scope="module")
+def core_host32():
+    """The alternative radix-2^32 field representation (HSV_FE_RADIX=32)."""
+    out = BIN + "32"
+    src = os.path.join(ROOT, "tests", "native", "core_host.cpp")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wno-unknown-pragmas", "-DHSV_FE_RADIX=32",
+                    "-I", os.path.join(PKG, "csrc"), src, "-o", out], check=True)
+    return out
+
+
+def test_radix32_field_matches_golden(core_host32, golden):
+    lines = [f"{bytes(p).hex()} {bytes(s).hex()} {bytes(m).hex()}"
+             for p, s, m in zip(golden["pk"], golden["sig"], golden["msg"])]
+    got = np.array([int(x, 16) for x in _run(core_host32, ["--variant", "0"], lines)], np.uint8)
+    assert (got == golden["flags"]).all()
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 4])
+def test_verify_core_all_geometries_match_golden(core_host, golden, variant):
+    lines = [f"{bytes(p).hex()} {bytes(s).hex()} {bytes(m).hex()}"
+             for p, s, m in zip(golden["pk"], golden["sig"], golden["msg"])]
+    got = np.array([int(x, 16) for x in _run(core_host, ["--variant", str(variant)], lines)], np.uint8)
+    bad = np.nonzero(got != golden["flags"])[0]
+    assert bad.size == 0, [golden["cases"][i] for i in bad[:10]]
