@@ -27,7 +27,7 @@
 #include <hip/hip_runtime.h>
 #define HSV_INL __host__ __device__ __forceinline__
 #else
-#define HSV_INL static inline __attribute__((always_inline))
+#define HSV_INL static inline  // host test builds: let the compiler decide
 #endif
 
 #if defined(__HIP_DEVICE_COMPILE__)

@@ -18,15 +18,24 @@ from conftest import PKG, ROOT
 BIN = os.path.join(ROOT, "build", "core_host")
 
 
+def _build(out, *defines):
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    src = os.path.join(ROOT, "tests", "native", "core_host.cpp")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wno-unknown-pragmas", *defines,
+                    "-I", os.path.join(PKG, "csrc"), src, "-o", out], check=True)
+    return out
+
+
 @pytest.fixture(scope="module")
 def core_host():
-    os.makedirs(os.path.dirname(BIN), exist_ok=True)
-    src = os.path.join(ROOT, "tests", "native", "core_host.cpp")
-    # -DHSV_CHECK_BOUNDS: every field multiply asserts its operand classes and
-    # that all 64-bit column sums are exact (checked in 128-bit arithmetic)
-    subprocess.run(["g++", "-O2", "-std=c++17", "-Wno-unknown-pragmas", "-DHSV_CHECK_BOUNDS",
-                    "-I", os.path.join(PKG, "csrc"), src, "-o", BIN], check=True)
-    return BIN
+    return _build(BIN)
+
+
+@pytest.fixture(scope="module")
+def core_host_checked():
+    """-DHSV_CHECK_BOUNDS: every field multiply asserts its operand classes and
+    that all 64-bit column sums are exact (checked in 128-bit arithmetic)."""
+    return _build(BIN + "_checked", "-DHSV_CHECK_BOUNDS")
 
 
 def _run(binary, args, lines):
@@ -34,7 +43,8 @@ def _run(binary, args, lines):
     return r.stdout.split()
 
 
-def test_field_ops_match_python(core_host):
+def test_field_ops_match_python(core_host_checked):
+    core_host = core_host_checked
     rnd = random.Random(5)
     lines, exp = [], []
     # operands enter through fe_from_words_masked (bit 255 dropped), so the domain is [0, 2^255)
@@ -72,11 +82,18 @@ def test_challenge_scalar_matches_python(core_host):
 @pytest.fixture(scope="module")
 def core_host32():
     """The alternative radix-2^32 field representation (HSV_FE_RADIX=32)."""
-    out = BIN + "32"
-    src = os.path.join(ROOT, "tests", "native", "core_host.cpp")
-    subprocess.run(["g++", "-O2", "-std=c++17", "-Wno-unknown-pragmas", "-DHSV_FE_RADIX=32",
-                    "-I", os.path.join(PKG, "csrc"), src, "-o", out], check=True)
-    return out
+    return _build(BIN + "32", "-DHSV_FE_RADIX=32")
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_operand_bounds_hold_on_edge_and_sample(core_host_checked, golden, variant):
+    """Bound-checked build over every edge vector and a random sample: no field
+    operand leaves its class and no 64-bit column sum overflows."""
+    idx = list(range(golden["n_edge"])) + list(range(golden["n_edge"], len(golden["flags"]), 7))
+    lines = [f"{bytes(golden['pk'][i]).hex()} {bytes(golden['sig'][i]).hex()} {bytes(golden['msg'][i]).hex()}"
+             for i in idx]
+    got = np.array([int(x, 16) for x in _run(core_host_checked, ["--variant", str(variant)], lines)], np.uint8)
+    assert (got == golden["flags"][idx]).all()
 
 
 def test_radix32_field_matches_golden(core_host32, golden):
