@@ -181,6 +181,15 @@ def main():
     f = flags.cpu().numpy()
     honest_ok = bool((f[w.honest] & 1).all())
     corrupt_rejected = bool(not (f[~w.honest] & 1).any())
+    global_accepted = int((f & 1).sum())
+    if world > 1:
+        # host gather of the per-signature STRICT_OK bitmask (outside the timed region)
+        from hsverify import dist as hd
+        strict_all = hd.gather_strict(f, a.n * world)
+        honest_all = hd.gather_strict(w.honest.astype(np.uint8), a.n * world)
+        honest_ok = bool(strict_all[honest_all].all())
+        corrupt_rejected = bool(not strict_all[~honest_all].any())
+        global_accepted = int(strict_all.sum())
 
     if rank != 0:
         if world > 1:
@@ -222,7 +231,8 @@ def main():
             "work_per_verify": f"{WORK_MACS} u32 MACs (SURVEY 8(d)); {IO_BYTES} HBM bytes algorithmic",
             "kernel_ms": kernel_ms,
         },
-        "checks": {"honest_all_accepted": honest_ok, "corrupted_all_rejected": corrupt_rejected},
+        "checks": {"honest_all_accepted": honest_ok, "corrupted_all_rejected": corrupt_rejected,
+                   "strict_accepted_global": global_accepted},
     }
     if world == 1 and not a.no_cpu_baseline:
         threads = max(1, min(16, os.cpu_count() or 1))

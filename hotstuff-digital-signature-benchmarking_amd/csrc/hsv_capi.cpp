@@ -57,7 +57,7 @@ struct Global {
   bool inited = false;
   int ndev = 0;
   std::vector<DevCtx *> ctx;
-  std::atomic<int> variant{0};
+  std::atomic<int> variant{3};  // fastest measured: WA=3, WB=9, 2 waves/SIMD
 };
 
 Global &G() {
@@ -79,7 +79,10 @@ int ensure_init() {
     if (hipGetDeviceProperties(&prop, i) == hipSuccess) c->cus = prop.multiProcessorCount;
     g.ctx.push_back(c);
   }
-  if (const char *v = std::getenv("HSV_VARIANT")) g.variant = std::atoi(v);
+  if (const char *v = std::getenv("HSV_VARIANT")) {
+    const int vi = std::atoi(v);
+    if (vi >= 0 && vi < hsv_num_variants()) g.variant = vi;
+  }
   g.inited = true;
   return n > 0 ? HSV_OK : fail(HSV_ERR_NO_DEVICE, "no HIP device visible");
 }
