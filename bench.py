@@ -99,6 +99,61 @@ def qc_latency(reps):
     return res
 
 
+def committee_bench(reps, dev, n_votes=1 << 20):
+    """Committee key cache: QC latency for C2/C3 through the
+    cached tables, and throughput for 2^20 votes by a 1000-key committee."""
+    import torch
+    from hsverify import _lib, committee, synth
+    from hsverify.verifier import sign_many
+    lib = _lib.load()
+    res = {}
+    for size in (100, 1000):
+        w = synth.qc_votes(size, seed=size)
+        packed = np.concatenate([w.pk, w.sig], axis=1).tobytes()
+        digest = bytes(w.msg)
+        t0 = time.perf_counter()
+        c = committee.Committee(synth.qc_votes(size, seed=size).pk)
+        build_ms = (time.perf_counter() - t0) * 1e3
+        h = c._h
+        for _ in range(10):
+            assert lib.hsv_committee_verify_batch_packed(h, digest, packed, w.n) == 1
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            rc = lib.hsv_committee_verify_batch_packed(h, digest, packed, w.n)
+            ts.append(time.perf_counter() - t0)
+            assert rc == 1
+        ts = np.array(ts) * 1e3
+        res[f"qc_n{size}_votes{w.n}"] = {"p50_ms": float(np.percentile(ts, 50)), "p99_ms": float(np.percentile(ts, 99)),
+                                         "reps": reps, "table_build_ms": build_ms}
+        c.close()
+    # throughput: n_votes votes, each by one of 1000 members over its own digest
+    seeds = synth.committee_seeds(1000, 7)
+    rng = np.random.default_rng(7)
+    who = rng.integers(0, 1000, n_votes)
+    msgs = rng.integers(0, 256, (n_votes, 32), dtype=np.uint8)
+    pks, sigs = sign_many(seeds[who], msgs)
+    c = committee.Committee(sign_many(seeds, np.zeros((1000, 32), np.uint8))[0])
+    idx = torch.from_numpy(who.astype(np.int32)).to(dev)
+    sig = torch.from_numpy(sigs).to(dev)
+    msg = torch.from_numpy(msgs).to(dev)
+    flags = torch.zeros(n_votes, dtype=torch.uint8, device=dev)
+    c.verify_device(idx, sig, msg, flags)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    steps = 5
+    e0.record()
+    for _ in range(steps):
+        c.verify_device(idx, sig, msg, flags)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / steps
+    res["throughput"] = {"votes": n_votes, "committee": 1000, "kernel_ms": ms, "verif_per_s": n_votes / (ms * 1e-3),
+                         "all_accepted": bool((flags.cpu().numpy() & 1).all())}
+    c.close()
+    return res
+
+
 def qc_cpu(reps=3):
     """Single-core C port verify_batch rule for the n=1000 QC (667 votes)."""
     from hsverify import synth
@@ -239,6 +294,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(w, f, a.cpu_sample, threads)
     if not a.no_qc:
         out["qc_latency"] = qc_latency(a.qc_reps)
+        out["committee_cache"] = committee_bench(a.qc_reps, dev)
         if world == 1 and not a.no_cpu_baseline:
             out["qc_cpu_baseline"] = qc_cpu()
     print(json.dumps(out), flush=True)

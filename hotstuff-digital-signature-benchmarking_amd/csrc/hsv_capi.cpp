@@ -17,6 +17,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "hsv.h"
@@ -44,6 +45,7 @@ size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 struct DevCtx {
   int device = 0;
   int cus = 0;
+  uint32_t *d_btable = nullptr;  // comb table of B (committee path), built lazily
   hipStream_t stream = nullptr;
   uint8_t *d_buf = nullptr;
   size_t d_cap = 0;
@@ -207,7 +209,9 @@ void hsv_shutdown(void) {
       if (c->stream) (void)hipStreamDestroy(c->stream);
       if (c->d_buf) (void)hipFree(c->d_buf);
       if (c->h_buf) (void)hipHostFree(c->h_buf);
+      if (c->d_btable) (void)hipFree(c->d_btable);
     }
+    c->d_btable = nullptr;
     c->stream = nullptr;
     c->d_buf = c->h_buf = nullptr;
     c->d_cap = c->h_cap = 0;
@@ -310,6 +314,174 @@ double hsv_measure_mad_peak(void) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return -1.0;
   return hsv_launch_mad_peak(prop.multiProcessorCount);
+}
+
+}  // extern "C"
+
+// ---- committee key cache -------------------------------------------------
+namespace {
+
+const uint8_t kBasepointEncoding[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
+                                        0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
+                                        0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
+
+// comb table of B on this device (caller holds c.mu and has set the device)
+int ensure_btable(DevCtx &c) {
+  if (c.d_btable) return HSV_OK;
+  uint8_t *d_enc = nullptr;
+  uint32_t *d_tab = nullptr, *d_tmp = nullptr;
+  hipError_t e = hipMalloc(&d_enc, 32);
+  if (e == hipSuccess) e = hipMalloc(&d_tab, hsv_comb_table_bytes());
+  if (e == hipSuccess) e = hipMalloc(&d_tmp, hsv_comb_tmp_bytes(1));
+  if (e == hipSuccess) e = hipMemcpy(d_enc, kBasepointEncoding, 32, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hsv_launch_comb_build(d_enc, 1, 0, d_tab, d_tmp, nullptr, c.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c.stream);
+  if (d_enc) (void)hipFree(d_enc);
+  if (d_tmp) (void)hipFree(d_tmp);
+  if (e != hipSuccess) {
+    if (d_tab) (void)hipFree(d_tab);
+    return hip_fail("building the B comb table", e);
+  }
+  c.d_btable = d_tab;
+  return HSV_OK;
+}
+
+}  // namespace
+
+struct hsv_committee {
+  int device = 0;
+  uint32_t n = 0;
+  uint8_t *d_pks = nullptr;
+  uint8_t *d_kflags = nullptr;
+  uint32_t *d_tables = nullptr;
+  std::unordered_map<std::string, uint32_t> index;
+};
+
+extern "C" {
+
+int hsv_committee_create(const uint8_t *pks, size_t n, hsv_committee **out) {
+  if (!out || (!pks && n)) return fail(HSV_ERR_INVALID_ARG, "null argument");
+  if (n > (1u << 20)) return fail(HSV_ERR_INVALID_ARG, "committee too large");
+  int rc = ensure_init();
+  if (rc != HSV_OK) return rc;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= G().ndev) dev = 0;
+  DevCtx &c = *G().ctx[dev];
+  std::lock_guard<std::mutex> lk(c.mu);
+  rc = ctx_prepare(c, 0, 0);
+  if (rc != HSV_OK) return rc;
+  rc = ensure_btable(c);
+  if (rc != HSV_OK) return rc;
+  hsv_committee *cm = new hsv_committee();
+  cm->device = dev;
+  cm->n = (uint32_t)n;
+  for (size_t i = 0; i < n; ++i) cm->index.emplace(std::string(reinterpret_cast<const char *>(pks + 32 * i), 32), (uint32_t)i);
+  uint32_t *d_tmp = nullptr;
+  hipError_t e = hipSuccess;
+  if (n) {
+    e = hipMalloc(&cm->d_pks, n * 32);
+    if (e == hipSuccess) e = hipMalloc(&cm->d_kflags, n);
+    if (e == hipSuccess) e = hipMalloc(&cm->d_tables, n * hsv_comb_table_bytes());
+    if (e == hipSuccess) e = hipMalloc(&d_tmp, hsv_comb_tmp_bytes((uint32_t)n));
+    if (e == hipSuccess) e = hipMemcpy(cm->d_pks, pks, n * 32, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hsv_launch_comb_build(cm->d_pks, (uint32_t)n, 1, cm->d_tables, d_tmp, cm->d_kflags, c.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c.stream);
+    if (d_tmp) (void)hipFree(d_tmp);
+  }
+  if (e != hipSuccess) {
+    hsv_committee_destroy(cm);
+    return hip_fail("building committee tables", e);
+  }
+  *out = cm;
+  return HSV_OK;
+}
+
+void hsv_committee_destroy(hsv_committee *cm) {
+  if (!cm) return;
+  if (hipSetDevice(cm->device) == hipSuccess) {
+    if (cm->d_pks) (void)hipFree(cm->d_pks);
+    if (cm->d_kflags) (void)hipFree(cm->d_kflags);
+    if (cm->d_tables) (void)hipFree(cm->d_tables);
+  }
+  delete cm;
+}
+
+size_t hsv_committee_size(const hsv_committee *cm) { return cm ? cm->n : 0; }
+
+int64_t hsv_committee_index(const hsv_committee *cm, const uint8_t pk[32]) {
+  if (!cm || !pk) return -1;
+  auto it = cm->index.find(std::string(reinterpret_cast<const char *>(pk), 32));
+  return it == cm->index.end() ? -1 : (int64_t)it->second;
+}
+
+int hsv_committee_verify_device(const hsv_committee *cm, const uint32_t *d_key_idx, const uint8_t *d_sig,
+                                size_t sig_stride, const uint8_t *d_msg, size_t msg_stride, size_t m,
+                                uint8_t *d_flags, void *stream) {
+  if (m == 0) return HSV_OK;
+  if (!cm || !d_key_idx || !d_sig || !d_msg || !d_flags) return fail(HSV_ERR_INVALID_ARG, "null argument");
+  if (((reinterpret_cast<uintptr_t>(d_sig) | reinterpret_cast<uintptr_t>(d_msg) | sig_stride | msg_stride) & 15u) != 0)
+    return fail(HSV_ERR_ALIGN, "device pointers and strides must be multiples of 16");
+  if (sig_stride < 64 || (msg_stride != 0 && msg_stride < 32)) return fail(HSV_ERR_INVALID_ARG, "record strides overlap");
+  if (m > 0xffffffffu) return fail(HSV_ERR_INVALID_ARG, "batch too large");
+  DevCtx &c = *G().ctx[cm->device];
+  hipError_t e = hsv_launch_comb_verify(d_key_idx, d_sig, sig_stride, d_msg, msg_stride, (uint32_t)m, cm->d_pks,
+                                        cm->d_kflags, cm->n, cm->d_tables, c.d_btable, d_flags,
+                                        reinterpret_cast<hipStream_t>(stream));
+  return e == hipSuccess ? HSV_OK : hip_fail("committee verify launch", e);
+}
+
+int hsv_committee_verify(hsv_committee *cm, const uint32_t *key_idx, const uint8_t *sig, const uint8_t *msg,
+                         size_t msg_stride, size_t m, uint8_t *flags_out) {
+  if (m == 0) return HSV_OK;
+  if (!cm || !key_idx || !sig || !msg || !flags_out) return fail(HSV_ERR_INVALID_ARG, "null argument");
+  if (msg_stride != 0 && msg_stride != 32) return fail(HSV_ERR_INVALID_ARG, "msg_stride must be 0 or 32");
+  DevCtx &c = *G().ctx[cm->device];
+  std::lock_guard<std::mutex> lk(c.mu);
+  for (size_t base = 0; base < m; base += kChunk) {
+    const size_t k = std::min(kChunk, m - base);
+    const size_t idx_off = 0;
+    const size_t sig_off = round_up(k * 4, kAlign);
+    const size_t msg_off = sig_off + round_up(k * 64, kAlign);
+    const size_t msg_bytes = msg_stride ? k * 32 : 32;
+    const size_t flag_off = msg_off + round_up(msg_bytes, kAlign);
+    const size_t total = flag_off + round_up(k, kAlign);
+    int rc = ctx_prepare(c, total, total);
+    if (rc != HSV_OK) return rc;
+    uint8_t *h = c.h_buf;
+    std::memcpy(h + idx_off, key_idx + base, k * 4);
+    std::memcpy(h + sig_off, sig + base * 64, k * 64);
+    std::memcpy(h + msg_off, msg + base * msg_stride, msg_bytes);
+    hipError_t e = hipMemcpyAsync(c.d_buf, h, msg_off + msg_bytes, hipMemcpyHostToDevice, c.stream);
+    if (e != hipSuccess) return hip_fail("hipMemcpyAsync H2D", e);
+    e = hsv_launch_comb_verify(reinterpret_cast<const uint32_t *>(c.d_buf + idx_off), c.d_buf + sig_off, 64,
+                               c.d_buf + msg_off, msg_stride ? 32 : 0, (uint32_t)k, cm->d_pks, cm->d_kflags,
+                               cm->n, cm->d_tables, c.d_btable, c.d_buf + flag_off, c.stream);
+    if (e != hipSuccess) return hip_fail("committee verify launch", e);
+    e = hipMemcpyAsync(h + flag_off, c.d_buf + flag_off, k, hipMemcpyDeviceToHost, c.stream);
+    if (e != hipSuccess) return hip_fail("hipMemcpyAsync D2H", e);
+    e = hipStreamSynchronize(c.stream);
+    if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
+    std::memcpy(flags_out + base, h + flag_off, k);
+  }
+  return HSV_OK;
+}
+
+int hsv_committee_verify_batch_packed(hsv_committee *cm, const uint8_t digest[32], const uint8_t *votes, size_t m) {
+  if (m == 0) return 1;
+  if (!cm || !digest || !votes) return fail(HSV_ERR_INVALID_ARG, "null argument");
+  std::vector<uint32_t> idx(m);
+  std::vector<uint8_t> sigs(m * 64);
+  for (size_t i = 0; i < m; ++i) {
+    const int64_t k = hsv_committee_index(cm, votes + 96 * i);
+    if (k < 0) return hsv_verify_batch_packed(digest, votes, m);  // a non-member key: generic kernel
+    idx[i] = (uint32_t)k;
+    std::memcpy(sigs.data() + 64 * i, votes + 96 * i + 32, 64);
+  }
+  std::vector<uint8_t> flags(m);
+  int rc = hsv_committee_verify(cm, idx.data(), sigs.data(), digest, 0, m, flags.data());
+  if (rc != HSV_OK) return rc;
+  return batch_verdict(flags);
 }
 
 }  // extern "C"

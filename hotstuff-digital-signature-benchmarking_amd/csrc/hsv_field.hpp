@@ -26,8 +26,10 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define HSV_INL __host__ __device__ __forceinline__
+#define HSV_MEMBER __host__ __device__ __forceinline__
 #else
 #define HSV_INL static inline  // host test builds: let the compiler decide
+#define HSV_MEMBER inline
 #endif
 
 #if defined(__HIP_DEVICE_COMPILE__)

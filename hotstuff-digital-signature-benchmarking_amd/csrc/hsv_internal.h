@@ -20,3 +20,19 @@ double hsv_launch_mad_peak(int device_cus);
 #ifdef __cplusplus
 }
 #endif
+
+// ---- committee key cache (hsv_committee.hip) -----------------------------
+#ifdef __cplusplus
+extern "C" {
+#endif
+hipError_t hsv_launch_comb_build(const uint8_t *encs, uint32_t nkeys, uint32_t negate, uint32_t *tables,
+                                 uint32_t *tmp, uint8_t *key_flags, hipStream_t stream);
+hipError_t hsv_launch_comb_verify(const uint32_t *key_idx, const uint8_t *sig, uint64_t sig_stride,
+                                  const uint8_t *msg, uint64_t msg_stride, uint32_t m, const uint8_t *pks,
+                                  const uint8_t *key_flags, uint32_t nkeys, const uint32_t *tables,
+                                  const uint32_t *btable, uint8_t *flags_out, hipStream_t stream);
+uint64_t hsv_comb_table_bytes(void);
+uint64_t hsv_comb_tmp_bytes(uint32_t nkeys);
+#ifdef __cplusplus
+}
+#endif

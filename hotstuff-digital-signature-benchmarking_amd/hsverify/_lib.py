@@ -67,6 +67,14 @@ def _declare(lib):
         "hsv_sign": (ctypes.c_int, [c_u8p, c_u8p, sz, c_u8p]),
         "hsv_sign_many": (ctypes.c_int, [c_u8p, c_u8p, sz, sz, c_u8p, c_u8p, ctypes.c_int]),
         "hsv_measure_mad_peak": (ctypes.c_double, []),
+        "hsv_committee_create": (ctypes.c_int, [c_u8p, sz, ctypes.POINTER(ctypes.c_void_p)]),
+        "hsv_committee_destroy": (None, [ctypes.c_void_p]),
+        "hsv_committee_size": (sz, [ctypes.c_void_p]),
+        "hsv_committee_index": (ctypes.c_int64, [ctypes.c_void_p, c_u8p]),
+        "hsv_committee_verify": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, sz, sz, c_u8p]),
+        "hsv_committee_verify_batch_packed": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u8p, sz]),
+        "hsv_committee_verify_device": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u8p, sz, c_u8p, sz, sz, c_u8p,
+                                                       ctypes.c_void_p]),
         "hsv_set_variant": (ctypes.c_int, [ctypes.c_int]),
         "hsv_get_variant": (ctypes.c_int, []),
         "hsv_num_variants": (ctypes.c_int, []),

@@ -102,6 +102,34 @@ int hsv_verify_device_bits(const uint8_t *d_pk, size_t pk_stride, const uint8_t 
                            size_t sig_stride, const uint8_t *d_msg, size_t msg_stride, size_t n,
                            uint8_t *d_flags, uint32_t *d_strict_bits, void *stream);
 
+/* ---- committee key cache --------------------------- */
+/* Consensus keys are fixed per epoch (consensus/src/config.rs Committee).  A
+ * committee holds, in HBM of the device current at creation, a 384 KiB
+ * fixed-base comb table of -A per key; verifying a vote by a member then costs
+ * 64 mixed additions and no doublings.  Flags are identical to hsv_verify's
+ * (undecodable or small-order keys are accepted as members and reported
+ * through HSV_A_OK / HSV_SMALL_A exactly as the generic path does). */
+typedef struct hsv_committee hsv_committee;
+/* Build tables for n public keys (n*32 B). */
+int hsv_committee_create(const uint8_t *pks, size_t n, hsv_committee **out);
+void hsv_committee_destroy(hsv_committee *c);
+size_t hsv_committee_size(const hsv_committee *c);
+/* Index of pk in the committee, or -1. */
+int64_t hsv_committee_index(const hsv_committee *c, const uint8_t pk[32]);
+/* Votes by member index: key_idx[m], sig m*64 B, msg m*32 B (msg_stride 32)
+ * or one shared digest (msg_stride 0); flags_out m bytes.  An index >= n
+ * yields flags 0. */
+int hsv_committee_verify(hsv_committee *c, const uint32_t *key_idx, const uint8_t *sig,
+                         const uint8_t *msg, size_t msg_stride, size_t m, uint8_t *flags_out);
+/* crypto::Signature::verify_batch over votes packed pk||R||s: members use the
+ * cached tables, any other key the generic kernel.  1 = Ok, 0 = Err, < 0 error. */
+int hsv_committee_verify_batch_packed(hsv_committee *c, const uint8_t digest[32], const uint8_t *votes,
+                                      size_t m);
+/* Device-resident, stream-ordered form (device = the committee's). */
+int hsv_committee_verify_device(const hsv_committee *c, const uint32_t *d_key_idx, const uint8_t *d_sig,
+                                size_t sig_stride, const uint8_t *d_msg, size_t msg_stride, size_t m,
+                                uint8_t *d_flags, void *stream);
+
 /* ---- signing (host CPU; not on the hot path) ---------------------------- */
 /* Public key for a 32-byte secret seed (dalek Keypair from SecretKey). */
 int hsv_public_key(const uint8_t seed[32], uint8_t pk_out[32]);

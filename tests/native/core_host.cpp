@@ -12,7 +12,9 @@
 #include <string>
 #include <iostream>
 
+#include "hsv_comb.hpp"
 #include "hsv_verify_core.hpp"
+#include <vector>
 
 using namespace hsv;
 
@@ -98,6 +100,45 @@ int main(int argc, char **argv) {
       sc k = sc_reduce512(h);
       for (int i = 7; i >= 0; --i) printf("%08x", k.v[i]);
       printf("\n");
+    }
+    return 0;
+  }
+  if (argc > 1 && strcmp(argv[1], "--comb") == 0) {
+    // line 1: nkeys; then nkeys pk hex lines; then "idx sig_hex msg_hex" lines
+    size_t nkeys = 0;
+    std::cin >> nkeys;
+    std::vector<uint32_t> pkw(8 * nkeys), kflags(nkeys);
+    std::vector<uint32_t> tables(nkeys * kCombTableWords), btab(kCombTableWords), tmp(kCombEnt * 8);
+    auto build = [&](const uint32_t enc[8], uint32_t neg, uint32_t *tab) -> uint32_t {
+      fe x, y;
+      const uint32_t ok = ge_decompress(enc, x, y);
+      for (int j = 0; j < kCombPos; ++j)
+        comb_build_position(comb_position_base(x, y, neg, j), tab + (uint64_t)j * kCombEnt * kCombEntryWords,
+                            tmp.data());
+      return (ok ? kKeyAOk : 0u) | (ok && y_is_small_order(y) ? kKeySmallA : 0u);
+    };
+    const uint32_t bw[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
+                            0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
+    build(bw, 0, btab.data());
+    for (size_t k = 0; k < nkeys; ++k) {
+      std::string hs;
+      std::cin >> hs;
+      uint8_t b[32];
+      parse_hex(hs, b, 32);
+      to_words(b, &pkw[8 * k], 8);
+      kflags[k] = build(&pkw[8 * k], 1, tables.data() + k * kCombTableWords);
+    }
+    size_t idx;
+    std::string ss, ms;
+    while (std::cin >> idx >> ss >> ms) {
+      uint8_t sig[64], msg[32];
+      parse_hex(ss, sig, 64);
+      parse_hex(ms, msg, 32);
+      uint32_t sw[16], mw[8];
+      to_words(sig, sw, 16);
+      to_words(msg, mw, 8);
+      printf("%02x\n", verify_one_comb(&pkw[8 * idx], kflags[idx], sw, mw, tables.data() + idx * kCombTableWords,
+                                       btab.data()));
     }
     return 0;
   }

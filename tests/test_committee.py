@@ -1,0 +1,89 @@
+"""Committee key cache on the GPU: flags identical to the
+generic kernel and to the oracle, for every golden case and the C2/C3 shapes."""
+import numpy as np
+import pytest
+
+import ed25519_ref as o
+from conftest import oracle_flags
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mods(hsv):
+    from hsverify import committee, crypto, synth, verifier
+    return committee, crypto, synth, verifier
+
+
+def test_golden_through_committee(mods, golden):
+    committee, _, _, _ = mods
+    keys = sorted({bytes(k) for k in golden["pk"]})
+    kidx = {k: i for i, k in enumerate(keys)}
+    with committee.Committee(np.frombuffer(b"".join(keys), np.uint8).reshape(-1, 32)) as c:
+        assert len(c) == len(keys)
+        idx = np.array([kidx[bytes(k)] for k in golden["pk"]], np.uint32)
+        got = c.verify_flags(idx, golden["sig"], golden["msg"])
+        bad = np.nonzero(got != golden["flags"])[0]
+        assert bad.size == 0, [golden["cases"][i] for i in bad[:10]]
+        assert c.index(golden["pk"][0]) == kidx[bytes(golden["pk"][0])]
+        assert c.index(b"\x07" * 32) == -1
+
+
+def test_c3_qc_tc_committee_matches_generic_and_oracle(mods, oracle_lib):
+    committee, _, synth, verifier = mods
+    seeds = synth.committee_seeds(1000, 5)
+    from hsverify.verifier import sign_many
+    pks, _ = sign_many(seeds, np.zeros((1000, 32), np.uint8))
+    with committee.Committee(pks) as c:
+        for make in (synth.qc_votes, synth.tc_votes):
+            w = make(1000, seed=5, corrupt_frac=0.05)
+            msg = w.msg if w.msg.ndim == 2 else np.repeat(w.msg[None], w.n, 0)
+            idx = np.array([c.index(p) for p in w.pk], np.int64)
+            member = idx >= 0          # small_order_A corruptions replace the key
+            got = c.verify_flags(idx[member].astype(np.uint32), w.sig[member], msg[member])
+            generic = verifier.verify_flags(w.pk[member], w.sig[member], msg[member])
+            exp = oracle_flags(oracle_lib, w.pk[member], w.sig[member], msg[member])
+            assert (got == generic).all() and (got == exp).all()
+
+
+def test_qc_verify_batch_through_committee(mods):
+    committee, crypto, synth, _ = mods
+    w = synth.qc_votes(100, seed=100)
+    votes = [(crypto.PublicKey(bytes(p)), crypto.Signature(bytes(s[:32]), bytes(s[32:]))) for p, s in zip(w.pk, w.sig)]
+    d = crypto.Digest(bytes(w.msg))
+    with committee.Committee(w.pk) as c:
+        assert c.verify_batch(d, votes).is_ok()
+        bad = list(votes)
+        sg = bytearray(bad[3][1].flatten())
+        sg[33] ^= 1
+        bad[3] = (bad[3][0], crypto.Signature(bytes(sg[:32]), bytes(sg[32:])))
+        assert c.verify_batch(d, bad).is_err()
+        # a non-member key routes the batch through the generic kernel: still exact
+        other = synth.qc_votes(4, seed=9)
+        mixed = votes[:5] + [(crypto.PublicKey(bytes(other.pk[0])), crypto.Signature(bytes(other.sig[0][:32]), bytes(other.sig[0][32:])))]
+        assert c.verify_batch(d, mixed).is_err()   # other vote signs a different digest
+        assert c.verify_batch(d, []).is_ok()
+
+
+def test_invalid_member_index_yields_zero_flags(mods, golden):
+    committee, _, _, _ = mods
+    with committee.Committee(golden["pk"][:4]) as c:
+        f = c.verify_flags(np.array([0, 9, 2], np.uint32), golden["sig"][:3], golden["msg"][:3])
+        assert f[1] == 0                                   # index 9 is not a member
+        assert f[0] == golden["flags"][0] and f[2] == golden["flags"][2]
+
+
+def test_committee_device_api(mods, golden):
+    import torch
+    committee, _, _, _ = mods
+    keys = sorted({bytes(k) for k in golden["pk"]})
+    kidx = {k: i for i, k in enumerate(keys)}
+    dev = torch.device("cuda:0")
+    with committee.Committee(np.frombuffer(b"".join(keys), np.uint8).reshape(-1, 32)) as c:
+        idx = torch.tensor([kidx[bytes(k)] for k in golden["pk"]], dtype=torch.int32, device=dev)
+        sig = torch.from_numpy(golden["sig"].copy()).to(dev)
+        msg = torch.from_numpy(golden["msg"].copy()).to(dev)
+        flags = torch.zeros(len(golden["flags"]), dtype=torch.uint8, device=dev)
+        c.verify_device(idx, sig, msg, flags)
+        torch.cuda.synchronize()
+        assert (flags.cpu().numpy() == golden["flags"]).all()

@@ -110,3 +110,18 @@ def test_verify_core_all_geometries_match_golden(core_host, golden, variant):
     got = np.array([int(x, 16) for x in _run(core_host, ["--variant", str(variant)], lines)], np.uint8)
     bad = np.nonzero(got != golden["flags"])[0]
     assert bad.size == 0, [golden["cases"][i] for i in bad[:10]]
+
+
+def test_committee_comb_path_matches_golden(core_host, golden):
+    """Committee key cache (hsv_comb.hpp) built and verified on the host: every
+    distinct golden key becomes a member (undecodable, small-order, mixed-order
+    and non-canonical keys included); flags equal the generic path's."""
+    idx = list(range(golden["n_edge"])) + list(range(golden["n_edge"], len(golden["flags"]), 25))
+    keys = sorted({bytes(golden["pk"][i]).hex() for i in idx})
+    kidx = {k: n for n, k in enumerate(keys)}
+    lines = [str(len(keys))] + keys + [
+        f"{kidx[bytes(golden['pk'][i]).hex()]} {bytes(golden['sig'][i]).hex()} {bytes(golden['msg'][i]).hex()}"
+        for i in idx]
+    got = np.array([int(x, 16) for x in _run(core_host, ["--comb"], lines)], np.uint8)
+    bad = np.nonzero(got != golden["flags"][idx])[0]
+    assert bad.size == 0, [golden["cases"][idx[i]] for i in bad[:10]]
