@@ -1,0 +1,273 @@
+// Half-size scalars for the verification equation (lattice reduction in
+// dimension 2; cf. Pornin, "Optimized lattice basis reduction in dimension 2,
+// and fast Schnorr and EdDSA signature verification", 2020), adapted so the
+// result is EXACTLY dalek's cofactorless check, torsion included.
+//
+// The Ed25519 group E(F_p) is cyclic of order N = 8l.  For the challenge k we
+// find (c0, c1) in the lattice  { (x, y) : x == y k (mod N) }  with c1 odd and
+// |c0|, |c1| around 2^128.  Then [c1] is a bijection of E (gcd(c1, 8l) = 1:
+// c1 odd, 0 < c1 < l) and [x]P depends only on x mod N, so
+//    e = [s]B - R - [k]A = O   <=>   [c1]e = [(c1 s) mod l]B - [c1]R - [c0]A = O.
+// The right-hand side needs ~135 doublings instead of ~252.
+//
+// Reduction: Euclid on (N, k) with cofactors t (r == t k mod N, exact integer
+// arithmetic; quotients estimated in double precision and never over-
+// estimated, so every step is an exact unimodular update).  It stops at the
+// first remainder below 2^128, where |t| <= N / 2^128 < 2^128.  If that t is
+// even, the odd partner is the previous vector reduced against it (one
+// Gauss step).  Vectors longer than kLatMaxBits are reported as !ok and the
+// caller falls back to the full-length path (probability ~2^-14 per lane).
+#pragma once
+#include <math.h>
+
+#include "hsv_scalar.hpp"
+
+namespace hsv {
+
+constexpr int kLatMaxBits = 133;  // |c0|, |c1| < 2^133 (recoding over 135 bits needs < 2^133.78)
+
+struct LatOut {
+  uint32_t c0[5];  // |c0|, little-endian
+  uint32_t c1[5];  // c1 > 0, odd
+  uint32_t c0_neg; // c0 < 0
+  uint32_t ok;
+};
+
+#if defined(__HIP_DEVICE_COMPILE__)
+HSV_INL bool hsv_any(bool p) { return __any(p); }
+#else
+HSV_INL bool hsv_any(bool p) { return p; }
+#endif
+
+// value of an N-limb unsigned integer as a double (top 96 bits, then rounded)
+template <int N>
+HSV_INL double mp_to_double(const uint32_t x[N]) {
+  uint32_t a = 0, b = 0, c = 0;
+  int h = 0;
+  HSV_UNROLL
+  for (int i = 0; i < N; ++i) {
+    if (x[i] != 0) {
+      h = i;
+      a = x[i];
+      b = i >= 1 ? x[i - 1] : 0u;
+      c = i >= 2 ? x[i - 2] : 0u;
+    }
+  }
+  const double d = ((double)a * 4294967296.0 + (double)b) * 4294967296.0 + (double)c;
+  return ldexp(d, 32 * (h - 2));
+}
+
+// signed two's-complement N-limb value as a double
+template <int N>
+HSV_INL double mps_to_double(const uint32_t x[N]) {
+  const bool neg = (x[N - 1] >> 31) != 0;
+  uint32_t m[N];
+  uint64_t c = 1;
+  HSV_UNROLL
+  for (int i = 0; i < N; ++i) {
+    c += (uint64_t)(uint32_t)~x[i];
+    m[i] = neg ? (uint32_t)c : x[i];
+    c >>= 32;
+  }
+  const double d = mp_to_double<N>(m);
+  return neg ? -d : d;
+}
+
+// r = a - q*b  (q < 2^64), N limbs, modulo 2^(32N)
+template <int N>
+HSV_INL void mp_sub_mulq(uint32_t r[N], const uint32_t a[N], const uint32_t b[N], uint64_t q) {
+  const uint32_t ql = (uint32_t)q, qh = (uint32_t)(q >> 32);
+  uint32_t p[N];
+  uint64_t c = 0;
+  HSV_UNROLL
+  for (int i = 0; i < N; ++i) {
+    c = (uint64_t)b[i] * ql + (c >> 32);
+    p[i] = (uint32_t)c;
+  }
+  c = 0;
+  HSV_UNROLL
+  for (int i = 1; i < N; ++i) {
+    c = (uint64_t)b[i - 1] * qh + p[i] + (c >> 32);
+    p[i] = (uint32_t)c;
+  }
+  int64_t t = 0;
+  HSV_UNROLL
+  for (int i = 0; i < N; ++i) {
+    t += (int64_t)a[i] - (int64_t)p[i];
+    r[i] = (uint32_t)t;
+    t >>= 32;
+  }
+}
+
+// a < b (unsigned)
+template <int N>
+HSV_INL bool mp_lt(const uint32_t a[N], const uint32_t b[N]) {
+  int64_t t = 0;
+  HSV_UNROLL
+  for (int i = 0; i < N; ++i) {
+    t += (int64_t)a[i] - (int64_t)b[i];
+    t >>= 32;
+  }
+  return t != 0;
+}
+
+// |x| < 2^bits for a signed two's-complement N-limb value; writes |x| to mag (5 limbs)
+template <int N>
+HSV_INL bool mps_abs_fits(const uint32_t x[N], int bits, uint32_t mag[5], uint32_t &neg) {
+  neg = x[N - 1] >> 31;
+  uint32_t m[N];
+  uint64_t c = 1;
+  HSV_UNROLL
+  for (int i = 0; i < N; ++i) {
+    c += (uint64_t)(uint32_t)~x[i];
+    m[i] = neg ? (uint32_t)c : x[i];
+    c >>= 32;
+  }
+  bool fits = true;
+  HSV_UNROLL
+  for (int i = 0; i < N; ++i) {
+    const int lo = 32 * i;
+    if (lo >= bits) fits = fits && (m[i] == 0);
+    else if (lo + 32 > bits) fits = fits && ((m[i] >> (bits - lo)) == 0);
+  }
+  HSV_UNROLL
+  for (int i = 0; i < 5; ++i) mag[i] = i < N ? m[i] : 0u;
+  return fits;
+}
+
+HSV_INL LatOut lattice_reduce(const sc &k) {
+  // a = N = 8l, ta = 0;  b = k, tb = 1.   Invariant: a == ta*k, b == tb*k (mod N)
+  uint32_t a[8], b[8], ta[6], tb[6];
+  {
+    uint32_t l[8];
+    sc_l(l);
+    uint32_t c = 0;
+    HSV_UNROLL
+    for (int i = 0; i < 8; ++i) {
+      a[i] = (l[i] << 3) | c;
+      c = l[i] >> 29;
+      b[i] = k.v[i];
+    }
+  }
+  HSV_UNROLL
+  for (int i = 0; i < 6; ++i) {
+    ta[i] = 0;
+    tb[i] = i == 0 ? 1u : 0u;
+  }
+  // Euclid until b < 2^128 (all lanes of a wave iterate together)
+  HSV_NOUNROLL
+  for (int it = 0; it < 512; ++it) {
+    const bool active = (b[4] | b[5] | b[6] | b[7]) != 0;
+    if (!hsv_any(active)) break;
+    const double qd = mp_to_double<8>(a) / mp_to_double<8>(b);
+    double qf = floor(qd * (1.0 - 0x1p-40));
+    qf = qf < 1.0 ? 1.0 : (qf > 0x1p50 ? 0x1p50 : qf);
+    const uint64_t q = active ? (uint64_t)qf : 0u;
+    uint32_t r[8], tr[6];
+    mp_sub_mulq<8>(r, a, b, q);
+    mp_sub_mulq<6>(tr, ta, tb, q);
+    const bool swap = active && mp_lt<8>(r, b);
+    HSV_UNROLL
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t nb = swap ? r[i] : b[i];
+      a[i] = swap ? b[i] : (active ? r[i] : a[i]);
+      b[i] = nb;
+    }
+    HSV_UNROLL
+    for (int i = 0; i < 6; ++i) {
+      const uint32_t ntb = swap ? tr[i] : tb[i];
+      ta[i] = swap ? tb[i] : (active ? tr[i] : ta[i]);
+      tb[i] = ntb;
+    }
+  }
+  LatOut o;
+  o.ok = 0;
+  o.c0_neg = 0;
+  // candidate 1: (b, tb) when tb is odd:  c0 = b, c1 = tb
+  // candidate 2: (a, ta) - qv (b, tb), qv = round(<v,u>/<u,u>)  (ta odd when tb even)
+  const bool tb_odd = (tb[0] & 1u) != 0;
+  uint32_t c0[9], c1[6];
+  {
+    const double db = mp_to_double<8>(b), da = mp_to_double<8>(a);
+    const double dtb = mps_to_double<6>(tb), dta = mps_to_double<6>(ta);
+    const double den = db * db + dtb * dtb;
+    double qv = den > 0.0 ? rint((da * db + dta * dtb) / den) : 0.0;
+    const bool qv_ok = qv >= -0x1p50 && qv <= 0x1p50;
+    qv = qv_ok ? qv : 0.0;
+    // v - qv*u with qv >= 0, or v - |qv|*(-u) with qv < 0 (two's complement)
+    const bool qneg = qv < 0.0;
+    const uint64_t q = (uint64_t)(qneg ? -qv : qv);
+    uint32_t a9[9], b9[9], r9[9], tr[6], tbn[6];
+    {
+      uint64_t cb = 1, ct = 1;
+      HSV_UNROLL
+      for (int i = 0; i < 9; ++i) {
+        a9[i] = i < 8 ? a[i] : 0u;
+        const uint32_t bi = i < 8 ? b[i] : 0u;
+        cb += (uint64_t)(uint32_t)~bi;
+        b9[i] = qneg ? (uint32_t)cb : bi;
+        cb >>= 32;
+      }
+      HSV_UNROLL
+      for (int i = 0; i < 6; ++i) {
+        ct += (uint64_t)(uint32_t)~tb[i];
+        tbn[i] = qneg ? (uint32_t)ct : tb[i];
+        ct >>= 32;
+      }
+    }
+    mp_sub_mulq<9>(r9, a9, b9, q);
+    mp_sub_mulq<6>(tr, ta, tbn, q);
+    if (qneg) {  // candidate 1 needs the un-negated u
+      uint64_t cb = 1;
+      HSV_UNROLL
+      for (int i = 0; i < 9; ++i) {
+        cb += (uint64_t)(uint32_t)~b9[i];
+        b9[i] = (uint32_t)cb;
+        cb >>= 32;
+      }
+    }
+    HSV_UNROLL
+    for (int i = 0; i < 9; ++i) c0[i] = tb_odd ? b9[i] : r9[i];
+    HSV_UNROLL
+    for (int i = 0; i < 6; ++i) c1[i] = tb_odd ? tb[i] : tr[i];
+    if (!tb_odd && !qv_ok) c1[0] &= ~1u;  // force the "not ok" path below (even c1)
+  }
+  // normalise c1 > 0 (negate the whole vector), then bound-check
+  uint32_t n1;
+  uint32_t c1mag[5], c0mag[5];
+  const bool f1 = mps_abs_fits<6>(c1, kLatMaxBits, c1mag, n1);
+  uint32_t n0;
+  const bool f0 = mps_abs_fits<9>(c0, kLatMaxBits, c0mag, n0);
+  const bool odd = (c1[0] & 1u) != 0;
+  bool nz = false;
+  HSV_UNROLL
+  for (int i = 0; i < 5; ++i) nz = nz || (c1mag[i] != 0);
+  o.ok = (f0 && f1 && odd && nz) ? 1u : 0u;
+  o.c0_neg = n0 ^ n1;  // sign of c0 after making c1 positive
+  HSV_UNROLL
+  for (int i = 0; i < 5; ++i) {
+    o.c0[i] = c0mag[i];
+    o.c1[i] = c1mag[i];
+  }
+  return o;
+}
+
+// (c1 * s) mod l for c1 < 2^160 (5 limbs) and s < 2^256
+HSV_INL sc sc_mul_small(const uint32_t c1[5], const uint32_t s[8]) {
+  uint32_t t[16];
+  HSV_UNROLL
+  for (int i = 0; i < 16; ++i) t[i] = 0;
+  HSV_UNROLL
+  for (int i = 0; i < 5; ++i) {
+    uint64_t c = 0;
+    HSV_UNROLL
+    for (int j = 0; j < 8; ++j) {
+      c = (uint64_t)c1[i] * s[j] + t[i + j] + (c >> 32);
+      t[i + j] = (uint32_t)c;
+    }
+    t[i + 8] = (uint32_t)(c >> 32);
+  }
+  return sc_reduce512(t);
+}
+
+}  // namespace hsv

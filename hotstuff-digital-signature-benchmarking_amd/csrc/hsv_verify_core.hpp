@@ -25,6 +25,7 @@
 //   decompress R and compare projectively.
 #pragma once
 #include "hsv_field.hpp"
+#include "hsv_lattice.hpp"
 #include "hsv_point.hpp"
 #include "hsv_scalar.hpp"
 #include "hsv_sha512.hpp"
@@ -217,6 +218,141 @@ HSV_INL uint32_t verify_one(const uint32_t pk[8], const uint32_t sig[16], const 
   const uint32_t r_ok = ge_decompress(sig, rx, ry);
   const uint32_t small_r = r_ok & y_is_small_order(ry);
   const uint32_t same = ge_eq_affine(q, rx, ry);
+
+  const uint32_t parse_ok = s_ok & a_ok & r_ok;
+  const uint32_t eq_ok = parse_ok & same;
+  const uint32_t strict_ok = eq_ok & (small_a ^ 1u) & (small_r ^ 1u);
+  return (strict_ok ? kStrictOk : 0u) | (eq_ok ? kEqOk : 0u) | (parse_ok ? kParseOk : 0u) |
+         (small_a ? kSmallA : 0u) | (small_r ? kSmallR : 0u) | (s_ok ? kSOk : 0u) |
+         (a_ok ? kAOk : 0u) | (r_ok ? kROk : 0u);
+}
+
+// ---------------------------------------------------------------------------
+// Half-size-scalar verification (hsv_lattice.hpp).  With (c0, c1) from the
+// lattice reduction of k (c0 == c1 k mod 8l, c1 odd) and b = (c1 s) mod l,
+//   EQ_OK  <=>  [b]B + [c1](-R) + [|c0|](-sign(c0) A) == O.
+// One Straus chain of NW windows of WA bits runs both variable bases (tables of
+// [1..2^(WA-1)](-R) and of -sign(c0) A in registers) and the two fixed bases B
+// and B' = [2^SPLIT]B (b = b_lo + 2^SPLIT b_hi, LDS tables, WB-bit windows).
+// `fallback` is set when the reduction did not give short enough scalars; the
+// caller then uses verify_one for that lane (flags are exact either way).
+template <int WA, int WB>
+struct HalfWindows {
+  static_assert(WB % WA == 0, "B windows must align with A windows");
+  static constexpr int M = WB / WA;
+  static constexpr int NW = (WA == 3) ? 45 : (WA == 2 ? 68 : 34);  // 135 / 136 / 136 bits
+  static constexpr int BITS = NW * WA;
+  static constexpr int NBW = NW / M;
+  // b_lo < 2^(BITS-2): b_lo + C_WB (about 0.502 * 2^BITS) must not carry out of BITS bits
+  static constexpr int SPLIT = BITS - 2;
+  static constexpr int TS = 1 << (WA - 1);
+  static_assert(NW % M == 0 && NBW * WB == BITS, "window geometry");
+  static_assert(BITS <= 160 && (kLatMaxBits + 2) <= BITS, "scalar bound vs loop length");
+};
+
+// x (5 limbs) + C_w over nwin windows, shifted so the top window sits at the top of 5 limbs
+template <int W, int NWIN>
+HSV_INL void recode_top5(const uint32_t x[5], uint32_t out[5]) {
+  recode_add<5, W, NWIN>(x, 5, out);
+  limbs_shl_const<5, 160 - W * NWIN>(out);
+}
+
+template <int WA, int WB, class BTab, class BTab2>
+HSV_INL uint32_t verify_one_half(const uint32_t pk[8], const uint32_t sig[16], const uint32_t msg[8],
+                                 const BTab &btab, const BTab2 &btab2, bool &fallback) {
+  using G = HalfWindows<WA, WB>;
+  const uint32_t s_ok = sc_is_canonical(sig + 8);
+  uint32_t h[16];
+  sha512_96(sig, pk, msg, h);
+  const sc k = sc_reduce512(h);
+
+  fe ax, ay, rx, ry;
+  const uint32_t a_ok = ge_decompress(pk, ax, ay);
+  const uint32_t small_a = a_ok & y_is_small_order(ay);
+  const uint32_t r_ok = ge_decompress(sig, rx, ry);
+  const uint32_t small_r = r_ok & y_is_small_order(ry);
+
+  const LatOut lat = lattice_reduce(k);
+  fallback = !lat.ok;
+  const sc b = sc_mul_small(lat.c1, sig + 8);  // (c1 s) mod l
+
+  // b = b_lo + 2^SPLIT b_hi
+  uint32_t blo[5], bhi[5];
+  HSV_UNROLL
+  for (int i = 0; i < 5; ++i) {
+    const int lo = 32 * i;
+    blo[i] = lo + 32 <= G::SPLIT ? b.v[i] : (lo < G::SPLIT ? (b.v[i] & ((1u << (G::SPLIT - lo)) - 1u)) : 0u);
+  }
+  {
+    constexpr int W = G::SPLIT / 32, S = G::SPLIT % 32;
+    HSV_UNROLL
+    for (int i = 0; i < 5; ++i) {
+      const uint32_t x0 = (i + W < 8) ? b.v[i + W] : 0u;
+      const uint32_t x1 = (i + W + 1 < 8) ? b.v[i + W + 1] : 0u;
+      bhi[i] = S ? ((x0 >> S) | (x1 << ((32 - S) & 31))) : x0;
+    }
+  }
+
+  // variable-base tables: [1..TS](-R) and [1..TS](-sign(c0) A)
+  ge_cached tabr[G::TS], taba[G::TS];
+  {
+    ge_ext p1;
+    p1.X = fe_carry(fe_neg(rx));
+    p1.Y = ry;
+    p1.Z = fe_small(1);
+    p1.T = fe_mul(p1.X, p1.Y);
+    tabr[0] = ge_to_cached(p1);
+    if (G::TS >= 2) {
+      ge_ext p2 = ge_dbl<true>(p1);
+      tabr[1] = ge_to_cached(p2);
+      build_table_tail<3, G::TS>(p2, tabr);
+    }
+  }
+  {
+    ge_ext p1;
+    p1.X = fe_carry(fe_select(fe_neg(ax), ax, lat.c0_neg));
+    p1.Y = ay;
+    p1.Z = fe_small(1);
+    p1.T = fe_mul(p1.X, p1.Y);
+    taba[0] = ge_to_cached(p1);
+    if (G::TS >= 2) {
+      ge_ext p2 = ge_dbl<true>(p1);
+      taba[1] = ge_to_cached(p2);
+      build_table_tail<3, G::TS>(p2, taba);
+    }
+  }
+
+  uint32_t dr[5], da[5], dlo[5], dhi[5];
+  recode_top5<WA, G::NW>(lat.c1, dr);
+  recode_top5<WA, G::NW>(lat.c0, da);
+  recode_top5<WB, G::NBW>(blo, dlo);
+  recode_top5<WB, G::NBW>(bhi, dhi);
+
+  ge_ext q = ge_identity();
+  HSV_NOUNROLL
+  for (int i = G::NW - 1; i >= 0; --i) {
+    if (i != G::NW - 1) {
+      HSV_UNROLL
+      for (int j = 0; j < WA - 1; ++j) q = ge_dbl<false>(q);
+      q = ge_dbl<true>(q);
+    }
+    const uint32_t cr = dr[4] >> (32 - WA), ca = da[4] >> (32 - WA);
+    limbs_shl<5>(dr, WA);
+    limbs_shl<5>(da, WA);
+    q = ge_add_cached<true>(q, select_cached<G::TS>(tabr, cr));
+    if (i % G::M == 0) {
+      q = ge_add_cached<true>(q, select_cached<G::TS>(taba, ca));
+      const uint32_t cl = dlo[4] >> (32 - WB), ch = dhi[4] >> (32 - WB);
+      limbs_shl<5>(dlo, WB);
+      limbs_shl<5>(dhi, WB);
+      q = ge_add_niels<true>(q, select_niels<WB>(btab, cl));
+      q = ge_add_niels<false>(q, select_niels<WB>(btab2, ch));
+    } else {
+      q = ge_add_cached<false>(q, select_cached<G::TS>(taba, ca));
+    }
+  }
+  // Q == O  <=>  X == 0 and Y == Z
+  const uint32_t same = fe_is_zero(q.X) & fe_eq(q.Y, q.Z);
 
   const uint32_t parse_ok = s_ok & a_ok & r_ok;
   const uint32_t eq_ok = parse_ok & same;
