@@ -59,7 +59,7 @@ struct Global {
   bool inited = false;
   int ndev = 0;
   std::vector<DevCtx *> ctx;
-  std::atomic<int> variant{3};  // fastest measured: WA=3, WB=9, 2 waves/SIMD
+  std::atomic<int> variant{11};  // fastest measured: half-size scalars + B comb, WA=4, 2 waves/SIMD
 };
 
 Global &G() {
@@ -117,6 +117,32 @@ int ctx_prepare(DevCtx &c, size_t dev_bytes, size_t host_bytes) {
   return HSV_OK;
 }
 
+const uint8_t kBasepointEncoding[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
+                                        0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
+                                        0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
+
+// comb table of B on this device (caller holds c.mu and has set the device)
+int ensure_btable(DevCtx &c) {
+  if (c.d_btable) return HSV_OK;
+  uint8_t *d_enc = nullptr;
+  uint32_t *d_tab = nullptr, *d_tmp = nullptr;
+  hipError_t e = hipMalloc(&d_enc, 32);
+  if (e == hipSuccess) e = hipMalloc(&d_tab, hsv_comb_table_bytes());
+  if (e == hipSuccess) e = hipMalloc(&d_tmp, hsv_comb_tmp_bytes(1));
+  if (e == hipSuccess) e = hipMemcpy(d_enc, kBasepointEncoding, 32, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hsv_launch_comb_build(d_enc, 1, 0, d_tab, d_tmp, nullptr, c.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c.stream);
+  if (d_enc) (void)hipFree(d_enc);
+  if (d_tmp) (void)hipFree(d_tmp);
+  if (e != hipSuccess) {
+    if (d_tab) (void)hipFree(d_tab);
+    return hip_fail("building the B comb table", e);
+  }
+  c.d_btable = d_tab;
+  return HSV_OK;
+}
+
+
 // Host records: item i at pk + i*pk_stride, sig + i*sig_stride, msg + i*msg_stride
 // (msg_stride 0 = shared).  Runs [0, n) on one device, chunk by chunk.
 int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t *sig,
@@ -133,6 +159,10 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
   int rc = ctx_prepare(c, total, total);
   if (rc != HSV_OK) return rc;
   const int variant = G().variant.load();
+  if (hsv_variant_needs_comb(variant)) {
+    rc = ensure_btable(c);
+    if (rc != HSV_OK) return rc;
+  }
   for (size_t base = 0; base < n; base += chunk) {
     const size_t m = std::min(chunk, n - base);
     uint8_t *h = c.h_buf;
@@ -148,7 +178,7 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
     hipError_t e = hipMemcpyAsync(c.d_buf, h, in_bytes, hipMemcpyHostToDevice, c.stream);
     if (e != hipSuccess) return hip_fail("hipMemcpyAsync H2D", e);
     e = hsv_launch_verify(variant, c.d_buf + pk_off, 32, c.d_buf + sig_off, 64, c.d_buf + msg_off,
-                          msg_stride ? 32 : 0, (uint32_t)m, c.d_buf + flag_off, nullptr, c.stream);
+                          msg_stride ? 32 : 0, (uint32_t)m, c.d_buf + flag_off, nullptr, c.d_btable, c.stream);
     if (e != hipSuccess) return hip_fail("verify kernel launch", e);
     e = hipMemcpyAsync(h + flag_off, c.d_buf + flag_off, m, hipMemcpyDeviceToHost, c.stream);
     if (e != hipSuccess) return hip_fail("hipMemcpyAsync D2H", e);
@@ -287,13 +317,26 @@ int hsv_verify_device_bits(const uint8_t *d_pk, size_t pk_stride, const uint8_t 
   int rc = ensure_init();
   if (rc != HSV_OK) return rc;
   const int variant = G().variant.load();
+  const uint32_t *comb_b = nullptr;
+  if (hsv_variant_needs_comb(variant)) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail("hipGetDevice", e);
+    if (dev < 0 || dev >= G().ndev) return fail(HSV_ERR_INVALID_ARG, "current device out of range");
+    DevCtx &c = *G().ctx[dev];
+    std::lock_guard<std::mutex> lk(c.mu);
+    rc = ctx_prepare(c, 0, 0);
+    if (rc == HSV_OK) rc = ensure_btable(c);
+    if (rc != HSV_OK) return rc;
+    comb_b = c.d_btable;
+  }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   for (size_t base = 0; base < n; base += kChunk) {
     const size_t m = std::min(kChunk, n - base);
     hipError_t e = hsv_launch_verify(
         variant, d_pk + base * pk_stride, pk_stride, d_sig + base * sig_stride, sig_stride,
         d_msg + base * msg_stride, msg_stride, (uint32_t)m, d_flags ? d_flags + base : nullptr,
-        d_strict_bits ? d_strict_bits + base / 32 : nullptr, s);
+        d_strict_bits ? d_strict_bits + base / 32 : nullptr, comb_b, s);
     if (e != hipSuccess) return hip_fail("verify kernel launch", e);
   }
   return HSV_OK;
@@ -320,31 +363,6 @@ double hsv_measure_mad_peak(void) {
 
 // ---- committee key cache -------------------------------------------------
 namespace {
-
-const uint8_t kBasepointEncoding[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
-                                        0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
-                                        0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
-
-// comb table of B on this device (caller holds c.mu and has set the device)
-int ensure_btable(DevCtx &c) {
-  if (c.d_btable) return HSV_OK;
-  uint8_t *d_enc = nullptr;
-  uint32_t *d_tab = nullptr, *d_tmp = nullptr;
-  hipError_t e = hipMalloc(&d_enc, 32);
-  if (e == hipSuccess) e = hipMalloc(&d_tab, hsv_comb_table_bytes());
-  if (e == hipSuccess) e = hipMalloc(&d_tmp, hsv_comb_tmp_bytes(1));
-  if (e == hipSuccess) e = hipMemcpy(d_enc, kBasepointEncoding, 32, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hsv_launch_comb_build(d_enc, 1, 0, d_tab, d_tmp, nullptr, c.stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(c.stream);
-  if (d_enc) (void)hipFree(d_enc);
-  if (d_tmp) (void)hipFree(d_tmp);
-  if (e != hipSuccess) {
-    if (d_tab) (void)hipFree(d_tab);
-    return hip_fail("building the B comb table", e);
-  }
-  c.d_btable = d_tab;
-  return HSV_OK;
-}
 
 }  // namespace
 

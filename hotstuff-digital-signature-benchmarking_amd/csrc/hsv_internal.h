@@ -12,7 +12,9 @@ int hsv_num_variants(void);
 hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig,
                              uint64_t sig_stride, const uint8_t *msg, uint64_t msg_stride,
                              uint32_t n, uint8_t *flags_out, uint32_t *strict_bits,
-                             hipStream_t stream);
+                             const uint32_t *comb_b, hipStream_t stream);
+// variants that read the B comb table (comb_b must be non-null for them)
+int hsv_variant_needs_comb(int variant);
 
 // Time the v_mad_u64_u32 probe on the current device; MAC/s.
 double hsv_launch_mad_peak(int device_cus);

@@ -8,13 +8,26 @@
 //                      denominator (bench.py reports against it).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <mutex>
+#include <unordered_map>
+
 #include "hsv_internal.h"
 #include "hsv_verify_core.hpp"
+#include "hsv_verify_hc.hpp"
 
 namespace hsv {
 
 __device__ const uint32_t g_btable[256 * 24] = {
 #include "hsv_btable.inc"
+};
+// [m * 2^133]B and [m * 2^134]B: the second fixed base of the half-size
+// scalar path (b = b_lo + 2^SPLIT b_hi, hsv_verify_core.hpp)
+__device__ const uint32_t g_btable133[256 * 24] = {
+#include "hsv_btable133.inc"
+};
+__device__ const uint32_t g_btable134[256 * 24] = {
+#include "hsv_btable134.inc"
 };
 
 struct LdsBTab {
@@ -40,17 +53,27 @@ constexpr int kBlock = 256;
 // One verification per lane.  WA/WB: window widths (hsv_verify_core.hpp);
 // WAVES: waves per SIMD requested from the register allocator (256 regs at 2,
 // 512 at 1).  The B table needs 2^(WB-1) entries x 96 B of LDS.
-template <int WA, int WB, int WAVES>
+// HALF: half-size scalars (verify_one_half: ~135 doublings instead of ~253,
+// a second LDS table for B' = [2^SPLIT]B); a lane whose lattice reduction
+// does not give short scalars (~2^-14) takes the full-length path.
+template <int WA, int WB, int WAVES, bool HALF>
 __global__ void __launch_bounds__(kBlock, WAVES)
 hsv_verify_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
                   const uint8_t *__restrict__ sig, uint64_t sig_stride,
                   const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
                   uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits) {
   constexpr int kEntries = 1 << (WB - 1);
-  __shared__ uint4 lds_b[kEntries * 6];
+  constexpr int kTables = HALF ? 2 : 1;
+  __shared__ uint4 lds_b[kTables * kEntries * 6];
   {
     const uint4 *src = reinterpret_cast<const uint4 *>(g_btable);
     for (int i = threadIdx.x; i < kEntries * 6; i += kBlock) lds_b[i] = src[i];
+    if constexpr (HALF) {
+      const uint4 *src2 = reinterpret_cast<const uint4 *>(HalfWindows<WA, WB>::SPLIT == 133 ? g_btable133
+                                                                                           : g_btable134);
+      static_assert(HalfWindows<WA, WB>::SPLIT == 133 || HalfWindows<WA, WB>::SPLIT == 134, "B' table");
+      for (int i = threadIdx.x; i < kEntries * 6; i += kBlock) lds_b[kEntries * 6 + i] = src2[i];
+    }
   }
   __syncthreads();
 
@@ -77,7 +100,15 @@ hsv_verify_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
   }
 
   LdsBTab bt{lds_b};
-  const uint32_t f = verify_one<WA, WB>(pkw, sigw, msgw, bt);
+  uint32_t f;
+  if constexpr (HALF) {
+    LdsBTab bt2{lds_b + kEntries * 6};
+    bool fallback = false;
+    f = verify_one_half<WA, WB>(pkw, sigw, msgw, bt, bt2, fallback);
+    if (fallback) f = verify_one<WA, WB>(pkw, sigw, msgw, bt);
+  } else {
+    f = verify_one<WA, WB>(pkw, sigw, msgw, bt);
+  }
 
   if (valid && flags_out) flags_out[idx] = (uint8_t)f;
   if (strict_bits) {
@@ -89,6 +120,148 @@ hsv_verify_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
       const uint32_t w0 = wave_base / 32u;
       if (w0 < nwords) strict_bits[w0] = (uint32_t)mask;
       if (w0 + 1 < nwords) strict_bits[w0 + 1] = (uint32_t)(mask >> 32);
+    }
+  }
+}
+
+// Per-lane variable-base tables in global memory (hsv_verify_core.hpp, VT):
+// lane region = 2 tables x ENT entries x 128 B, entry = 8 x uint4.
+template <int ENT>
+struct GlobalVarTab {
+  uint4 *base;
+  __device__ __forceinline__ void put(int t, int m, const uint32_t w[32]) const {
+    uint4 *e = base + (t * ENT + m) * 8;
+    HSV_UNROLL
+    for (int q = 0; q < 8; ++q) e[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  }
+  __device__ __forceinline__ void get(int t, uint32_t m, uint32_t w[32]) const {
+    const uint4 *e = base + (t * ENT + (int)m) * 8;
+    HSV_UNROLL
+    for (int q = 0; q < 8; ++q) {
+      const uint4 v = e[q];
+      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+  }
+};
+
+template <int WA>
+constexpr int vt_lane_uint4() { return 2 * ((1 << (WA - 1)) + 1) * 8; }
+
+// Half-size scalars with memory-resident variable-base tables.  Persistent
+// grid: block b owns lane slots [b*kBlock, (b+1)*kBlock) of `vt_ws` and walks
+// the batch with stride gridDim.x * kBlock.
+template <int WA, int WB, int WAVES>
+__global__ void __launch_bounds__(kBlock, WAVES)
+hsv_verify_mt_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
+                     const uint8_t *__restrict__ sig, uint64_t sig_stride,
+                     const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
+                     uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
+                     uint4 *__restrict__ vt_ws) {
+  constexpr int kEntries = 1 << (WB - 1);
+  constexpr int kEnt = (1 << (WA - 1)) + 1;
+  using HW = HalfWindows<WA, WB>;
+  static_assert(HW::SPLIT == 133 || HW::SPLIT == 134, "B' table");
+  __shared__ uint4 lds_b[2 * kEntries * 6];
+  {
+    const uint4 *src = reinterpret_cast<const uint4 *>(g_btable);
+    const uint4 *src2 = reinterpret_cast<const uint4 *>(HW::SPLIT == 133 ? g_btable133 : g_btable134);
+    for (int i = threadIdx.x; i < kEntries * 6; i += kBlock) {
+      lds_b[i] = src[i];
+      lds_b[kEntries * 6 + i] = src2[i];
+    }
+  }
+  __syncthreads();
+  const GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)(blockIdx.x * kBlock + threadIdx.x) * vt_lane_uint4<WA>()};
+  const LdsBTab bt{lds_b}, bt2{lds_b + kEntries * 6};
+
+  for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+    const uint32_t idx = base + threadIdx.x;
+    const bool valid = idx < n;
+    const uint64_t li = valid ? idx : (uint64_t)(n - 1);
+    uint32_t pkw[8], sigw[16], msgw[8];
+    {
+      const uint4 *p = reinterpret_cast<const uint4 *>(pk + li * pk_stride);
+      const uint4 *s = reinterpret_cast<const uint4 *>(sig + li * sig_stride);
+      const uint4 *m = reinterpret_cast<const uint4 *>(msg + li * msg_stride);
+      const uint4 p0 = p[0], p1 = p[1];
+      const uint4 s0 = s[0], s1 = s[1], s2 = s[2], s3 = s[3];
+      const uint4 m0 = m[0], m1 = m[1];
+      pkw[0] = p0.x; pkw[1] = p0.y; pkw[2] = p0.z; pkw[3] = p0.w;
+      pkw[4] = p1.x; pkw[5] = p1.y; pkw[6] = p1.z; pkw[7] = p1.w;
+      sigw[0] = s0.x; sigw[1] = s0.y; sigw[2] = s0.z; sigw[3] = s0.w;
+      sigw[4] = s1.x; sigw[5] = s1.y; sigw[6] = s1.z; sigw[7] = s1.w;
+      sigw[8] = s2.x; sigw[9] = s2.y; sigw[10] = s2.z; sigw[11] = s2.w;
+      sigw[12] = s3.x; sigw[13] = s3.y; sigw[14] = s3.z; sigw[15] = s3.w;
+      msgw[0] = m0.x; msgw[1] = m0.y; msgw[2] = m0.z; msgw[3] = m0.w;
+      msgw[4] = m1.x; msgw[5] = m1.y; msgw[6] = m1.z; msgw[7] = m1.w;
+    }
+    bool fallback = false;
+    uint32_t f = verify_one_half_mt<WA, WB>(pkw, sigw, msgw, bt, bt2, vt, fallback);
+    if (fallback) f = verify_one_mt<WA, WB>(pkw, sigw, msgw, bt, vt);
+
+    if (valid && flags_out) flags_out[idx] = (uint8_t)f;
+    if (strict_bits) {
+      const uint64_t mask = __ballot(valid && (f & kStrictOk));
+      const uint32_t lane = threadIdx.x & 63u;
+      const uint32_t wave_base = idx - lane;
+      const uint32_t nwords = (n + 31u) / 32u;
+      if (lane == 0) {
+        const uint32_t w0 = wave_base / 32u;
+        if (w0 < nwords) strict_bits[w0] = (uint32_t)mask;
+        if (w0 + 1 < nwords) strict_bits[w0 + 1] = (uint32_t)(mask >> 32);
+      }
+    }
+  }
+}
+
+// Half-size scalars + comb table for B (hsv_verify_hc.hpp).  No LDS; the
+// per-lane tables live in `vt_ws` (persistent grid, as hsv_verify_mt_kernel),
+// the B comb table `comb_b` (384 KiB) is read through L2.
+template <int WA, int WAVES, bool PREFETCH>
+__global__ void __launch_bounds__(kBlock, WAVES)
+hsv_verify_hc_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
+                     const uint8_t *__restrict__ sig, uint64_t sig_stride,
+                     const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
+                     uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
+                     uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b) {
+  constexpr int kEnt = (1 << (WA - 1)) + 1;
+  GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)(blockIdx.x * kBlock + threadIdx.x) * vt_lane_uint4<WA>()};
+  for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+    const uint32_t idx = base + threadIdx.x;
+    const bool valid = idx < n;
+    const uint64_t li = valid ? idx : (uint64_t)(n - 1);
+    uint32_t pkw[8], sigw[16], msgw[8];
+    {
+      const uint4 *p = reinterpret_cast<const uint4 *>(pk + li * pk_stride);
+      const uint4 *s = reinterpret_cast<const uint4 *>(sig + li * sig_stride);
+      const uint4 *m = reinterpret_cast<const uint4 *>(msg + li * msg_stride);
+      const uint4 p0 = p[0], p1 = p[1];
+      const uint4 s0 = s[0], s1 = s[1], s2 = s[2], s3 = s[3];
+      const uint4 m0 = m[0], m1 = m[1];
+      pkw[0] = p0.x; pkw[1] = p0.y; pkw[2] = p0.z; pkw[3] = p0.w;
+      pkw[4] = p1.x; pkw[5] = p1.y; pkw[6] = p1.z; pkw[7] = p1.w;
+      sigw[0] = s0.x; sigw[1] = s0.y; sigw[2] = s0.z; sigw[3] = s0.w;
+      sigw[4] = s1.x; sigw[5] = s1.y; sigw[6] = s1.z; sigw[7] = s1.w;
+      sigw[8] = s2.x; sigw[9] = s2.y; sigw[10] = s2.z; sigw[11] = s2.w;
+      sigw[12] = s3.x; sigw[13] = s3.y; sigw[14] = s3.z; sigw[15] = s3.w;
+      msgw[0] = m0.x; msgw[1] = m0.y; msgw[2] = m0.z; msgw[3] = m0.w;
+      msgw[4] = m1.x; msgw[5] = m1.y; msgw[6] = m1.z; msgw[7] = m1.w;
+    }
+    bool fallback = false;
+    uint32_t f = verify_one_half_comb<WA, PREFETCH>(pkw, sigw, msgw, comb_b, vt, fallback);
+    if (fallback) f = verify_one_full_comb<WA, PREFETCH>(pkw, sigw, msgw, comb_b, vt);
+
+    if (valid && flags_out) flags_out[idx] = (uint8_t)f;
+    if (strict_bits) {
+      const uint64_t mask = __ballot(valid && (f & kStrictOk));
+      const uint32_t lane = threadIdx.x & 63u;
+      const uint32_t wave_base = idx - lane;
+      const uint32_t nwords = (n + 31u) / 32u;
+      if (lane == 0) {
+        const uint32_t w0 = wave_base / 32u;
+        if (w0 < nwords) strict_bits[w0] = (uint32_t)mask;
+        if (w0 + 1 < nwords) strict_bits[w0 + 1] = (uint32_t)(mask >> 32);
+      }
     }
   }
 }
@@ -121,24 +294,107 @@ __global__ void __launch_bounds__(256) hsv_mad_peak_kernel(uint32_t *sink, uint3
 //   1: WA=3 WB=9  1 wave/SIMD
 //   2: WA=4 WB=8  1 wave/SIMD
 //   3: WA=3 WB=9  2 waves/SIMD (register-capped; spills if it does not fit)
-extern "C" int hsv_num_variants(void) { return 4; }
+//   4: half-size scalars, WA=3 WB=9, 2 waves/SIMD
+//   5: half-size scalars, WA=3 WB=9, 1 wave/SIMD
+//   6: half-size scalars, WA=2 WB=8, 2 waves/SIMD
+//   7: half-size scalars, memory-resident variable-base tables, WA=3 WB=9, 2 waves/SIMD
+//   8: as 7 with WA=2 WB=8
+//   9: as 7 with WA=4 WB=8
+//  10: half-size scalars + comb table for B, memory tables, WA=3, 2 waves/SIMD
+//  11: as 10 with WA=4
+//  12: as 10 with WA=5
+//  13: as 11, 3 waves/SIMD, table entries loaded at their addition (no prefetch)
+//  14: as 11, 2 waves/SIMD, no prefetch
+extern "C" int hsv_num_variants(void) { return 15; }
+
+namespace {
+
+// Persistent-grid launch of hsv_verify_mt_kernel with a stream-ordered
+// workspace for the per-lane tables (freed on the same stream).
+template <int WA, int WB, int WAVES, bool COMB, bool PREFETCH = true>
+hipError_t launch_mt(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
+                     const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
+                     uint32_t *strict_bits, const uint32_t *comb_b, hipStream_t stream) {
+  const void *kern;
+  if constexpr (COMB) kern = reinterpret_cast<const void *>(hsv::hsv_verify_hc_kernel<WA, WAVES, PREFETCH>);
+  else kern = reinterpret_cast<const void *>(hsv::hsv_verify_mt_kernel<WA, WB, WAVES>);
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  static std::mutex mu;
+  static std::unordered_map<int, int> slots_per_dev;  // resident blocks per device for this kernel
+  int resident = 0;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = slots_per_dev.find(dev);
+    if (it == slots_per_dev.end()) {
+      int bpc = 0, cus = 0;
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kern, hsv::kBlock, 0);
+      if (e != hipSuccess) return e;
+      e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (e != hipSuccess) return e;
+      hipMemPool_t pool;
+      if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+        uint64_t keep = UINT64_MAX;  // keep freed workspaces cached in the pool
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+      }
+      it = slots_per_dev.emplace(dev, std::max(1, bpc) * std::max(1, cus)).first;
+    }
+    resident = it->second;
+  }
+  const uint32_t blocks_needed = (n + hsv::kBlock - 1) / hsv::kBlock;
+  const uint32_t grid = std::min<uint32_t>(blocks_needed, (uint32_t)resident);
+  const size_t ws_bytes = (size_t)grid * hsv::kBlock * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
+  void *ws = nullptr;
+  e = hipMallocAsync(&ws, ws_bytes, stream);
+  if (e != hipSuccess) return e;
+  if constexpr (COMB)
+    hipLaunchKernelGGL((hsv::hsv_verify_hc_kernel<WA, WAVES, PREFETCH>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
+                       pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits,
+                       reinterpret_cast<uint4 *>(ws), comb_b);
+  else
+    hipLaunchKernelGGL((hsv::hsv_verify_mt_kernel<WA, WB, WAVES>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
+                       pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits,
+                       reinterpret_cast<uint4 *>(ws));
+  e = hipGetLastError();
+  const hipError_t ef = hipFreeAsync(ws, stream);
+  return e != hipSuccess ? e : ef;
+}
+
+}  // namespace
 
 extern "C" hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t pk_stride,
                                         const uint8_t *sig, uint64_t sig_stride,
                                         const uint8_t *msg, uint64_t msg_stride, uint32_t n,
                                         uint8_t *flags_out, uint32_t *strict_bits,
-                                        hipStream_t stream) {
+                                        const uint32_t *comb_b, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const uint32_t grid = (n + hsv::kBlock - 1) / hsv::kBlock;
-#define HSV_LAUNCH(WA, WB, WV)                                                                \
-  hipLaunchKernelGGL((hsv::hsv_verify_kernel<WA, WB, WV>), dim3(grid), dim3(hsv::kBlock), 0, \
+#define HSV_LAUNCH(WA, WB, WV, HALF)                                                           \
+  hipLaunchKernelGGL((hsv::hsv_verify_kernel<WA, WB, WV, HALF>), dim3(grid), dim3(hsv::kBlock), 0, \
                      stream, pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out,   \
                      strict_bits)
   switch (variant) {
-    case 0: HSV_LAUNCH(2, 8, 2); break;
-    case 1: HSV_LAUNCH(3, 9, 1); break;
-    case 2: HSV_LAUNCH(4, 8, 1); break;
-    case 3: HSV_LAUNCH(3, 9, 2); break;
+    case 0: HSV_LAUNCH(2, 8, 2, false); break;
+    case 1: HSV_LAUNCH(3, 9, 1, false); break;
+    case 2: HSV_LAUNCH(4, 8, 1, false); break;
+    case 3: HSV_LAUNCH(3, 9, 2, false); break;
+    case 4: HSV_LAUNCH(3, 9, 2, true); break;
+    case 5: HSV_LAUNCH(3, 9, 1, true); break;
+    case 6: HSV_LAUNCH(2, 8, 2, true); break;
+#define HSV_LAUNCH_MT(WA, WB, WV, COMB) \
+  return launch_mt<WA, WB, WV, COMB>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream)
+    case 7: HSV_LAUNCH_MT(3, 9, 2, false);
+    case 8: HSV_LAUNCH_MT(2, 8, 2, false);
+    case 9: HSV_LAUNCH_MT(4, 8, 2, false);
+    case 10: if (!comb_b) return hipErrorInvalidValue; HSV_LAUNCH_MT(3, 3, 2, true);
+    case 11: if (!comb_b) return hipErrorInvalidValue; HSV_LAUNCH_MT(4, 4, 2, true);
+    case 12: if (!comb_b) return hipErrorInvalidValue; HSV_LAUNCH_MT(5, 5, 2, true);
+    case 13: if (!comb_b) return hipErrorInvalidValue;
+      return launch_mt<4, 4, 3, true, false>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
+    case 14: if (!comb_b) return hipErrorInvalidValue;
+      return launch_mt<4, 4, 2, true, false>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
+#undef HSV_LAUNCH_MT
     default: return hipErrorInvalidValue;
   }
 #undef HSV_LAUNCH
@@ -168,3 +424,5 @@ extern "C" double hsv_launch_mad_peak(int device_cus) {
   const double macs = (double)reps * grid * 256.0 * hsv::kPeakIters * hsv::kPeakChains;
   return ms > 0.f ? macs / (ms * 1e-3) : -1.0;
 }
+
+extern "C" int hsv_variant_needs_comb(int variant) { return variant >= 10 && variant <= 14; }

@@ -120,6 +120,47 @@ HSV_INL ge_ext ge_add_niels(const ge_ext &p, const ge_niels &q) {
   return r;
 }
 
+// Runtime-flag forms of the two formulas above: one copy of the code serves
+// every doubling / addition of a loop (the T product sits behind a wave-
+// uniform branch), which keeps the main loop inside the instruction cache.
+// Without T, r.T is left holding an unrelated value that must not be read.
+HSV_INL ge_ext ge_dbl_rt(const ge_ext &p, bool with_t) {
+  fe A = fe_sq(p.X);
+  fe B = fe_sq(p.Y);
+  fe C = fe_sq(p.Z);
+  C = fe_add(C, C);
+  fe H = fe_add(A, B);
+  fe xy = fe_add(p.X, p.Y);
+  fe E = fe_sub(H, fe_sq(xy));
+  fe G = fe_sub(A, B);
+  fe F = fe_carry(fe_add(C, G));
+  ge_ext r;
+  r.X = fe_mul(E, F);
+  r.Y = fe_mul(G, H);
+  r.Z = fe_mul(F, G);
+  r.T = r.Z;
+  if (with_t) r.T = fe_mul(E, H);
+  return r;
+}
+
+HSV_INL ge_ext ge_add_cached_rt(const ge_ext &p, const ge_cached &q, bool with_t) {
+  fe A = fe_mul(fe_sub(p.Y, p.X), q.YmX);
+  fe B = fe_mul(fe_add(p.Y, p.X), q.YpX);
+  fe C = fe_mul(p.T, q.T2d);
+  fe D = fe_mul(p.Z, q.Z2);
+  fe E = fe_sub(B, A);
+  fe F = fe_sub(D, C);
+  fe G = fe_add(D, C);
+  fe H = fe_add(B, A);
+  ge_ext r;
+  r.X = fe_mul(E, F);
+  r.Y = fe_mul(G, H);
+  r.Z = fe_mul(F, G);
+  r.T = r.Z;
+  if (with_t) r.T = fe_mul(E, H);
+  return r;
+}
+
 // -Q for a cached point: swap Y+X / Y-X, negate 2dT.
 HSV_INL ge_cached ge_cached_cneg(const ge_cached &q, uint32_t neg) {
   ge_cached r;

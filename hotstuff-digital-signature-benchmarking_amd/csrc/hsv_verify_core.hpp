@@ -362,4 +362,214 @@ HSV_INL uint32_t verify_one_half(const uint32_t pk[8], const uint32_t sig[16], c
          (a_ok ? kAOk : 0u) | (r_ok ? kROk : 0u);
 }
 
+
+// ---------------------------------------------------------------------------
+// Variable-base tables in memory.  Keeping [0..TS]P for two variable bases in
+// VGPRs (2 x 5 x 40 registers) forces heavy spilling at two waves per SIMD,
+// and a register-resident table is read with TS x 40 v_cndmask per addition.
+// Instead each lane writes its tables once to a private region (VT) and reads
+// one entry per addition by index: 8 x 16-byte loads issued a whole window
+// (WA doublings) ahead of their use, no selects.  Entries are packed
+// canonical field elements, 4 x 8 words = 128 bytes (one cache line).
+//   VT::put(t, m, const uint32_t w[32])   store entry m of table t
+//   VT::get(t, m, uint32_t w[32])         load it back
+// Entry 0 is the identity, so a zero digit needs no special case.
+
+HSV_INL void cached_pack(const ge_cached &c, uint32_t w[32]) {
+  fe_pack(c.YpX, w);
+  fe_pack(c.YmX, w + 8);
+  fe_pack(c.Z2, w + 16);
+  fe_pack(c.T2d, w + 24);
+}
+
+HSV_INL ge_cached cached_unpack(const uint32_t w[32]) {
+  ge_cached c;
+  c.YpX = fe_from_words_masked(w);
+  c.YmX = fe_from_words_masked(w + 8);
+  c.Z2 = fe_from_words_masked(w + 16);
+  c.T2d = fe_from_words_masked(w + 24);
+  return c;
+}
+
+// table t of VT <- [0..TS]P for the affine point (x, y)
+template <int TS, class VT>
+HSV_INL void vt_build(VT &vt, int t, const fe &x, const fe &y) {
+  uint32_t w[32];
+  cached_pack(ge_cached_identity(), w);
+  vt.put(t, 0, w);
+  ge_ext p1;
+  p1.X = x;
+  p1.Y = y;
+  p1.Z = fe_small(1);
+  p1.T = fe_mul(x, y);
+  const ge_cached c1 = ge_to_cached(p1);
+  cached_pack(c1, w);
+  vt.put(t, 1, w);
+  if (TS >= 2) {
+    ge_ext p = ge_dbl<true>(p1);
+    cached_pack(ge_to_cached(p), w);
+    vt.put(t, 2, w);
+    HSV_NOUNROLL
+    for (int m = 3; m <= TS; ++m) {
+      p = ge_add_cached<true>(p, c1);
+      cached_pack(ge_to_cached(p), w);
+      vt.put(t, m, w);
+    }
+  }
+}
+
+// signed digit (chunk - TS) -> table index |d| and sign
+template <int TS>
+HSV_INL uint32_t digit_mag(uint32_t chunk, uint32_t &neg) {
+  const int32_t d = (int32_t)chunk - TS;
+  neg = d < 0;
+  return (uint32_t)(d < 0 ? -d : d);
+}
+
+// Full-length verification with the table of -A in VT (table 0): the
+// fallback of the half-size path for the rare lanes without short scalars.
+template <int WA, int WB, class BTab, class VT>
+HSV_INL uint32_t verify_one_mt(const uint32_t pk[8], const uint32_t sig[16], const uint32_t msg[8],
+                               const BTab &btab, VT &vt) {
+  using G = Windows<WA, WB>;
+  const uint32_t s_ok = sc_is_canonical(sig + 8);
+  uint32_t h[16];
+  sha512_96(sig, pk, msg, h);
+  const sc k = sc_reduce512(h);
+  fe ax, ay;
+  const uint32_t a_ok = ge_decompress(pk, ax, ay);
+  const uint32_t small_a = a_ok & y_is_small_order(ay);
+  vt_build<G::TS>(vt, 0, fe_carry(fe_neg(ax)), ay);
+
+  uint32_t kr[8];
+  recode_add<8, WA, G::NA>(k.v, 8, kr);
+  limbs_shl_const<8, 256 - G::KBITS>(kr);
+  uint32_t sr[9];
+  recode_add<9, WB, G::NB>(sig + 8, 8, sr);
+  limbs_shl_const<9, 288 - G::SBITS>(sr);
+
+  ge_ext q = ge_identity();
+  HSV_NOUNROLL
+  for (int i = G::NA - 1; i >= 0; --i) {
+    uint32_t na;
+    const uint32_t ma = digit_mag<G::TS>(kr[7] >> (32 - WA), na);
+    limbs_shl<8>(kr, WA);
+    uint32_t wa[32];
+    vt.get(0, ma, wa);
+    if (i != G::NA - 1) {
+      HSV_UNROLL
+      for (int j = 0; j < WA - 1; ++j) q = ge_dbl<false>(q);
+      q = ge_dbl<true>(q);
+    }
+    const ge_cached qa = ge_cached_cneg(cached_unpack(wa), na);
+    if (i % G::M == 0) {
+      q = ge_add_cached<true>(q, qa);
+      const uint32_t cb = sr[8] >> (32 - WB);
+      limbs_shl<9>(sr, WB);
+      q = ge_add_niels<false>(q, select_niels<WB>(btab, cb));
+    } else {
+      q = ge_add_cached<false>(q, qa);
+    }
+  }
+  fe rx, ry;
+  const uint32_t r_ok = ge_decompress(sig, rx, ry);
+  const uint32_t small_r = r_ok & y_is_small_order(ry);
+  const uint32_t same = ge_eq_affine(q, rx, ry);
+  const uint32_t parse_ok = s_ok & a_ok & r_ok;
+  const uint32_t eq_ok = parse_ok & same;
+  const uint32_t strict_ok = eq_ok & (small_a ^ 1u) & (small_r ^ 1u);
+  return (strict_ok ? kStrictOk : 0u) | (eq_ok ? kEqOk : 0u) | (parse_ok ? kParseOk : 0u) |
+         (small_a ? kSmallA : 0u) | (small_r ? kSmallR : 0u) | (s_ok ? kSOk : 0u) |
+         (a_ok ? kAOk : 0u) | (r_ok ? kROk : 0u);
+}
+
+// Half-size-scalar verification (same equation as verify_one_half) with the
+// tables of -R (table 0) and -sign(c0) A (table 1) in VT.
+template <int WA, int WB, class BTab, class BTab2, class VT>
+HSV_INL uint32_t verify_one_half_mt(const uint32_t pk[8], const uint32_t sig[16], const uint32_t msg[8],
+                                    const BTab &btab, const BTab2 &btab2, VT &vt, bool &fallback) {
+  using G = HalfWindows<WA, WB>;
+  const uint32_t s_ok = sc_is_canonical(sig + 8);
+  uint32_t h[16];
+  sha512_96(sig, pk, msg, h);
+  const sc k = sc_reduce512(h);
+
+  const LatOut lat = lattice_reduce(k);
+  fallback = !lat.ok;
+
+  uint32_t a_ok, small_a, r_ok, small_r;
+  {
+    fe x, y;
+    r_ok = ge_decompress(sig, x, y);
+    small_r = r_ok & y_is_small_order(y);
+    vt_build<G::TS>(vt, 0, fe_carry(fe_neg(x)), y);
+  }
+  {
+    fe x, y;
+    a_ok = ge_decompress(pk, x, y);
+    small_a = a_ok & y_is_small_order(y);
+    vt_build<G::TS>(vt, 1, fe_carry(fe_select(fe_neg(x), x, lat.c0_neg)), y);
+  }
+
+  uint32_t dr[5], da[5], dlo[5], dhi[5];
+  {
+    const sc b = sc_mul_small(lat.c1, sig + 8);  // (c1 s) mod l = b_lo + 2^SPLIT b_hi
+    uint32_t blo[5], bhi[5];
+    HSV_UNROLL
+    for (int i = 0; i < 5; ++i) {
+      const int lo = 32 * i;
+      blo[i] = lo + 32 <= G::SPLIT ? b.v[i] : (lo < G::SPLIT ? (b.v[i] & ((1u << (G::SPLIT - lo)) - 1u)) : 0u);
+    }
+    constexpr int W = G::SPLIT / 32, S = G::SPLIT % 32;
+    HSV_UNROLL
+    for (int i = 0; i < 5; ++i) {
+      const uint32_t x0 = (i + W < 8) ? b.v[i + W] : 0u;
+      const uint32_t x1 = (i + W + 1 < 8) ? b.v[i + W + 1] : 0u;
+      bhi[i] = S ? ((x0 >> S) | (x1 << ((32 - S) & 31))) : x0;
+    }
+    recode_top5<WA, G::NW>(lat.c1, dr);
+    recode_top5<WA, G::NW>(lat.c0, da);
+    recode_top5<WB, G::NBW>(blo, dlo);
+    recode_top5<WB, G::NBW>(bhi, dhi);
+  }
+
+  ge_ext q = ge_identity();
+  HSV_NOUNROLL
+  for (int i = G::NW - 1; i >= 0; --i) {
+    uint32_t nr, na;
+    const uint32_t mr = digit_mag<G::TS>(dr[4] >> (32 - WA), nr);
+    const uint32_t ma = digit_mag<G::TS>(da[4] >> (32 - WA), na);
+    limbs_shl<5>(dr, WA);
+    limbs_shl<5>(da, WA);
+    uint32_t wr[32], wa[32];
+    vt.get(0, mr, wr);  // in flight during the doublings
+    vt.get(1, ma, wa);
+    if (i != G::NW - 1) {
+      HSV_UNROLL
+      for (int j = 0; j < WA - 1; ++j) q = ge_dbl<false>(q);
+      q = ge_dbl<true>(q);
+    }
+    q = ge_add_cached<true>(q, ge_cached_cneg(cached_unpack(wr), nr));
+    const ge_cached qa = ge_cached_cneg(cached_unpack(wa), na);
+    if (i % G::M == 0) {
+      q = ge_add_cached<true>(q, qa);
+      const uint32_t cl = dlo[4] >> (32 - WB), ch = dhi[4] >> (32 - WB);
+      limbs_shl<5>(dlo, WB);
+      limbs_shl<5>(dhi, WB);
+      q = ge_add_niels<true>(q, select_niels<WB>(btab, cl));
+      q = ge_add_niels<false>(q, select_niels<WB>(btab2, ch));
+    } else {
+      q = ge_add_cached<false>(q, qa);
+    }
+  }
+  const uint32_t same = fe_is_zero(q.X) & fe_eq(q.Y, q.Z);  // Q == O
+
+  const uint32_t parse_ok = s_ok & a_ok & r_ok;
+  const uint32_t eq_ok = parse_ok & same;
+  const uint32_t strict_ok = eq_ok & (small_a ^ 1u) & (small_r ^ 1u);
+  return (strict_ok ? kStrictOk : 0u) | (eq_ok ? kEqOk : 0u) | (parse_ok ? kParseOk : 0u) |
+         (small_a ? kSmallA : 0u) | (small_r ? kSmallR : 0u) | (s_ok ? kSOk : 0u) |
+         (a_ok ? kAOk : 0u) | (r_ok ? kROk : 0u);
+}
+
 }  // namespace hsv

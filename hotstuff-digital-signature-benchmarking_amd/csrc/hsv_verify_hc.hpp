@@ -1,0 +1,175 @@
+// Half-size scalars + fixed-base comb for B (the default generic kernel).
+//
+// Same verification equation as verify_one_half (hsv_verify_core.hpp):
+//   EQ_OK  <=>  [c1](-R) + [|c0|](-sign(c0) A) + [b]B == O,
+//   (c0, c1) = lattice_reduce(k),  b = (c1 s) mod l,
+// evaluated in two phases so the hot loop stays small:
+//   1. Straus over the two ~133-bit scalars c1, |c0|: NW windows of WA bits,
+//      WA doublings + 2 cached additions per window, entries of the per-lane
+//      tables [0..2^(WA-1)](-R), [0..2^(WA-1)](-sign(c0) A) read from memory
+//      (VT, one 128-byte line per entry) a window ahead of their use;
+//   2. [b]B from the comb table T_B[j][m] = [m 2^(8j)]B (hsv_comb.hpp, built
+//      once per device, L2-resident): 32 mixed additions, no doublings.
+// Each phase has one copy of its point formula (runtime with_t flag), so the
+// window loop is ~3k instructions instead of ~10k and stays in the shared
+// instruction cache.  A lane whose lattice reduction fails (~2^-14) takes
+// verify_one_full_comb: the same two phases with the full-length k.
+#pragma once
+#include "hsv_comb.hpp"
+#include "hsv_lattice.hpp"
+#include "hsv_verify_core.hpp"
+
+namespace hsv {
+
+// q += [s]B for a scalar s < 2^256 (8 words) via the B comb table (32 signed
+// radix-2^8 digits, consumed from the bottom).
+HSV_INL ge_ext comb_add_b(ge_ext q, const uint32_t s[8], const uint32_t *tb) {
+  uint32_t sr[9];
+  recode_add<9, 8, kCombPos>(s, 8, sr);
+  HSV_NOUNROLL
+  for (int j = 0; j < kCombPos; ++j) {
+    const uint32_t cb = sr[0] & 0xffu;
+    HSV_UNROLL
+    for (int i = 0; i < 8; ++i) sr[i] = (sr[i] >> 8) | (sr[i + 1] << 24);
+    sr[8] >>= 8;
+    const CombPosTab tpb{tb + (uint64_t)j * kCombEnt * kCombEntryWords};
+    q = ge_add_niels<true>(q, select_niels<8>(tpb, cb));
+  }
+  return q;
+}
+
+HSV_INL uint32_t flags_byte(uint32_t s_ok, uint32_t a_ok, uint32_t r_ok, uint32_t small_a, uint32_t small_r,
+                            uint32_t same) {
+  const uint32_t parse_ok = s_ok & a_ok & r_ok;
+  const uint32_t eq_ok = parse_ok & same;
+  const uint32_t strict_ok = eq_ok & (small_a ^ 1u) & (small_r ^ 1u);
+  return (strict_ok ? kStrictOk : 0u) | (eq_ok ? kEqOk : 0u) | (parse_ok ? kParseOk : 0u) |
+         (small_a ? kSmallA : 0u) | (small_r ? kSmallR : 0u) | (s_ok ? kSOk : 0u) |
+         (a_ok ? kAOk : 0u) | (r_ok ? kROk : 0u);
+}
+
+// Straus over NV (1 or 2) variable bases from VT tables 0..NV-1, scalars given
+// as recoded digit registers d[v] (L limbs, top window at the top bit).
+// Returns the accumulator with T valid (the comb phase follows).
+template <int WA, int NW, int L, int NV, bool PREFETCH, class VT>
+HSV_INL ge_ext straus_vt(uint32_t d[NV][L], VT &vt) {
+  constexpr int TS = 1 << (WA - 1);
+  ge_ext q = ge_identity();
+  HSV_NOUNROLL
+  for (int i = NW - 1; i >= 0; --i) {
+    uint32_t m[NV], neg[NV];
+    HSV_UNROLL
+    for (int v = 0; v < NV; ++v) {
+      m[v] = digit_mag<TS>(d[v][L - 1] >> (32 - WA), neg[v]);
+      limbs_shl<L>(d[v], WA);
+    }
+    if constexpr (PREFETCH) {
+      // both entries in flight during the doublings (2 x 32 registers)
+      uint32_t w[NV][32];
+      HSV_UNROLL
+      for (int v = 0; v < NV; ++v) vt.get(v, m[v], w[v]);
+      if (i != NW - 1) {
+        HSV_NOUNROLL
+        for (int j = 0; j < WA; ++j) q = ge_dbl_rt(q, j == WA - 1);
+      }
+      uint32_t cur[32], cneg = neg[0];
+      HSV_UNROLL
+      for (int x = 0; x < 32; ++x) cur[x] = w[0][x];
+      HSV_NOUNROLL
+      for (int v = 0; v < NV; ++v) {
+        q = ge_add_cached_rt(q, ge_cached_cneg(cached_unpack(cur), cneg), v + 1 < NV || i == 0);
+        if (NV > 1) {
+          HSV_UNROLL
+          for (int x = 0; x < 32; ++x) cur[x] = w[NV - 1][x];
+          cneg = neg[NV - 1];
+        }
+      }
+    } else {
+      // entries loaded right before their addition (fewer live registers;
+      // latency left to the other waves of the SIMD)
+      if (i != NW - 1) {
+        HSV_NOUNROLL
+        for (int j = 0; j < WA; ++j) q = ge_dbl_rt(q, j == WA - 1);
+      }
+      uint32_t mv = m[0], cneg = neg[0];
+      HSV_NOUNROLL
+      for (int v = 0; v < NV; ++v) {
+        uint32_t cur[32];
+        vt.get(v, mv, cur);
+        q = ge_add_cached_rt(q, ge_cached_cneg(cached_unpack(cur), cneg), v + 1 < NV || i == 0);
+        mv = m[NV - 1];
+        cneg = neg[NV - 1];
+      }
+    }
+  }
+  return q;
+}
+
+// Full-length path (fallback): [k](-A) by Straus with table 0, [s]B by comb,
+// compared with R as points (dalek's check, verify_one's flags).
+template <int WA, bool PREFETCH = true, class VT>
+HSV_INL uint32_t verify_one_full_comb(const uint32_t pk[8], const uint32_t sig[16], const uint32_t msg[8],
+                                      const uint32_t *tb, VT &vt) {
+  using G = Windows<WA, WA>;
+  const uint32_t s_ok = sc_is_canonical(sig + 8);
+  uint32_t h[16];
+  sha512_96(sig, pk, msg, h);
+  const sc k = sc_reduce512(h);
+  fe ax, ay;
+  const uint32_t a_ok = ge_decompress(pk, ax, ay);
+  const uint32_t small_a = a_ok & y_is_small_order(ay);
+  vt_build<G::TS>(vt, 0, fe_carry(fe_neg(ax)), ay);
+  uint32_t d[1][8];
+  recode_add<8, WA, G::NA>(k.v, 8, d[0]);
+  limbs_shl_const<8, 256 - G::KBITS>(d[0]);
+  ge_ext q = straus_vt<WA, G::NA, 8, 1, PREFETCH>(d, vt);
+  q = comb_add_b(q, sig + 8, tb);
+  fe rx, ry;
+  const uint32_t r_ok = ge_decompress(sig, rx, ry);
+  const uint32_t small_r = r_ok & y_is_small_order(ry);
+  return flags_byte(s_ok, a_ok, r_ok, small_a, small_r, ge_eq_affine(q, rx, ry));
+}
+
+template <int WA>
+struct HalfCombWindows {
+  static constexpr int NW = (kLatMaxBits + 1 + WA) / WA;  // c + C_WA < 2^(NW*WA) for c < 2^133
+  static constexpr int BITS = NW * WA;
+  static_assert(BITS <= 160 && BITS >= kLatMaxBits + 2, "scalar bound vs loop length");
+};
+
+template <int WA, bool PREFETCH = true, class VT>
+HSV_INL uint32_t verify_one_half_comb(const uint32_t pk[8], const uint32_t sig[16], const uint32_t msg[8],
+                                      const uint32_t *tb, VT &vt, bool &fallback) {
+  using G = HalfCombWindows<WA>;
+  constexpr int TS = 1 << (WA - 1);
+  const uint32_t s_ok = sc_is_canonical(sig + 8);
+  uint32_t h[16];
+  sha512_96(sig, pk, msg, h);
+  const sc k = sc_reduce512(h);
+  const LatOut lat = lattice_reduce(k);
+  fallback = !lat.ok;
+
+  uint32_t a_ok, small_a, r_ok, small_r;
+  {
+    fe x, y;
+    r_ok = ge_decompress(sig, x, y);
+    small_r = r_ok & y_is_small_order(y);
+    vt_build<TS>(vt, 0, fe_carry(fe_neg(x)), y);
+  }
+  {
+    fe x, y;
+    a_ok = ge_decompress(pk, x, y);
+    small_a = a_ok & y_is_small_order(y);
+    vt_build<TS>(vt, 1, fe_carry(fe_select(fe_neg(x), x, lat.c0_neg)), y);
+  }
+  uint32_t d[2][5];
+  recode_top5<WA, G::NW>(lat.c1, d[0]);
+  recode_top5<WA, G::NW>(lat.c0, d[1]);
+  ge_ext q = straus_vt<WA, G::NW, 5, 2, PREFETCH>(d, vt);
+  const sc b = sc_mul_small(lat.c1, sig + 8);
+  q = comb_add_b(q, b.v, tb);
+  const uint32_t same = fe_is_zero(q.X) & fe_eq(q.Y, q.Z);  // Q == O
+  return flags_byte(s_ok, a_ok, r_ok, small_a, small_r, same);
+}
+
+}  // namespace hsv

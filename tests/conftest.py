@@ -81,6 +81,16 @@ def golden():
 
 
 @pytest.fixture(scope="session")
+def fallback_records():
+    """Records whose challenge takes the kernels' full-length fallback path
+    (tests/golden/make_lattice_fallback.py): honest, corrupted-s, s + l and
+    mixed-order-key variants."""
+    raw = np.fromfile(os.path.join(GOLDEN, "lattice_fallback.bin"), dtype=np.uint8).reshape(-1, 129)
+    return {"pk": raw[:, :32].copy(), "sig": raw[:, 32:96].copy(), "msg": raw[:, 96:128].copy(),
+            "flags": raw[:, 128].copy()}
+
+
+@pytest.fixture(scope="session")
 def reference_fixtures():
     with open(os.path.join(GOLDEN, "reference_fixtures.json")) as f:
         return json.load(f)

@@ -15,6 +15,7 @@
 #include "hsv_comb.hpp"
 #include "hsv_lattice.hpp"
 #include "hsv_verify_core.hpp"
+#include "hsv_verify_hc.hpp"
 #include <vector>
 
 using namespace hsv;
@@ -40,6 +41,30 @@ struct HostBTab {
     return n;
   }
 };
+
+// per-lane variable-base tables (the kernel keeps them in a global-memory slot)
+struct HostVarTab {
+  uint32_t e[2][17][32];
+  void put(int t, int m, const uint32_t w[32]) { memcpy(e[t][m], w, 128); }
+  void get(int t, uint32_t m, uint32_t w[32]) const { memcpy(w, e[t][m], 128); }
+};
+
+// comb table of B (hsv_comb.hpp), built once on first use
+static const uint32_t *comb_b() {
+  static std::vector<uint32_t> tab;
+  if (tab.empty()) {
+    tab.resize(kCombTableWords);
+    std::vector<uint32_t> tmp(kCombEnt * 8);
+    const uint32_t bw[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
+                            0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
+    fe x, y;
+    ge_decompress(bw, x, y);
+    for (int j = 0; j < kCombPos; ++j)
+      comb_build_position(comb_position_base(x, y, 0, j), tab.data() + (uint64_t)j * kCombEnt * kCombEntryWords,
+                          tmp.data());
+  }
+  return tab.data();
+}
 
 static bool parse_hex(const std::string &s, uint8_t *out, size_t n) {
   if (s.size() != 2 * n) return false;
@@ -193,6 +218,43 @@ int main(int argc, char **argv) {
         b2.tab = variant == 10 ? kBTable133 : kBTable134;
         f = variant == 10 ? verify_one_half<3, 9>(pw, sw, mw, bt, b2, fb) : verify_one_half<2, 8>(pw, sw, mw, bt, b2, fb);
         if (fb) f = verify_one<3, 9>(pw, sw, mw, bt) | 0x100u;  // mark fallback for the test
+        break;
+      }
+      case 12:
+      case 13: {
+        bool fb = false;
+        HostBTab b2;
+        HostVarTab vt;
+        b2.tab = variant == 12 ? kBTable133 : kBTable134;
+        f = variant == 12 ? verify_one_half_mt<3, 9>(pw, sw, mw, bt, b2, vt, fb)
+                          : verify_one_half_mt<2, 8>(pw, sw, mw, bt, b2, vt, fb);
+        if (fb) f = verify_one_mt<3, 9>(pw, sw, mw, bt, vt) | 0x100u;
+        break;
+      }
+      case 14: {
+        HostVarTab vt;
+        f = verify_one_mt<3, 9>(pw, sw, mw, bt, vt);
+        break;
+      }
+      case 15: {
+        HostVarTab vt;
+        f = verify_one_mt<4, 8>(pw, sw, mw, bt, vt);
+        break;
+      }
+      case 16:
+      case 17:
+      case 19: {
+        bool fb = false;
+        HostVarTab vt;
+        f = variant == 16 ? verify_one_half_comb<3>(pw, sw, mw, comb_b(), vt, fb)
+          : variant == 17 ? verify_one_half_comb<4>(pw, sw, mw, comb_b(), vt, fb)
+                          : verify_one_half_comb<5>(pw, sw, mw, comb_b(), vt, fb);
+        if (fb) f = verify_one_full_comb<3>(pw, sw, mw, comb_b(), vt) | 0x100u;
+        break;
+      }
+      case 18: {
+        HostVarTab vt;
+        f = verify_one_full_comb<3>(pw, sw, mw, comb_b(), vt);
         break;
       }
       default: f = verify_one<3, 9>(pw, sw, mw, bt); break;

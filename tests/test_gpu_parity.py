@@ -37,6 +37,25 @@ def test_golden_every_variant(api, golden):
         verifier.set_variant(default)
 
 
+def test_lattice_fallback_records_every_variant(api, fallback_records):
+    """Challenges the lattice reduction rejects take the full-length path inside
+    the half-size kernels; every variant must still match the oracle's flags."""
+    _, verifier, _ = api
+    fb = fallback_records
+    default = verifier.get_variant()
+    try:
+        for v in range(verifier.num_variants()):
+            verifier.set_variant(v)
+            got = verifier.verify_flags(fb["pk"], fb["sig"], fb["msg"])
+            assert (got == fb["flags"]).all(), (v, np.nonzero(got != fb["flags"])[0][:8])
+            # mixed into a wave of ordinary records (the fallback lane diverges)
+            idx = np.arange(256) % len(fb["flags"])
+            got = verifier.verify_flags(fb["pk"][idx], fb["sig"][idx], fb["msg"][idx])
+            assert (got == fb["flags"][idx]).all(), v
+    finally:
+        verifier.set_variant(default)
+
+
 # ---- the reference's own tests (crypto/src/tests/crypto_tests.rs) ---------
 def _keys(crypto):
     return [crypto.generate_keypair(lambda n, s=s: s) for s in o.reference_key_seeds()]

@@ -85,7 +85,7 @@ def core_host32():
     return _build(BIN + "32", "-DHSV_FE_RADIX=32")
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 10, 11, 12, 14, 16, 18])
 def test_operand_bounds_hold_on_edge_and_sample(core_host_checked, golden, variant):
     """Bound-checked build over every edge vector and a random sample: no field
     operand leaves its class and no 64-bit column sum overflows."""
@@ -103,7 +103,7 @@ def test_radix32_field_matches_golden(core_host32, golden):
     assert (got == golden["flags"]).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19])
 def test_verify_core_all_geometries_match_golden(core_host, golden, variant):
     lines = [f"{bytes(p).hex()} {bytes(s).hex()} {bytes(m).hex()}"
              for p, s, m in zip(golden["pk"], golden["sig"], golden["msg"])]
@@ -125,3 +125,42 @@ def test_committee_comb_path_matches_golden(core_host, golden):
     got = np.array([int(x, 16) for x in _run(core_host, ["--comb"], lines)], np.uint8)
     bad = np.nonzero(got != golden["flags"][idx])[0]
     assert bad.size == 0, [golden["cases"][idx[i]] for i in bad[:10]]
+
+
+def test_lattice_reduction_properties(core_host):
+    """hsv_lattice.hpp: for challenges k < l the reduced pair satisfies
+    c0 == c1 k (mod 8l), c1 odd and 0 < c1, |c0| < 2^133 (ok == 1), or reports
+    ok == 0 (the kernel then takes the full-length path).  Includes k = 0, 1,
+    l - 1, small and structured values."""
+    rnd = random.Random(11)
+    N = 8 * o.L
+    ks = [0, 1, 2, 3, 8, o.L - 1, o.L - 2, 2**128, 2**128 - 1, 2**127 + 1, 2**252, (o.L - 1) // 2,
+          (o.L + 1) // 2, (o.L - 1) // 3, 2**200 + 12345]
+    ks += [rnd.randrange(o.L) for _ in range(3000)]
+    got = _run(core_host, ["--lattice"], [f"{k:064x}" for k in ks])
+    assert len(got) == 4 * len(ks)
+    n_ok = 0
+    for i, k in enumerate(ks):
+        ok, neg, c0, c1 = int(got[4 * i]), int(got[4 * i + 1]), int(got[4 * i + 2], 16), int(got[4 * i + 3], 16)
+        if not ok:
+            continue
+        n_ok += 1
+        c0s = -c0 if neg else c0
+        assert c1 % 2 == 1 and 0 < c1 < 2**133 and c0 < 2**133, k
+        assert (c0s - c1 * k) % N == 0, k
+    assert n_ok >= len(ks) - 8
+
+
+@pytest.mark.parametrize("variant", [16, 17])
+def test_lattice_fallback_records(core_host, fallback_records, variant):
+    """Records built on challenges the lattice reduction rejects: the half-size
+    path hands them to the full-length path (reported on stderr) and the flags
+    equal the oracle's."""
+    fb = fallback_records
+    lines = [f"{bytes(p).hex()} {bytes(s).hex()} {bytes(m).hex()}" for p, s, m in zip(fb["pk"], fb["sig"], fb["msg"])]
+    r = subprocess.run([core_host, "--variant", str(variant)], input="\n".join(lines) + "\n",
+                       capture_output=True, text=True, check=True)
+    got = np.array([int(x, 16) for x in r.stdout.split()], np.uint8)
+    assert (got == fb["flags"]).all()
+    # 24 challenges x (honest, flipped s, s + l) keep k; the mixed-order key changes it
+    assert r.stderr.count("fallback") >= 48

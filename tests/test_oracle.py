@@ -142,3 +142,12 @@ def test_c_oracle_batch_rule(reference_fixtures, oracle_lib):
         sig = b"".join(bytes.fromhex(s) for _, s in v["votes"])
         got = oracle_lib.oracle_verify_batch(bytes.fromhex(v["digest"]), pk, sig, len(v["votes"]))
         assert bool(got) == v["expect_ok"], name
+
+
+def test_c_oracle_reproduces_fallback_records(fallback_records, oracle_lib):
+    """tests/golden/lattice_fallback.bin (flags from the Python oracle) agrees
+    with the C oracle; honest records are accepted, flipped-s / s + l rejected."""
+    fb = fallback_records
+    got = oracle_flags(oracle_lib, fb["pk"], fb["sig"], fb["msg"])
+    assert (got == fb["flags"]).all()
+    assert (fb["flags"][0::4] & o.STRICT_OK).all()

@@ -24,6 +24,10 @@ def main():
     lo, hi = max(back, key=lambda x: x[1] - x[0])
     c = collections.Counter(l.split()[0] for l in K[lo:hi + 1] if is_ins(l))
     print(f"kernel instrs {sum(is_ins(l) for l in K)}  main loop instrs {sum(c.values())}")
+    body = K[lo:hi + 1]
+    print("  in main loop: scratch ops %d, global loads %d, ds_read %d; whole kernel scratch ops %d" % (
+        sum("scratch_" in l for l in body), sum("global_load" in l for l in body),
+        sum("ds_read" in l for l in body), sum("scratch_" in l for l in K)))
     for k, v in c.most_common(14):
         print(f"  {k:28s} {v}")
 

@@ -73,6 +73,50 @@ KERNEL(k_cndmask, uint32_t x[NCHAIN]; uint32_t a = t | 1;
        for (int c = 0; c < NCHAIN; ++c) x[c] = t + c,
        asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(x[c]) : "v"(a) : "vcc"), x[c])
 
+
+KERNEL(k_cndmask_s, uint32_t x[NCHAIN]; uint32_t a = t | 1; uint64_t m;
+       asm volatile("v_cmp_lt_u32 %0, %1, %2" : "=s"(m) : "v"(t & 63u), "v"(32u));
+       for (int c = 0; c < NCHAIN; ++c) x[c] = t + c,
+       asm volatile("v_cndmask_b32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(a), "s"(m)), x[c])
+
+KERNEL(k_add_u32, uint32_t x[NCHAIN]; uint32_t a = t | 1;
+       for (int c = 0; c < NCHAIN; ++c) x[c] = t + c,
+       asm volatile("v_add_u32 %0, %0, %1" : "+v"(x[c]) : "v"(a)), x[c])
+
+KERNEL(k_and_b32, uint32_t x[NCHAIN]; uint32_t a = t | 1;
+       for (int c = 0; c < NCHAIN; ++c) x[c] = t + c,
+       asm volatile("v_and_b32 %0, %0, %1" : "+v"(x[c]) : "v"(a)), x[c])
+
+KERNEL(k_mov_b32, uint32_t x[NCHAIN]; uint32_t a = t | 1;
+       for (int c = 0; c < NCHAIN; ++c) x[c] = t + c,
+       asm volatile("v_mov_b32 %0, %1" : "=v"(x[c]) : "v"(a + c)), x[c])
+
+KERNEL(k_lshrrev_b64, uint64_t x[NCHAIN];
+       for (int c = 0; c < NCHAIN; ++c) x[c] = ((uint64_t)t << 20) + c,
+       asm volatile("v_lshrrev_b64 %0, 1, %0" : "+v"(x[c])), (uint32_t)(x[c] ^ (x[c] >> 32)))
+
+KERNEL(k_add3_u32, uint32_t x[NCHAIN]; uint32_t a = t | 1; uint32_t b = t * 7;
+       for (int c = 0; c < NCHAIN; ++c) x[c] = t + c,
+       asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(a), "v"(b)), x[c])
+
+KERNEL(k_bfe_u32, uint32_t x[NCHAIN];
+       for (int c = 0; c < NCHAIN; ++c) x[c] = t + c,
+       asm volatile("v_bfe_u32 %0, %0, 3, 26" : "+v"(x[c])), x[c])
+
+KERNEL(k_mad_u64_u32_dep, uint64_t x[NCHAIN]; uint32_t a = t | 1; uint32_t b = t * 3 + 7;
+       for (int c = 0; c < NCHAIN; ++c) x[c] = t + c,
+       asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(x[0]) : "v"(a), "v"(b) : "vcc"),
+       (uint32_t)(x[c] ^ (x[c] >> 32)))
+
+KERNEL(k_pk_add_u16, uint32_t x[NCHAIN]; uint32_t a = t | 1;
+       for (int c = 0; c < NCHAIN; ++c) x[c] = t + c,
+       asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(x[c]) : "v"(a)), x[c])
+
+KERNEL(k_fma_f64b, double x[NCHAIN]; double a = 1.0000001 + t * 1e-12; double b = 1e-9;
+       for (int c = 0; c < NCHAIN; ++c) x[c] = t + c,
+       asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(x[c]) : "v"(a), "v"(b)),
+       (uint32_t)(x[c]))
+
 typedef void (*kfn)(uint32_t *, uint32_t);
 
 static double run(kfn k, const char *name, int blocks_per_cu, uint32_t *sink, int ncu) {
@@ -101,7 +145,7 @@ int main() {
   uint32_t *sink;
   hipMalloc(&sink, 64);
   int ncu = prop.multiProcessorCount;
-  for (int bpc : {4, 8}) {
+  for (int bpc : {8, 16}) {
     run(k_fma_f32, "v_fma_f32", bpc, sink, ncu);
     run(k_add_co_u32, "v_add_co_u32", bpc, sink, ncu);
     run(k_addc_co_u32, "v_addc_co_u32", bpc, sink, ncu);
@@ -114,6 +158,16 @@ int main() {
     run(k_mul_hi_u32_u24, "v_mul_hi_u32_u24", bpc, sink, ncu);
     run(k_lshl_add_u64, "v_lshl_add_u64", bpc, sink, ncu);
     run(k_fma_f64, "v_fma_f64", bpc, sink, ncu);
+    run(k_cndmask_s, "v_cndmask_b32_sgpr", bpc, sink, ncu);
+    run(k_add_u32, "v_add_u32", bpc, sink, ncu);
+    run(k_and_b32, "v_and_b32", bpc, sink, ncu);
+    run(k_mov_b32, "v_mov_b32", bpc, sink, ncu);
+    run(k_lshrrev_b64, "v_lshrrev_b64", bpc, sink, ncu);
+    run(k_add3_u32, "v_add3_u32", bpc, sink, ncu);
+    run(k_bfe_u32, "v_bfe_u32", bpc, sink, ncu);
+    run(k_mad_u64_u32_dep, "v_mad_u64_u32_dep1", bpc, sink, ncu);
+    run(k_pk_add_u16, "v_pk_add_u16", bpc, sink, ncu);
+    run(k_fma_f64b, "v_fma_f64_acc", bpc, sink, ncu);
   }
   hipFree(sink);
   return 0;
