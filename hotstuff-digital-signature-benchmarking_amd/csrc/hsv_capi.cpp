@@ -59,7 +59,7 @@ struct Global {
   bool inited = false;
   int ndev = 0;
   std::vector<DevCtx *> ctx;
-  std::atomic<int> variant{11};  // fastest measured: half-size scalars + B comb, WA=4, 2 waves/SIMD
+  std::atomic<int> variant{13};  // fastest measured: half-size scalars + B comb, WA=4, 3 waves/SIMD
 };
 
 Global &G() {

@@ -184,10 +184,65 @@ HSV_INL void fe26_check_columns(const fe &f, const fe &g) {
       if ((i & 1) && (j & 1)) m *= 2;
       acc += (unsigned __int128)f.v[i] * g.v[j] * m;
     }
-    HSV_BOUND((acc >> 64) == 0, "fe_mul column overflow");
+    HSV_BOUND(((acc + ((unsigned __int128)1 << 40)) >> 64) == 0, "fe_mul column overflow (incl. carry-in)");
   }
 }
 #endif
+
+// acc + sum_i a[i] * b[i] as ONE chain of v_mad_u64_u32 starting from acc.
+// On the device the chain is a single asm statement: the compiler would
+// otherwise split a column into parallel partial sums (and move the carry-in
+// to the end), paying a 64-bit add per split; a dependent chain issues as
+// fast as independent ones on gfx950 (tools/ubench_chain.hip).  The carry-out
+// SGPR pair of the instruction is a dead early-clobber output.
+#define HSV_MAD1(i) "v_mad_u64_u32 %0, %1, %" #i ", %" #i "+1, %0\n\t"
+template <int N>
+HSV_INL uint64_t fe26_chain(const uint32_t *a, const uint32_t *b, uint64_t acc) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t cc;
+#define HSV_P(i) "v"(a[i]), "v"(b[i])
+#define HSV_M(k) "v_mad_u64_u32 %0, %1, %" #k
+  static_assert(N >= 1 && N <= 10, "chain length");
+  if constexpr (N == 5)
+    asm(HSV_M(2) ", %3, %0\n\t" HSV_M(4) ", %5, %0\n\t" HSV_M(6) ", %7, %0\n\t" HSV_M(8) ", %9, %0\n\t"
+        HSV_M(10) ", %11, %0"
+        : "+v"(acc), "=&s"(cc) : HSV_P(0), HSV_P(1), HSV_P(2), HSV_P(3), HSV_P(4));
+  else if constexpr (N == 6)
+    asm(HSV_M(2) ", %3, %0\n\t" HSV_M(4) ", %5, %0\n\t" HSV_M(6) ", %7, %0\n\t" HSV_M(8) ", %9, %0\n\t"
+        HSV_M(10) ", %11, %0\n\t" HSV_M(12) ", %13, %0"
+        : "+v"(acc), "=&s"(cc) : HSV_P(0), HSV_P(1), HSV_P(2), HSV_P(3), HSV_P(4), HSV_P(5));
+  else if constexpr (N == 10)
+    asm(HSV_M(2) ", %3, %0\n\t" HSV_M(4) ", %5, %0\n\t" HSV_M(6) ", %7, %0\n\t" HSV_M(8) ", %9, %0\n\t"
+        HSV_M(10) ", %11, %0\n\t" HSV_M(12) ", %13, %0\n\t" HSV_M(14) ", %15, %0\n\t" HSV_M(16) ", %17, %0\n\t"
+        HSV_M(18) ", %19, %0\n\t" HSV_M(20) ", %21, %0"
+        : "+v"(acc), "=&s"(cc)
+        : HSV_P(0), HSV_P(1), HSV_P(2), HSV_P(3), HSV_P(4), HSV_P(5), HSV_P(6), HSV_P(7), HSV_P(8), HSV_P(9));
+  else {
+    HSV_UNROLL
+    for (int i = 0; i < N; ++i) acc += (uint64_t)a[i] * b[i];
+  }
+#undef HSV_P
+#undef HSV_M
+  (void)cc;
+  return acc;
+#else
+  for (int i = 0; i < N; ++i) acc += (uint64_t)a[i] * b[i];
+  return acc;
+#endif
+}
+#undef HSV_MAD1
+
+// Columns are produced in order 0..9; the carry out of column k is the
+// initial accumulator of column k+1 (v_mad_u64_u32 adds it for free), so the
+// carry chain costs one 64-bit shift and one mask per limb and no 64-bit adds.
+// The final carry (weight 2^255) wraps into limbs 0/1 times 19.
+// -DHSV_FE26_PARALLEL_CARRY selects the earlier form (independent column
+// sums, then a ref10-order carry pass).
+HSV_INL void fe26_wrap_carry(fe &r, uint64_t acc) {
+  const uint64_t t = (uint64_t)r.v[0] + acc * 19u;
+  r.v[0] = (uint32_t)t & 0x3ffffffu;
+  r.v[1] += (uint32_t)(t >> 26);
+}
 
 HSV_INL fe fe_mul(const fe &f, const fe &g) {
   HSV_SCHED_FENCE();
@@ -201,6 +256,7 @@ HSV_INL fe fe_mul(const fe &f, const fe &g) {
     g19[i] = g.v[i] * 19u;
     f2[i] = (i & 1) ? f.v[i] * 2u : f.v[i];
   }
+#ifdef HSV_FE26_PARALLEL_CARRY
   uint64_t h[10];
   HSV_UNROLL
   for (int k = 0; k < 10; ++k) {
@@ -217,8 +273,64 @@ HSV_INL fe fe_mul(const fe &f, const fe &g) {
     h[k] = acc;
   }
   fe r = fe26_carry64(h);
+#else
+  fe r;
+  uint64_t acc = 0;
+  HSV_UNROLL
+  for (int k = 0; k < 10; ++k) {
+    uint32_t ca[10], cb[10];
+    HSV_UNROLL
+    for (int i = 0; i < 10; ++i) {
+      int j = k - i;
+      const bool wrap = j < 0;
+      if (wrap) j += 10;
+      ca[i] = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+      cb[i] = wrap ? g19[j] : g.v[j];
+    }
+    acc = fe26_chain<10>(ca, cb, acc);
+    r.v[k] = (uint32_t)acc & fe26_mask(k);
+    acc >>= fe26_bits(k);
+  }
+  fe26_wrap_carry(r, acc);
+#endif
   HSV_SCHED_FENCE();
   return r;
+}
+
+// operands of the product f_i f_j (i <= j) in a squaring, with its factor
+// (2 for i != j, 2 for odd i and j, 19 for a wrap past limb 9) folded in
+HSV_INL void fe26_sq_operands(int i, int j, const uint32_t *f, const uint32_t *f2, const uint32_t *f19,
+                              const uint32_t *f38, uint32_t &a, uint32_t &b) {
+  const bool odd = (i & 1) && (j & 1);
+  const bool wrap = i + j >= 10;
+  const int m = (i != j ? 2 : 1) * (odd ? 2 : 1) * (wrap ? 19 : 1);
+  if (m == 1) { a = f[i]; b = f[j]; }
+  else if (m == 2) { a = f2[i]; b = f[j]; }
+  else if (m == 4) { a = f2[i]; b = f2[j]; }
+  else if (m == 19) { a = f[i]; b = f19[j]; }
+  else if (m == 38) {
+    if (i == j) { a = f[i]; b = f38[j]; }
+    else { a = f2[i]; b = f19[j]; }
+  } else { a = f2[i]; b = f38[j]; }  // m == 76
+}
+
+// column K of a squaring (6 products for even K, 5 for odd K) added to acc
+template <int K>
+HSV_INL uint64_t fe26_sq_column(const uint32_t *f, const uint32_t *f2, const uint32_t *f19, const uint32_t *f38,
+                                uint64_t acc) {
+  constexpr int N = (K % 2 == 0) ? 6 : 5;
+  uint32_t ca[N], cb[N];
+  int n = 0;
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) {
+    HSV_UNROLL
+    for (int j = i; j < 10; ++j) {
+      if ((i + j) % 10 != K) continue;
+      fe26_sq_operands(i, j, f, f2, f19, f38, ca[n], cb[n]);
+      ++n;
+    }
+  }
+  return fe26_chain<N>(ca, cb, acc);
 }
 
 HSV_INL fe fe_sq(const fe &f) {
@@ -232,8 +344,9 @@ HSV_INL fe fe_sq(const fe &f) {
   for (int i = 0; i < 10; ++i) {
     f2[i] = f.v[i] * 2u;
     f19[i] = f.v[i] * 19u;
-    f38[i] = (i & 1) ? f.v[i] * 38u : 0u;  // only odd limbs are scaled by 38
+    f38[i] = (i & 1) ? f19[i] * 2u : 0u;  // only odd limbs are scaled by 38
   }
+#ifdef HSV_FE26_PARALLEL_CARRY
   uint64_t h[10];
   HSV_UNROLL
   for (int k = 0; k < 10; ++k) {
@@ -243,24 +356,26 @@ HSV_INL fe fe_sq(const fe &f) {
       HSV_UNROLL
       for (int j = i; j < 10; ++j) {
         if ((i + j) % 10 != k) continue;
-        const bool odd = (i & 1) && (j & 1);
-        const bool wrap = i + j >= 10;
-        const int m = (i != j ? 2 : 1) * (odd ? 2 : 1) * (wrap ? 19 : 1);
         uint32_t a, b;
-        if (m == 1) { a = f.v[i]; b = f.v[j]; }
-        else if (m == 2) { a = f2[i]; b = f.v[j]; }
-        else if (m == 4) { a = f2[i]; b = f2[j]; }
-        else if (m == 19) { a = f.v[i]; b = f19[j]; }
-        else if (m == 38) {
-          if (i == j) { a = f.v[i]; b = f38[j]; }
-          else { a = f2[i]; b = f19[j]; }
-        } else { a = f2[i]; b = f38[j]; }  // m == 76
+        fe26_sq_operands(i, j, f.v, f2, f19, f38, a, b);
         acc += (uint64_t)a * b;
       }
     }
     h[k] = acc;
   }
   fe r = fe26_carry64(h);
+#else
+  fe r;
+  uint64_t acc = 0;
+#define HSV_SQC(K)                                 \
+  acc = fe26_sq_column<K>(f.v, f2, f19, f38, acc); \
+  r.v[K] = (uint32_t)acc & fe26_mask(K);           \
+  acc >>= fe26_bits(K);
+  HSV_SQC(0) HSV_SQC(1) HSV_SQC(2) HSV_SQC(3) HSV_SQC(4)
+  HSV_SQC(5) HSV_SQC(6) HSV_SQC(7) HSV_SQC(8) HSV_SQC(9)
+#undef HSV_SQC
+  fe26_wrap_carry(r, acc);
+#endif
   HSV_SCHED_FENCE();
   return r;
 }
