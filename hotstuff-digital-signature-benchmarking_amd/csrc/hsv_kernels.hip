@@ -111,16 +111,11 @@ hsv_verify_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
   }
 
   if (valid && flags_out) flags_out[idx] = (uint8_t)f;
-  if (strict_bits) {
+  if (strict_bits) {  // lanes 0 and 1 store the two halves of the wave's ballot
     const uint64_t mask = __ballot(valid && (f & kStrictOk));
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave_base = idx - lane;  // multiple of 64
-    const uint32_t nwords = (n + 31u) / 32u;
-    if (lane == 0) {
-      const uint32_t w0 = wave_base / 32u;
-      if (w0 < nwords) strict_bits[w0] = (uint32_t)mask;
-      if (w0 + 1 < nwords) strict_bits[w0 + 1] = (uint32_t)(mask >> 32);
-    }
+    const uint32_t w = (idx - lane) / 32u + lane;  // idx - lane: multiple of 64
+    if (lane < 2u && w < (n + 31u) / 32u) strict_bits[w] = lane ? (uint32_t)(mask >> 32) : (uint32_t)mask;
   }
 }
 
@@ -203,31 +198,35 @@ hsv_verify_mt_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
     if (strict_bits) {
       const uint64_t mask = __ballot(valid && (f & kStrictOk));
       const uint32_t lane = threadIdx.x & 63u;
-      const uint32_t wave_base = idx - lane;
-      const uint32_t nwords = (n + 31u) / 32u;
-      if (lane == 0) {
-        const uint32_t w0 = wave_base / 32u;
-        if (w0 < nwords) strict_bits[w0] = (uint32_t)mask;
-        if (w0 + 1 < nwords) strict_bits[w0 + 1] = (uint32_t)(mask >> 32);
-      }
+      const uint32_t w = (idx - lane) / 32u + lane;
+      if (lane < 2u && w < (n + 31u) / 32u) strict_bits[w] = lane ? (uint32_t)(mask >> 32) : (uint32_t)mask;
     }
   }
 }
 
 // Half-size scalars + comb table for B (hsv_verify_hc.hpp).  No LDS; the
-// per-lane tables live in `vt_ws` (persistent grid, as hsv_verify_mt_kernel),
-// the B comb table `comb_b` (384 KiB) is read through L2.
+// per-lane tables live in `vt_ws` (lane slot = blockIdx * kBlock + threadIdx),
+// the B comb table `comb_b` (384 KiB) is read through L2.  Work is handed out
+// per wave, 64 items at a time, from the counter `next` (zero at launch): a
+// wave slowed by a lane on the full-length fallback, or one that started
+// late, simply takes fewer batches, so the grid finishes together.
 template <int WA, int WAVES, bool PREFETCH>
 __global__ void __launch_bounds__(kBlock, WAVES)
 hsv_verify_hc_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
                      const uint8_t *__restrict__ sig, uint64_t sig_stride,
                      const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
                      uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
-                     uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b) {
+                     uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b,
+                     uint32_t *__restrict__ next) {
   constexpr int kEnt = (1 << (WA - 1)) + 1;
   GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)(blockIdx.x * kBlock + threadIdx.x) * vt_lane_uint4<WA>()};
-  for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-    const uint32_t idx = base + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  for (;;) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(next, 64u);
+    base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
+    if (base >= n) break;
+    const uint32_t idx = base + lane;
     const bool valid = idx < n;
     const uint64_t li = valid ? idx : (uint64_t)(n - 1);
     uint32_t pkw[8], sigw[16], msgw[8];
@@ -253,15 +252,10 @@ hsv_verify_hc_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
 
     if (valid && flags_out) flags_out[idx] = (uint8_t)f;
     if (strict_bits) {
+      // lanes 0 and 1 store the two 32-bit halves of the wave's ballot
       const uint64_t mask = __ballot(valid && (f & kStrictOk));
-      const uint32_t lane = threadIdx.x & 63u;
-      const uint32_t wave_base = idx - lane;
-      const uint32_t nwords = (n + 31u) / 32u;
-      if (lane == 0) {
-        const uint32_t w0 = wave_base / 32u;
-        if (w0 < nwords) strict_bits[w0] = (uint32_t)mask;
-        if (w0 + 1 < nwords) strict_bits[w0 + 1] = (uint32_t)(mask >> 32);
-      }
+      const uint32_t w = base / 32u + lane;
+      if (lane < 2u && w < (n + 31u) / 32u) strict_bits[w] = lane ? (uint32_t)(mask >> 32) : (uint32_t)mask;
     }
   }
 }
@@ -346,12 +340,17 @@ hipError_t launch_mt(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
   const uint32_t grid = std::min<uint32_t>(blocks_needed, (uint32_t)resident);
   const size_t ws_bytes = (size_t)grid * hsv::kBlock * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
   void *ws = nullptr;
-  e = hipMallocAsync(&ws, ws_bytes, stream);
+  e = hipMallocAsync(&ws, ws_bytes + 256, stream);  // + the work counter of the comb kernel
   if (e != hipSuccess) return e;
+  uint32_t *next = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(ws) + ws_bytes);
+  if constexpr (COMB) {
+    e = hipMemsetAsync(next, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+  }
   if constexpr (COMB)
     hipLaunchKernelGGL((hsv::hsv_verify_hc_kernel<WA, WAVES, PREFETCH>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
                        pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits,
-                       reinterpret_cast<uint4 *>(ws), comb_b);
+                       reinterpret_cast<uint4 *>(ws), comb_b, next);
   else
     hipLaunchKernelGGL((hsv::hsv_verify_mt_kernel<WA, WB, WAVES>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
                        pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits,

@@ -135,7 +135,237 @@ HSV_INL bool mps_abs_fits(const uint32_t x[N], int bits, uint32_t mag[5], uint32
   return fits;
 }
 
+
+// One (possibly partial) Euclid step on the full numbers: q = an under-
+// estimate of floor(a / b) (never over: the quotient comes from doubles and is
+// scaled down by 1 - 2^-40), r = a - q b; (a, b) <- (b, r) when r < b, else
+// a <- r (the next step continues the division).  Cofactors follow.
+HSV_INL void lat_exact_step(uint32_t a[8], uint32_t b[8], uint32_t ta[6], uint32_t tb[6], bool active) {
+  const double qd = mp_to_double<8>(a) / mp_to_double<8>(b);
+  double qf = floor(qd * (1.0 - 0x1p-40));
+  qf = qf < 1.0 ? 1.0 : (qf > 0x1p50 ? 0x1p50 : qf);
+  const uint64_t q = active ? (uint64_t)qf : 0u;
+  uint32_t r[8], tr[6];
+  mp_sub_mulq<8>(r, a, b, q);
+  mp_sub_mulq<6>(tr, ta, tb, q);
+  const bool swap = active && mp_lt<8>(r, b);
+  HSV_UNROLL
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t nb = swap ? r[i] : b[i];
+    a[i] = swap ? b[i] : (active ? r[i] : a[i]);
+    b[i] = nb;
+  }
+  HSV_UNROLL
+  for (int i = 0; i < 6; ++i) {
+    const uint32_t ntb = swap ? tr[i] : tb[i];
+    ta[i] = swap ? tb[i] : (active ? tr[i] : ta[i]);
+    tb[i] = ntb;
+  }
+}
+
+// Euclid until b < 2^128, one exact step per iteration (reference form).
+HSV_INL void lat_euclid_to_128(uint32_t a[8], uint32_t b[8], uint32_t ta[6], uint32_t tb[6]) {
+  HSV_NOUNROLL
+  for (int it = 0; it < 512; ++it) {
+    const bool active = (b[4] | b[5] | b[6] | b[7]) != 0;
+    if (!hsv_any(active)) break;
+    lat_exact_step(a, b, ta, tb, active);
+  }
+}
+
+// out = s * (|A| x - |B| y)  mod 2^(32N), s = -1 when A < 0 (or A == 0 < B),
+// else +1.
+// |A|, |B| < 2^31; x, y as N little-endian limbs (two's complement for the
+// cofactors).  For a Euclid cofactor matrix A and B have opposite signs (or
+// one is 0), so A x + B y = s (|A| x - |B| y).
+template <int N>
+HSV_INL void lat_combine(uint32_t out[N], const uint32_t x[N], const uint32_t y[N], int64_t A, int64_t B) {
+  const uint32_t ma = (uint32_t)(A < 0 ? -A : A), mb = (uint32_t)(B < 0 ? -B : B);
+  int64_t c = 0;
+  HSV_UNROLL
+  for (int i = 0; i < N; ++i) {
+    const int64_t t = (int64_t)((uint64_t)ma * x[i]) - (int64_t)((uint64_t)mb * y[i]) + c;
+    out[i] = (uint32_t)t;
+    c = t >> 32;
+  }
+  if (A < 0 || (A == 0 && B > 0)) {
+    uint64_t cc = 1;
+    HSV_UNROLL
+    for (int i = 0; i < N; ++i) {
+      cc += (uint64_t)(uint32_t)~out[i];
+      out[i] = (uint32_t)cc;
+      cc >>= 32;
+    }
+  }
+}
+
+// floor(n / d) estimate for integers 0 <= n < 2^53, 1 <= d < 2^53 held in
+// doubles: hardware reciprocal, then one exact remainder correction.  The
+// caller's step conditions reject any step whose quotient is not the true one,
+// so an estimate that is still off only ends the single-precision run early.
+HSV_INL double lat_floor_div(double n, double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double q = floor(n * __builtin_amdgcn_rcp(d));
+#else
+  double q = floor(n / d);
+#endif
+  const double r = fma(-q, d, n);
+  q += (r >= d) ? 1.0 : (r < 0.0 ? -1.0 : 0.0);
+  return q;
+}
+
+// bits [s, s + 52) of an 8-limb number, as an exact double (0 <= s <= 204)
+HSV_INL double lat_digits52(const uint32_t x[8], int s) {
+  const int w = s >> 5, sh = s & 31;
+  uint32_t l0 = 0, l1 = 0, l2 = 0;
+  HSV_UNROLL
+  for (int i = 0; i < 8; ++i) {
+    l0 = (i == w) ? x[i] : l0;
+    l1 = (i == w + 1) ? x[i] : l1;
+    l2 = (i == w + 2) ? x[i] : l2;
+  }
+  uint64_t v = (((uint64_t)l1 << 32) | l0) >> sh;
+  if (sh) v |= (uint64_t)l2 << (64 - sh);
+  return (double)(v & ((1ull << 52) - 1));
+}
+
+HSV_INL int lat_bitlen8(const uint32_t x[8]) {
+  int h = 0;
+  HSV_UNROLL
+  for (int i = 0; i < 8; ++i)
+    if (x[i] != 0) h = 32 * i + 32 - __builtin_clz(x[i]);
+  return h;
+}
+
+// Lehmer's algorithm (Knuth 4.5.2, Algorithm L) on 52-bit leading digits held
+// in doubles, stopping exactly at the first remainder below 2^128 like
+// lat_euclid_to_128.  Each round runs single-precision Euclid steps on the
+// leading digits while the two quotient bounds agree, the cofactors stay
+// below 2^31 and the new remainder is provably >= 2^128, then applies the
+// 2x2 cofactor matrix to (a, b) and (ta, tb); a round that can take no step
+// takes one exact full-precision step instead.  All lanes of a wave iterate
+// together; finished lanes are masked.
+HSV_INL void lat_lehmer_to_128(uint32_t a[8], uint32_t b[8], uint32_t ta[6], uint32_t tb[6]) {
+  HSV_NOUNROLL
+  for (int round = 0; round < 256; ++round) {
+    const bool active = (b[4] | b[5] | b[6] | b[7]) != 0;
+    if (!hsv_any(active)) break;
+    const int h = lat_bitlen8(a);
+    const int s = active ? h - 52 : 0;  // h >= 129 while active
+    double x = lat_digits52(a, s), y = lat_digits52(b, s);
+    const double thr = ldexp(1.0, 128 - s);
+    double A = 1.0, B = 0.0, C = 0.0, D = 1.0;
+    bool go = active;
+    HSV_NOUNROLL
+    for (int j = 0; j < 64; ++j) {
+      if (!hsv_any(go)) break;
+      // The true current pair is r0 = x + A al + B be, r1 = y + C al + D be
+      // (al, be in [0, 1): the digits cut off below 2^s); row entries have
+      // opposite signs, so over the box r2 = ny + nC al + nD be is smallest
+      // near ny + min(nC, nD) and r1 - r2 near (y - ny) + min(C - nC, D - nD).
+      // q is the true quotient iff 0 <= r2 < r1 for every (al, be): checked
+      // below, together with r2 >= 2^128 (never step past the first remainder
+      // under 2^128).  One division per step.
+      bool ok = go && y >= 1.0;
+      const double q = ok ? lat_floor_div(x, y) : 0.0;
+      const double nC = fma(-q, C, A), nD = fma(-q, D, B), ny = fma(-q, y, x);
+      ok = ok && q >= 1.0 && q < 0x1p30 && fabs(nC) < 0x1p31 && fabs(nD) < 0x1p31 &&
+           ny + fmin(nC, nD) >= thr && (y - ny) + fmin(C - nC, D - nD) >= 1.0;
+      if (ok) {
+        A = C; B = D; C = nC; D = nD;
+        x = y; y = ny;
+      }
+      go = ok;
+    }
+    const bool matrix = active && B != 0.0;
+    if (hsv_any(matrix)) {
+      uint32_t na[8], nb[8], nta[6], ntb[6];
+      const int64_t iA = (int64_t)A, iB = (int64_t)B, iC = (int64_t)C, iD = (int64_t)D;
+      lat_combine<8>(na, a, b, iA, iB);
+      lat_combine<8>(nb, a, b, iC, iD);
+      lat_combine<6>(nta, ta, tb, iA, iB);
+      lat_combine<6>(ntb, ta, tb, iC, iD);
+      HSV_UNROLL
+      for (int i = 0; i < 8; ++i) {
+        a[i] = matrix ? na[i] : a[i];
+        b[i] = matrix ? nb[i] : b[i];
+      }
+      HSV_UNROLL
+      for (int i = 0; i < 6; ++i) {
+        ta[i] = matrix ? nta[i] : ta[i];
+        tb[i] = matrix ? ntb[i] : tb[i];
+      }
+    }
+    const bool exact = active && B == 0.0;
+    if (hsv_any(exact)) lat_exact_step(a, b, ta, tb, exact);
+  }
+}
+
+
+// c0s == c1 k (mod 8l), c0s = (c0_neg ? -c0 : c0)?  Checked as
+// F = c1 k - c0s + 8l * 2^140 (>= 0):  F == 0 mod 8  and  F == 0 mod l.
+// The reduction maintains the congruence by construction; this check makes
+// a wrong pair cost only the full-length path, never a wrong flag.
+HSV_INL bool lat_congruent(const sc &k, const LatOut &o) {
+  uint32_t f[16];
+  HSV_UNROLL
+  for (int i = 0; i < 16; ++i) f[i] = 0;
+  HSV_UNROLL
+  for (int i = 0; i < 5; ++i) {  // c1 * k
+    uint64_t c = 0;
+    HSV_UNROLL
+    for (int j = 0; j < 8; ++j) {
+      c = (uint64_t)o.c1[i] * k.v[j] + f[i + j] + (c >> 32);
+      f[i + j] = (uint32_t)c;
+    }
+    f[i + 8] = (uint32_t)(c >> 32);
+  }
+  {  // + 8l * 2^140 = l << 143: limbs 4.. of (l << 15)
+    uint32_t l[8];
+    sc_l(l);
+    uint64_t c = 0;
+    HSV_UNROLL
+    for (int i = 0; i < 9; ++i) {
+      const uint32_t li = (i < 8 ? (l[i] << 15) : 0u) | (i >= 1 ? (l[i - 1] >> 17) : 0u);
+      c += (uint64_t)f[4 + i] + li;
+      f[4 + i] = (uint32_t)c;
+      c >>= 32;
+    }
+    HSV_UNROLL
+    for (int i = 13; i < 16; ++i) {
+      c += f[i];
+      f[i] = (uint32_t)c;
+      c >>= 32;
+    }
+  }
+  {  // -/+ c0
+    int64_t c = 0;
+    HSV_UNROLL
+    for (int i = 0; i < 16; ++i) {
+      const int64_t ci = i < 5 ? (int64_t)o.c0[i] : 0;
+      c += (int64_t)f[i] + (o.c0_neg ? ci : -ci);
+      f[i] = (uint32_t)c;
+      c >>= 32;
+    }
+  }
+  const sc r = sc_reduce512(f);
+  uint32_t nz = f[0] & 7u;
+  HSV_UNROLL
+  for (int i = 0; i < 8; ++i) nz |= r.v[i];
+  return nz == 0;
+}
+
 HSV_INL LatOut lattice_reduce(const sc &k) {
+#ifdef HSV_TIMING_STUB_LATTICE  // tools/phase_probe.py only: wrong results, timing share of the reduction
+  {
+    LatOut o;
+    for (int i = 0; i < 5; ++i) { o.c0[i] = i < 4 ? k.v[i] : 0u; o.c1[i] = i < 4 ? k.v[4 + i] : 0u; }
+    o.c1[0] |= 1u;
+    o.c0_neg = 0;
+    o.ok = 1;
+    return o;
+  }
+#endif
   // a = N = 8l, ta = 0;  b = k, tb = 1.   Invariant: a == ta*k, b == tb*k (mod N)
   uint32_t a[8], b[8], ta[6], tb[6];
   {
@@ -154,32 +384,11 @@ HSV_INL LatOut lattice_reduce(const sc &k) {
     ta[i] = 0;
     tb[i] = i == 0 ? 1u : 0u;
   }
-  // Euclid until b < 2^128 (all lanes of a wave iterate together)
-  HSV_NOUNROLL
-  for (int it = 0; it < 512; ++it) {
-    const bool active = (b[4] | b[5] | b[6] | b[7]) != 0;
-    if (!hsv_any(active)) break;
-    const double qd = mp_to_double<8>(a) / mp_to_double<8>(b);
-    double qf = floor(qd * (1.0 - 0x1p-40));
-    qf = qf < 1.0 ? 1.0 : (qf > 0x1p50 ? 0x1p50 : qf);
-    const uint64_t q = active ? (uint64_t)qf : 0u;
-    uint32_t r[8], tr[6];
-    mp_sub_mulq<8>(r, a, b, q);
-    mp_sub_mulq<6>(tr, ta, tb, q);
-    const bool swap = active && mp_lt<8>(r, b);
-    HSV_UNROLL
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t nb = swap ? r[i] : b[i];
-      a[i] = swap ? b[i] : (active ? r[i] : a[i]);
-      b[i] = nb;
-    }
-    HSV_UNROLL
-    for (int i = 0; i < 6; ++i) {
-      const uint32_t ntb = swap ? tr[i] : tb[i];
-      ta[i] = swap ? tb[i] : (active ? tr[i] : ta[i]);
-      tb[i] = ntb;
-    }
-  }
+#ifdef HSV_LATTICE_EUCLID
+  lat_euclid_to_128(a, b, ta, tb);
+#else
+  lat_lehmer_to_128(a, b, ta, tb);
+#endif
   LatOut o;
   o.ok = 0;
   o.c0_neg = 0;
@@ -249,6 +458,7 @@ HSV_INL LatOut lattice_reduce(const sc &k) {
     o.c0[i] = c0mag[i];
     o.c1[i] = c1mag[i];
   }
+  o.ok = (o.ok && lat_congruent(k, o)) ? 1u : 0u;
   return o;
 }
 

@@ -51,8 +51,10 @@ HSV_INL uint32_t flags_byte(uint32_t s_ok, uint32_t a_ok, uint32_t r_ok, uint32_
 // Straus over NV (1 or 2) variable bases from VT tables 0..NV-1, scalars given
 // as recoded digit registers d[v] (L limbs, top window at the top bit).
 // Returns the accumulator with T valid (the comb phase follows).
+// flip_last: negate every digit of the last scalar (its table holds the
+// negated base).
 template <int WA, int NW, int L, int NV, bool PREFETCH, class VT>
-HSV_INL ge_ext straus_vt(uint32_t d[NV][L], VT &vt) {
+HSV_INL ge_ext straus_vt(uint32_t d[NV][L], VT &vt, uint32_t flip_last = 0) {
   constexpr int TS = 1 << (WA - 1);
   ge_ext q = ge_identity();
   HSV_NOUNROLL
@@ -61,6 +63,7 @@ HSV_INL ge_ext straus_vt(uint32_t d[NV][L], VT &vt) {
     HSV_UNROLL
     for (int v = 0; v < NV; ++v) {
       m[v] = digit_mag<TS>(d[v][L - 1] >> (32 - WA), neg[v]);
+      if (v == NV - 1) neg[v] ^= flip_last;
       limbs_shl<L>(d[v], WA);
     }
     if constexpr (PREFETCH) {
@@ -146,9 +149,9 @@ HSV_INL uint32_t verify_one_half_comb(const uint32_t pk[8], const uint32_t sig[1
   uint32_t h[16];
   sha512_96(sig, pk, msg, h);
   const sc k = sc_reduce512(h);
-  const LatOut lat = lattice_reduce(k);
-  fallback = !lat.ok;
 
+  // tables first (R and A are dead afterwards), the lattice reduction after
+  // them, so its outputs are not live across the two root chains
   uint32_t a_ok, small_a, r_ok, small_r;
   {
     fe x, y;
@@ -160,12 +163,14 @@ HSV_INL uint32_t verify_one_half_comb(const uint32_t pk[8], const uint32_t sig[1
     fe x, y;
     a_ok = ge_decompress(pk, x, y);
     small_a = a_ok & y_is_small_order(y);
-    vt_build<TS>(vt, 1, fe_carry(fe_select(fe_neg(x), x, lat.c0_neg)), y);
+    vt_build<TS>(vt, 1, fe_carry(fe_neg(x)), y);  // -A; the sign of c0 flips the digits
   }
+  const LatOut lat = lattice_reduce(k);
+  fallback = !lat.ok;
   uint32_t d[2][5];
   recode_top5<WA, G::NW>(lat.c1, d[0]);
   recode_top5<WA, G::NW>(lat.c0, d[1]);
-  ge_ext q = straus_vt<WA, G::NW, 5, 2, PREFETCH>(d, vt);
+  ge_ext q = straus_vt<WA, G::NW, 5, 2, PREFETCH>(d, vt, lat.c0_neg);
   const sc b = sc_mul_small(lat.c1, sig + 8);
   q = comb_add_b(q, b.v, tb);
   const uint32_t same = fe_is_zero(q.X) & fe_eq(q.Y, q.Z);  // Q == O
