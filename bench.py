@@ -38,6 +38,26 @@ sys.path.insert(0, os.path.join(ROOT, "hotstuff-digital-signature-benchmarking_a
 
 WORK_MACS = 192_000          # u32 MACs per verification
 IO_BYTES = 129               # algorithmic HBM bytes per verification (128 in + 1 out)
+# int32 VALU peak: 256 CUs x 4 SIMDs x 16 lanes/clk (v_mad_u64_u32 issues at
+# half the f32 rate on gfx950, profiles/r01e_ubench) x 2.4 GHz max clock
+# (MI355X_MICROARCH.md chip table) = 39.3 T MAC/s
+PEAK_MACS = 256 * 4 * 16 * 2.4e9
+PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "latest_pmc_traffic.json")
+
+
+def pmc_traffic(variant, n):
+    """HBM bytes per launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE
+    passes (tools/pmc_traffic.sh), when they were taken on this kernel variant
+    and batch size; gfx950 correction: FETCH_SIZE counts half the bytes of
+    16-byte-per-lane reads (MI355X_MICROARCH.md), so it is doubled."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if t.get("variant") != variant or t.get("n") != n:
+        return None, None
+    return 2 * t["fetch_bytes_per_launch"] + t["write_bytes_per_launch"], t.get("source")
 
 
 def log(*a):
@@ -178,7 +198,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=1 << 20, help="triples per GPU")
     ap.add_argument("--variant", type=int, default=None)
-    ap.add_argument("--cpu-sample", type=int, default=1 << 17)
+    ap.add_argument("--cpu-sample", type=int, default=1 << 20,
+                    help="triples the CPU port verifies (default: the whole C4 batch, about 3 s on 16 cores)")
     ap.add_argument("--qc-reps", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-qc", action="store_true")
@@ -254,8 +275,9 @@ def main():
 
     total = a.n * world * a.steps
     value = total / elapsed
-    peak = verifier.measure_mad_peak()
+    probe = verifier.measure_mad_peak()
     achieved = a.n * WORK_MACS / (kernel_ms * 1e-3)
+    traffic, traffic_src = pmc_traffic(verifier.get_variant(), a.n)
     out = {
         "metric": "Ed25519 verifies/sec at batch 2^20 per GPU (bit-exact ed25519-dalek verify_strict flags)",
         "value": value,
@@ -279,10 +301,14 @@ def main():
         "roofline": {
             "bound": "valu",
             "achieved": achieved / 1e12,
-            "peak": peak / 1e12,
+            "peak": PEAK_MACS / 1e12,
             "unit": "T u32-MAC/s",
-            "frac": achieved / peak if peak > 0 else None,
-            "traffic": None,
+            "frac": achieved / PEAK_MACS,
+            "traffic": traffic,
+            "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+            "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": a.n * IO_BYTES,
+            "peak_probe": probe / 1e12,
             "work_per_verify": f"{WORK_MACS} u32 MACs (SURVEY 8(d)); {IO_BYTES} HBM bytes algorithmic",
             "kernel_ms": kernel_ms,
         },

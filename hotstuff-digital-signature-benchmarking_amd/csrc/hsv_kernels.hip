@@ -261,25 +261,27 @@ hsv_verify_hc_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
 }
 
 // ---- v_mad_u64_u32 issue-rate probe -------------------------------------
-constexpr int kPeakChains = 8;
-constexpr int kPeakIters = 4096;
+// 8 independent accumulation chains, 16 mads per asm statement (the compiler
+// puts an s_nop after every asm statement that writes an SGPR, so one mad per
+// statement would measure mad + s_nop).
+constexpr int kPeakIters = 2048;
 
+#define HSV_PEAK_MAD(c) "v_mad_u64_u32 %" #c ", s[40:41], %8, %9, %" #c "\n\t"
 __global__ void __launch_bounds__(256) hsv_mad_peak_kernel(uint32_t *sink, uint32_t seed) {
   const uint32_t t = threadIdx.x + blockIdx.x * blockDim.x + seed;
-  uint64_t x[kPeakChains];
+  uint64_t x0 = t, x1 = t + 1, x2 = t + 2, x3 = t + 3, x4 = t + 4, x5 = t + 5, x6 = t + 6, x7 = t + 7;
   const uint32_t a = t | 1u, b = t * 3u + 7u;
-#pragma unroll
-  for (int c = 0; c < kPeakChains; ++c) x[c] = t + c;
-  for (int it = 0; it < kPeakIters; ++it) {
-#pragma unroll
-    for (int c = 0; c < kPeakChains; ++c)
-      asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(x[c]) : "v"(a), "v"(b) : "vcc");
-  }
-  uint32_t r = 0;
-#pragma unroll
-  for (int c = 0; c < kPeakChains; ++c) r ^= (uint32_t)(x[c] ^ (x[c] >> 32));
-  if (r == 0x9e3779b9u) sink[0] = r;
+  for (int it = 0; it < kPeakIters; ++it)
+    asm volatile(HSV_PEAK_MAD(0) HSV_PEAK_MAD(1) HSV_PEAK_MAD(2) HSV_PEAK_MAD(3) HSV_PEAK_MAD(4) HSV_PEAK_MAD(5)
+                 HSV_PEAK_MAD(6) HSV_PEAK_MAD(7) HSV_PEAK_MAD(0) HSV_PEAK_MAD(1) HSV_PEAK_MAD(2) HSV_PEAK_MAD(3)
+                 HSV_PEAK_MAD(4) HSV_PEAK_MAD(5) HSV_PEAK_MAD(6) HSV_PEAK_MAD(7)
+                 : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7)
+                 : "v"(a), "v"(b)
+                 : "s40", "s41");
+  const uint64_t r = x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7;
+  if ((uint32_t)(r ^ (r >> 32)) == 0x9e3779b9u) sink[0] = 1u;
 }
+#undef HSV_PEAK_MAD
 
 }  // namespace hsv
 
@@ -420,7 +422,7 @@ extern "C" double hsv_launch_mad_peak(int device_cus) {
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   (void)hipFree(sink);
-  const double macs = (double)reps * grid * 256.0 * hsv::kPeakIters * hsv::kPeakChains;
+  const double macs = (double)reps * grid * 256.0 * hsv::kPeakIters * 16.0;
   return ms > 0.f ? macs / (ms * 1e-3) : -1.0;
 }
 
