@@ -46,6 +46,7 @@ struct DevCtx {
   int device = 0;
   int cus = 0;
   uint32_t *d_btable = nullptr;  // comb table of B (committee path), built lazily
+  uint32_t *d_btable16 = nullptr;  // wide comb table of B (generic kernels 15, 16), built lazily
   hipStream_t stream = nullptr;
   uint8_t *d_buf = nullptr;
   size_t d_cap = 0;
@@ -59,7 +60,7 @@ struct Global {
   bool inited = false;
   int ndev = 0;
   std::vector<DevCtx *> ctx;
-  std::atomic<int> variant{13};  // fastest measured: half-size scalars + B comb, WA=4, 3 waves/SIMD
+  std::atomic<int> variant{15};  // fastest measured: half-size scalars + wide B comb, WA=4, 3 waves/SIMD
 };
 
 Global &G() {
@@ -142,6 +143,35 @@ int ensure_btable(DevCtx &c) {
   return HSV_OK;
 }
 
+// wide (16-bit digit) comb table of B on this device (caller holds c.mu and
+// has set the device): 48 MiB, built once
+int ensure_btable16(DevCtx &c) {
+  if (c.d_btable16) return HSV_OK;
+  uint32_t *d_tab = nullptr, *d_tmp = nullptr;
+  hipError_t e = hipMalloc(&d_tab, hsv_comb16_table_bytes());
+  if (e == hipSuccess) e = hipMalloc(&d_tmp, hsv_comb16_tmp_bytes());
+  if (e == hipSuccess) e = hsv_launch_comb16_build(d_tab, d_tmp, c.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c.stream);
+  if (d_tmp) (void)hipFree(d_tmp);
+  if (e != hipSuccess) {
+    if (d_tab) (void)hipFree(d_tab);
+    return hip_fail("building the wide B comb table", e);
+  }
+  c.d_btable16 = d_tab;
+  return HSV_OK;
+}
+
+// the B comb table `variant` reads (nullptr when none); caller holds c.mu
+int comb_table_for(DevCtx &c, int variant, const uint32_t **out) {
+  *out = nullptr;
+  const int bits = hsv_variant_needs_comb(variant);
+  if (bits == 0) return HSV_OK;
+  const int rc = bits == 16 ? ensure_btable16(c) : ensure_btable(c);
+  if (rc != HSV_OK) return rc;
+  *out = bits == 16 ? c.d_btable16 : c.d_btable;
+  return HSV_OK;
+}
+
 
 // Host records: item i at pk + i*pk_stride, sig + i*sig_stride, msg + i*msg_stride
 // (msg_stride 0 = shared).  Runs [0, n) on one device, chunk by chunk.
@@ -159,10 +189,9 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
   int rc = ctx_prepare(c, total, total);
   if (rc != HSV_OK) return rc;
   const int variant = G().variant.load();
-  if (hsv_variant_needs_comb(variant)) {
-    rc = ensure_btable(c);
-    if (rc != HSV_OK) return rc;
-  }
+  const uint32_t *comb_b = nullptr;
+  rc = comb_table_for(c, variant, &comb_b);
+  if (rc != HSV_OK) return rc;
   for (size_t base = 0; base < n; base += chunk) {
     const size_t m = std::min(chunk, n - base);
     uint8_t *h = c.h_buf;
@@ -178,7 +207,7 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
     hipError_t e = hipMemcpyAsync(c.d_buf, h, in_bytes, hipMemcpyHostToDevice, c.stream);
     if (e != hipSuccess) return hip_fail("hipMemcpyAsync H2D", e);
     e = hsv_launch_verify(variant, c.d_buf + pk_off, 32, c.d_buf + sig_off, 64, c.d_buf + msg_off,
-                          msg_stride ? 32 : 0, (uint32_t)m, c.d_buf + flag_off, nullptr, c.d_btable, c.stream);
+                          msg_stride ? 32 : 0, (uint32_t)m, c.d_buf + flag_off, nullptr, comb_b, c.stream);
     if (e != hipSuccess) return hip_fail("verify kernel launch", e);
     e = hipMemcpyAsync(h + flag_off, c.d_buf + flag_off, m, hipMemcpyDeviceToHost, c.stream);
     if (e != hipSuccess) return hip_fail("hipMemcpyAsync D2H", e);
@@ -240,8 +269,10 @@ void hsv_shutdown(void) {
       if (c->d_buf) (void)hipFree(c->d_buf);
       if (c->h_buf) (void)hipHostFree(c->h_buf);
       if (c->d_btable) (void)hipFree(c->d_btable);
+      if (c->d_btable16) (void)hipFree(c->d_btable16);
     }
     c->d_btable = nullptr;
+    c->d_btable16 = nullptr;
     c->stream = nullptr;
     c->d_buf = c->h_buf = nullptr;
     c->d_cap = c->h_cap = 0;
@@ -326,9 +357,8 @@ int hsv_verify_device_bits(const uint8_t *d_pk, size_t pk_stride, const uint8_t 
     DevCtx &c = *G().ctx[dev];
     std::lock_guard<std::mutex> lk(c.mu);
     rc = ctx_prepare(c, 0, 0);
-    if (rc == HSV_OK) rc = ensure_btable(c);
+    if (rc == HSV_OK) rc = comb_table_for(c, variant, &comb_b);
     if (rc != HSV_OK) return rc;
-    comb_b = c.d_btable;
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   for (size_t base = 0; base < n; base += kChunk) {

@@ -64,6 +64,76 @@ HSV_INL void comb_build_position(const ge_ext &base, uint32_t *out, uint32_t *tm
   }
 }
 
+// Wide comb of B for the generic kernels: 16-bit signed digits, so [b]B for
+// b < 2^256 is 16 mixed additions instead of 32.
+//   T16[j][m] = [m * 2^(16j)] B,   j in [0, 16), m in [1, 32768]
+// Entry (j, m) at word ((j * 32768) + m - 1) * 24 (same 24-word format),
+// 16 * 32768 * 96 B = 48 MiB per device: MALL-resident, one 96-byte read per
+// addition.  Built on the GPU in chunks of 128 consecutive multiples, one
+// chunk per lane (hsv_comb16_build_kernel).
+constexpr int kComb16Pos = 16;
+constexpr int kComb16Ent = 1 << 15;
+constexpr int kComb16Chunk = 128;
+constexpr int kComb16ChunksPerPos = kComb16Ent / kComb16Chunk;  // 256
+constexpr uint64_t kComb16TableWords = (uint64_t)kComb16Pos * kComb16Ent * kCombEntryWords;
+
+// Fill kComb16Chunk entries [start + m * base] (m = 1..128) of a run of the
+// table: projective sums first, then one batched inversion.
+HSV_INL void comb_build_run(const ge_ext &start, const ge_ext &base, uint32_t *out, uint32_t *tmp) {
+  const ge_cached bc = ge_to_cached(base);
+  ge_ext acc = start;
+  fe pp = fe_small(1);
+  HSV_NOUNROLL
+  for (int m = 1; m <= kComb16Chunk; ++m) {
+    acc = ge_add_cached<true>(acc, bc);
+    uint32_t *e = out + (m - 1) * kCombEntryWords;
+    fe_pack(acc.X, e);
+    fe_pack(acc.Y, e + 8);
+    fe_pack(acc.Z, e + 16);
+    pp = fe_mul(pp, acc.Z);
+    fe_pack(pp, tmp + (m - 1) * 8);
+  }
+  fe inv = fe_invert(pp);
+  HSV_NOUNROLL
+  for (int m = kComb16Chunk; m >= 1; --m) {
+    uint32_t *e = out + (m - 1) * kCombEntryWords;
+    const fe X = fe_from_words_masked(e), Y = fe_from_words_masked(e + 8), Z = fe_from_words_masked(e + 16);
+    fe zinv = inv;
+    if (m > 1) {
+      zinv = fe_mul(inv, fe_from_words_masked(tmp + (m - 2) * 8));
+      inv = fe_mul(inv, Z);
+    }
+    const fe x = fe_mul(X, zinv), y = fe_mul(Y, zinv);
+    fe_pack(fe_add(y, x), e);
+    fe_pack(fe_sub(y, x), e + 8);
+    fe_pack(fe_mul(fe_mul(x, y), fe_d2()), e + 16);
+  }
+}
+
+// One chunk (position j, chunk c) of the wide B table: entries
+// m = 128c + 1 .. 128c + 128 of position j.  bx, by: affine B.
+HSV_INL void comb16_build_chunk(const fe &bx, const fe &by, int j, uint32_t c, uint32_t *table, uint32_t *tmp) {
+  ge_ext base;
+  base.X = bx;
+  base.Y = by;
+  base.Z = fe_small(1);
+  base.T = fe_mul(bx, by);
+  HSV_NOUNROLL
+  for (int i = 0; i < 16 * j; ++i) base = ge_dbl<true>(base);  // [2^(16j)]B
+  ge_ext step = base;
+  HSV_NOUNROLL
+  for (int i = 0; i < 7; ++i) step = ge_dbl<true>(step);  // [128 * 2^(16j)]B
+  const ge_cached sc128 = ge_to_cached(step);
+  ge_ext start = ge_identity();
+  HSV_NOUNROLL
+  for (int b = 7; b >= 0; --b) {  // start = [128c] base
+    start = ge_dbl<true>(start);
+    if ((c >> b) & 1u) start = ge_add_cached<true>(start, sc128);
+  }
+  comb_build_run(start, base,
+                 table + ((uint64_t)j * kComb16Ent + (uint64_t)c * kComb16Chunk) * kCombEntryWords, tmp);
+}
+
 // [2^(8j)] P for a decompressed affine P (negated when neg), extended coords.
 HSV_INL ge_ext comb_position_base(const fe &x, const fe &y, uint32_t neg, int j) {
   ge_ext p;

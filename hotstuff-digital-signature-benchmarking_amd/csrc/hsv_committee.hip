@@ -68,7 +68,32 @@ hsv_comb_verify_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__re
   flags_out[i] = kvalid ? (uint8_t)f : (uint8_t)0;
 }
 
+// one lane per (position j, chunk c) of the wide B table; j is wave-uniform
+// (256 chunks per position)
+__global__ void __launch_bounds__(256) hsv_comb16_build_kernel(uint32_t *__restrict__ table,
+                                                             uint32_t *__restrict__ tmp) {
+  const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t j = id / (uint32_t)kComb16ChunksPerPos, c = id % (uint32_t)kComb16ChunksPerPos;
+  if (j >= (uint32_t)kComb16Pos) return;
+  const uint32_t bw[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
+                          0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
+  fe x, y;
+  (void)ge_decompress(bw, x, y);
+  comb16_build_chunk(x, y, (int)j, c, table, tmp + (uint64_t)id * kComb16Chunk * 8);
+}
+
 }  // namespace hsv
+
+extern "C" hipError_t hsv_launch_comb16_build(uint32_t *table, uint32_t *tmp, hipStream_t stream) {
+  const uint32_t lanes = (uint32_t)(hsv::kComb16Pos * hsv::kComb16ChunksPerPos);
+  hipLaunchKernelGGL(hsv::hsv_comb16_build_kernel, dim3(lanes / 256u), dim3(256), 0, stream, table, tmp);
+  return hipGetLastError();
+}
+
+extern "C" uint64_t hsv_comb16_table_bytes(void) { return hsv::kComb16TableWords * 4ull; }
+extern "C" uint64_t hsv_comb16_tmp_bytes(void) {
+  return (uint64_t)hsv::kComb16Pos * hsv::kComb16ChunksPerPos * hsv::kComb16Chunk * 8ull * 4ull;
+}
 
 extern "C" hipError_t hsv_launch_comb_build(const uint8_t *encs, uint32_t nkeys, uint32_t negate,
                                             uint32_t *tables, uint32_t *tmp, uint8_t *key_flags,

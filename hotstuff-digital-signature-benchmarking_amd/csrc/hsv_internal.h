@@ -13,7 +13,9 @@ hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t pk_stride,
                              uint64_t sig_stride, const uint8_t *msg, uint64_t msg_stride,
                              uint32_t n, uint8_t *flags_out, uint32_t *strict_bits,
                              const uint32_t *comb_b, hipStream_t stream);
-// variants that read the B comb table (comb_b must be non-null for them)
+// digit width of the B comb table a variant reads: 8 (hsv_comb_table_bytes),
+// 16 (the wide table, hsv_comb16_table_bytes) or 0 (none); comb_b must be
+// that table for such variants
 int hsv_variant_needs_comb(int variant);
 
 // Time the v_mad_u64_u32 probe on the current device; MAC/s.
@@ -35,6 +37,10 @@ hipError_t hsv_launch_comb_verify(const uint32_t *key_idx, const uint8_t *sig, u
                                   const uint32_t *btable, uint8_t *flags_out, hipStream_t stream);
 uint64_t hsv_comb_table_bytes(void);
 uint64_t hsv_comb_tmp_bytes(uint32_t nkeys);
+// wide (16-bit digit) comb table of B, hsv_comb.hpp
+hipError_t hsv_launch_comb16_build(uint32_t *table, uint32_t *tmp, hipStream_t stream);
+uint64_t hsv_comb16_table_bytes(void);
+uint64_t hsv_comb16_tmp_bytes(void);
 #ifdef __cplusplus
 }
 #endif

@@ -210,7 +210,7 @@ hsv_verify_mt_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
 // per wave, 64 items at a time, from the counter `next` (zero at launch): a
 // wave slowed by a lane on the full-length fallback, or one that started
 // late, simply takes fewer batches, so the grid finishes together.
-template <int WA, int WAVES, bool PREFETCH>
+template <int WA, int WAVES, bool PREFETCH, int CB>
 __global__ void __launch_bounds__(kBlock, WAVES)
 hsv_verify_hc_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
                      const uint8_t *__restrict__ sig, uint64_t sig_stride,
@@ -247,8 +247,8 @@ hsv_verify_hc_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
       msgw[4] = m1.x; msgw[5] = m1.y; msgw[6] = m1.z; msgw[7] = m1.w;
     }
     bool fallback = false;
-    uint32_t f = verify_one_half_comb<WA, PREFETCH>(pkw, sigw, msgw, comb_b, vt, fallback);
-    if (fallback) f = verify_one_full_comb<WA, PREFETCH>(pkw, sigw, msgw, comb_b, vt);
+    uint32_t f = verify_one_half_comb<WA, PREFETCH, CB>(pkw, sigw, msgw, comb_b, vt, fallback);
+    if (fallback) f = verify_one_full_comb<WA, PREFETCH, CB>(pkw, sigw, msgw, comb_b, vt);
 
     if (valid && flags_out) flags_out[idx] = (uint8_t)f;
     if (strict_bits) {
@@ -301,18 +301,20 @@ __global__ void __launch_bounds__(256) hsv_mad_peak_kernel(uint32_t *sink, uint3
 //  12: as 10 with WA=5
 //  13: as 11, 3 waves/SIMD, table entries loaded at their addition (no prefetch)
 //  14: as 11, 2 waves/SIMD, no prefetch
-extern "C" int hsv_num_variants(void) { return 15; }
+//  15: as 13 with the wide (16-bit digit, 48 MiB) comb table of B
+//  16: as 14 with the wide comb table
+extern "C" int hsv_num_variants(void) { return 17; }
 
 namespace {
 
 // Persistent-grid launch of hsv_verify_mt_kernel with a stream-ordered
 // workspace for the per-lane tables (freed on the same stream).
-template <int WA, int WB, int WAVES, bool COMB, bool PREFETCH = true>
+template <int WA, int WB, int WAVES, bool COMB, bool PREFETCH = true, int CB = 8>
 hipError_t launch_mt(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
                      const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
                      uint32_t *strict_bits, const uint32_t *comb_b, hipStream_t stream) {
   const void *kern;
-  if constexpr (COMB) kern = reinterpret_cast<const void *>(hsv::hsv_verify_hc_kernel<WA, WAVES, PREFETCH>);
+  if constexpr (COMB) kern = reinterpret_cast<const void *>(hsv::hsv_verify_hc_kernel<WA, WAVES, PREFETCH, CB>);
   else kern = reinterpret_cast<const void *>(hsv::hsv_verify_mt_kernel<WA, WB, WAVES>);
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -350,7 +352,7 @@ hipError_t launch_mt(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
     if (e != hipSuccess) return e;
   }
   if constexpr (COMB)
-    hipLaunchKernelGGL((hsv::hsv_verify_hc_kernel<WA, WAVES, PREFETCH>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
+    hipLaunchKernelGGL((hsv::hsv_verify_hc_kernel<WA, WAVES, PREFETCH, CB>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
                        pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits,
                        reinterpret_cast<uint4 *>(ws), comb_b, next);
   else
@@ -395,6 +397,10 @@ extern "C" hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t
       return launch_mt<4, 4, 3, true, false>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
     case 14: if (!comb_b) return hipErrorInvalidValue;
       return launch_mt<4, 4, 2, true, false>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
+    case 15: if (!comb_b) return hipErrorInvalidValue;
+      return launch_mt<4, 4, 3, true, false, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
+    case 16: if (!comb_b) return hipErrorInvalidValue;
+      return launch_mt<4, 4, 2, true, false, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
 #undef HSV_LAUNCH_MT
     default: return hipErrorInvalidValue;
   }
@@ -426,4 +432,8 @@ extern "C" double hsv_launch_mad_peak(int device_cus) {
   return ms > 0.f ? macs / (ms * 1e-3) : -1.0;
 }
 
-extern "C" int hsv_variant_needs_comb(int variant) { return variant >= 10 && variant <= 14; }
+extern "C" int hsv_variant_needs_comb(int variant) {
+  if (variant >= 10 && variant <= 14) return 8;
+  if (variant >= 15 && variant <= 16) return 16;
+  return 0;
+}

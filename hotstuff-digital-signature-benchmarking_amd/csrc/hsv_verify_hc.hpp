@@ -21,19 +21,26 @@
 
 namespace hsv {
 
-// q += [s]B for a scalar s < 2^256 (8 words) via the B comb table (32 signed
-// radix-2^8 digits, consumed from the bottom).
+// q += [s]B for a scalar s < 2^256 (8 words) via a comb table of B: CB = 8,
+// the 384 KiB table (32 signed radix-2^8 digits), or CB = 16, the 48 MiB
+// wide table (16 signed radix-2^16 digits); digits consumed from the bottom.
+// (s >= 2^256 - C is only reached for non-canonical s, whose flags do not
+// depend on the equation.)
+template <int CB>
 HSV_INL ge_ext comb_add_b(ge_ext q, const uint32_t s[8], const uint32_t *tb) {
+  static_assert(CB == 8 || CB == 16, "comb digit width");
+  constexpr int NP = 256 / CB;
+  constexpr int ENT = 1 << (CB - 1);
   uint32_t sr[9];
-  recode_add<9, 8, kCombPos>(s, 8, sr);
+  recode_add<9, CB, NP>(s, 8, sr);
   HSV_NOUNROLL
-  for (int j = 0; j < kCombPos; ++j) {
-    const uint32_t cb = sr[0] & 0xffu;
+  for (int j = 0; j < NP; ++j) {
+    const uint32_t cb = sr[0] & ((1u << CB) - 1u);
     HSV_UNROLL
-    for (int i = 0; i < 8; ++i) sr[i] = (sr[i] >> 8) | (sr[i + 1] << 24);
-    sr[8] >>= 8;
-    const CombPosTab tpb{tb + (uint64_t)j * kCombEnt * kCombEntryWords};
-    q = ge_add_niels<true>(q, select_niels<8>(tpb, cb));
+    for (int i = 0; i < 8; ++i) sr[i] = (sr[i] >> CB) | (sr[i + 1] << (32 - CB));
+    sr[8] >>= CB;
+    const CombPosTab tpb{tb + (uint64_t)j * ENT * kCombEntryWords};
+    q = ge_add_niels<true>(q, select_niels<CB>(tpb, cb));
   }
   return q;
 }
@@ -110,7 +117,7 @@ HSV_INL ge_ext straus_vt(uint32_t d[NV][L], VT &vt, uint32_t flip_last = 0) {
 
 // Full-length path (fallback): [k](-A) by Straus with table 0, [s]B by comb,
 // compared with R as points (dalek's check, verify_one's flags).
-template <int WA, bool PREFETCH = true, class VT>
+template <int WA, bool PREFETCH = true, int CB = 8, class VT>
 HSV_INL uint32_t verify_one_full_comb(const uint32_t pk[8], const uint32_t sig[16], const uint32_t msg[8],
                                       const uint32_t *tb, VT &vt) {
   using G = Windows<WA, WA>;
@@ -126,7 +133,7 @@ HSV_INL uint32_t verify_one_full_comb(const uint32_t pk[8], const uint32_t sig[1
   recode_add<8, WA, G::NA>(k.v, 8, d[0]);
   limbs_shl_const<8, 256 - G::KBITS>(d[0]);
   ge_ext q = straus_vt<WA, G::NA, 8, 1, PREFETCH>(d, vt);
-  q = comb_add_b(q, sig + 8, tb);
+  q = comb_add_b<CB>(q, sig + 8, tb);
   fe rx, ry;
   const uint32_t r_ok = ge_decompress(sig, rx, ry);
   const uint32_t small_r = r_ok & y_is_small_order(ry);
@@ -140,7 +147,7 @@ struct HalfCombWindows {
   static_assert(BITS <= 160 && BITS >= kLatMaxBits + 2, "scalar bound vs loop length");
 };
 
-template <int WA, bool PREFETCH = true, class VT>
+template <int WA, bool PREFETCH = true, int CB = 8, class VT>
 HSV_INL uint32_t verify_one_half_comb(const uint32_t pk[8], const uint32_t sig[16], const uint32_t msg[8],
                                       const uint32_t *tb, VT &vt, bool &fallback) {
   using G = HalfCombWindows<WA>;
@@ -172,7 +179,7 @@ HSV_INL uint32_t verify_one_half_comb(const uint32_t pk[8], const uint32_t sig[1
   recode_top5<WA, G::NW>(lat.c0, d[1]);
   ge_ext q = straus_vt<WA, G::NW, 5, 2, PREFETCH>(d, vt, lat.c0_neg);
   const sc b = sc_mul_small(lat.c1, sig + 8);
-  q = comb_add_b(q, b.v, tb);
+  q = comb_add_b<CB>(q, b.v, tb);
   const uint32_t same = fe_is_zero(q.X) & fe_eq(q.Y, q.Z);  // Q == O
   return flags_byte(s_ok, a_ok, r_ok, small_a, small_r, same);
 }

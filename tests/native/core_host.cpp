@@ -66,6 +66,23 @@ static const uint32_t *comb_b() {
   return tab.data();
 }
 
+// wide comb table of B (16-bit digits, 48 MiB), built once on first use
+static const uint32_t *comb16_b() {
+  static std::vector<uint32_t> tab;
+  if (tab.empty()) {
+    tab.resize(kComb16TableWords);
+    std::vector<uint32_t> tmp(kComb16Chunk * 8);
+    const uint32_t bw[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
+                            0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
+    fe x, y;
+    ge_decompress(bw, x, y);
+    for (int j = 0; j < kComb16Pos; ++j)
+      for (uint32_t c = 0; c < (uint32_t)kComb16ChunksPerPos; ++c)
+        comb16_build_chunk(x, y, j, c, tab.data(), tmp.data());
+  }
+  return tab.data();
+}
+
 static bool parse_hex(const std::string &s, uint8_t *out, size_t n) {
   if (s.size() != 2 * n) return false;
   for (size_t i = 0; i < n; ++i) {
@@ -250,6 +267,13 @@ int main(int argc, char **argv) {
           : variant == 17 ? verify_one_half_comb<4>(pw, sw, mw, comb_b(), vt, fb)
                           : verify_one_half_comb<5>(pw, sw, mw, comb_b(), vt, fb);
         if (fb) f = verify_one_full_comb<3>(pw, sw, mw, comb_b(), vt) | 0x100u;
+        break;
+      }
+      case 20: {
+        bool fb = false;
+        HostVarTab vt;
+        f = verify_one_half_comb<4, true, 16>(pw, sw, mw, comb16_b(), vt, fb);
+        if (fb) f = verify_one_full_comb<4, true, 16>(pw, sw, mw, comb16_b(), vt) | 0x100u;
         break;
       }
       case 18: {

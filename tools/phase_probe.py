@@ -3,7 +3,7 @@
 one phase replaced by a stub (tools/build_phase_libs.sh, -DHSV_TIMING_STUB_*).
 Stub builds give WRONG flags; only their launch times are reported.
 
-python tools/phase_probe.py [--variant 13] [--n 1048576]
+python tools/phase_probe.py [--variant 15] [--n 1048576]
 """
 import argparse
 import os
@@ -41,7 +41,7 @@ print('%.4f' % (e0.elapsed_time(e1) / {reps}))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variant", type=int, default=13)
+    ap.add_argument("--variant", type=int, default=15)
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--only", default=None, help="time only this build: full, lattice, sqrt or sha")

@@ -3,7 +3,7 @@
 # per build (full and each stub build).  Usage (GPU box): bash tools/pmc_phase.sh [VARIANT]
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$(pwd)
-V=${1:-13}
+V=${1:-15}
 timeout -k 10 500 python tools/phase_probe.py --variant $V > gpurun_out/phase_probe.txt 2>&1 || exit 1
 cd /tmp && export TMPDIR=/tmp
 for b in full lattice sqrt sha; do
