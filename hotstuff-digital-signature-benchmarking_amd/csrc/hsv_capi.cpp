@@ -60,7 +60,7 @@ struct Global {
   bool inited = false;
   int ndev = 0;
   std::vector<DevCtx *> ctx;
-  std::atomic<int> variant{15};  // fastest measured: half-size scalars + wide B comb, WA=4, 3 waves/SIMD
+  std::atomic<int> variant{19};  // fastest measured: scalar prepass + half-size point pass, wide B comb, WA=4, 3 waves/SIMD
 };
 
 Global &G() {

@@ -204,58 +204,194 @@ hsv_verify_mt_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
   }
 }
 
+// one (pk, sig, msg) record into words
+__device__ __forceinline__ void load_triple(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig,
+                                            uint64_t sig_stride, const uint8_t *msg, uint64_t msg_stride,
+                                            uint64_t i, uint32_t pkw[8], uint32_t sigw[16], uint32_t msgw[8]) {
+  const uint4 *p = reinterpret_cast<const uint4 *>(pk + i * pk_stride);
+  const uint4 *s = reinterpret_cast<const uint4 *>(sig + i * sig_stride);
+  const uint4 *m = reinterpret_cast<const uint4 *>(msg + i * msg_stride);
+  const uint4 p0 = p[0], p1 = p[1];
+  const uint4 s0 = s[0], s1 = s[1], s2 = s[2], s3 = s[3];
+  const uint4 m0 = m[0], m1 = m[1];
+  pkw[0] = p0.x; pkw[1] = p0.y; pkw[2] = p0.z; pkw[3] = p0.w;
+  pkw[4] = p1.x; pkw[5] = p1.y; pkw[6] = p1.z; pkw[7] = p1.w;
+  sigw[0] = s0.x; sigw[1] = s0.y; sigw[2] = s0.z; sigw[3] = s0.w;
+  sigw[4] = s1.x; sigw[5] = s1.y; sigw[6] = s1.z; sigw[7] = s1.w;
+  sigw[8] = s2.x; sigw[9] = s2.y; sigw[10] = s2.z; sigw[11] = s2.w;
+  sigw[12] = s3.x; sigw[13] = s3.y; sigw[14] = s3.z; sigw[15] = s3.w;
+  msgw[0] = m0.x; msgw[1] = m0.y; msgw[2] = m0.z; msgw[3] = m0.w;
+  msgw[4] = m1.x; msgw[5] = m1.y; msgw[6] = m1.z; msgw[7] = m1.w;
+}
+
+// Work counters of the comb kernels, zeroed before the launch (16 bytes).
+struct HcCounters {
+  uint32_t next;      // main pass: next item handed out
+  uint32_t fb_count;  // deferred full-length items appended to fb_list
+  uint32_t fb_next;   // fallback pass: next fb_list entry handed out
+  uint32_t pad;
+};
+
 // Half-size scalars + comb table for B (hsv_verify_hc.hpp).  No LDS; the
 // per-lane tables live in `vt_ws` (lane slot = blockIdx * kBlock + threadIdx),
-// the B comb table `comb_b` (384 KiB) is read through L2.  Work is handed out
-// per wave, 64 items at a time, from the counter `next` (zero at launch): a
-// wave slowed by a lane on the full-length fallback, or one that started
-// late, simply takes fewer batches, so the grid finishes together.
-template <int WA, int WAVES, bool PREFETCH, int CB>
+// the B comb table `comb_b` is read through L2 / MALL.  Work is handed out
+// per wave, 64 items at a time, from ctr->next: a wave that started late
+// simply takes fewer batches, so the grid finishes together.
+// A lane whose lattice reduction fails (~2^-13.5) needs the full-length path,
+// about twice the work of the whole batch.  DEFER = false runs it inline
+// (its wave's batch takes ~2x as long, which shows up as a tail at the end of
+// the grid); DEFER = true appends the item to fb_list and leaves it to
+// hsv_verify_fb_kernel, launched right after on the same stream, which deals
+// the deferred items out 64 per wave (its flag byte and strict bit are
+// written there; the strict bit with an atomic OR into the word this pass
+// stored with that bit clear).
+template <int WA, int WAVES, bool PREFETCH, int CB, bool DEFER>
 __global__ void __launch_bounds__(kBlock, WAVES)
 hsv_verify_hc_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
                      const uint8_t *__restrict__ sig, uint64_t sig_stride,
                      const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
                      uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
                      uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b,
-                     uint32_t *__restrict__ next) {
+                     HcCounters *__restrict__ ctr, uint32_t *__restrict__ fb_list) {
   constexpr int kEnt = (1 << (WA - 1)) + 1;
   GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)(blockIdx.x * kBlock + threadIdx.x) * vt_lane_uint4<WA>()};
   const uint32_t lane = threadIdx.x & 63u;
   for (;;) {
     uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(next, 64u);
+    if (lane == 0) base = atomicAdd(&ctr->next, 64u);
     base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
     if (base >= n) break;
     const uint32_t idx = base + lane;
     const bool valid = idx < n;
-    const uint64_t li = valid ? idx : (uint64_t)(n - 1);
     uint32_t pkw[8], sigw[16], msgw[8];
-    {
-      const uint4 *p = reinterpret_cast<const uint4 *>(pk + li * pk_stride);
-      const uint4 *s = reinterpret_cast<const uint4 *>(sig + li * sig_stride);
-      const uint4 *m = reinterpret_cast<const uint4 *>(msg + li * msg_stride);
-      const uint4 p0 = p[0], p1 = p[1];
-      const uint4 s0 = s[0], s1 = s[1], s2 = s[2], s3 = s[3];
-      const uint4 m0 = m[0], m1 = m[1];
-      pkw[0] = p0.x; pkw[1] = p0.y; pkw[2] = p0.z; pkw[3] = p0.w;
-      pkw[4] = p1.x; pkw[5] = p1.y; pkw[6] = p1.z; pkw[7] = p1.w;
-      sigw[0] = s0.x; sigw[1] = s0.y; sigw[2] = s0.z; sigw[3] = s0.w;
-      sigw[4] = s1.x; sigw[5] = s1.y; sigw[6] = s1.z; sigw[7] = s1.w;
-      sigw[8] = s2.x; sigw[9] = s2.y; sigw[10] = s2.z; sigw[11] = s2.w;
-      sigw[12] = s3.x; sigw[13] = s3.y; sigw[14] = s3.z; sigw[15] = s3.w;
-      msgw[0] = m0.x; msgw[1] = m0.y; msgw[2] = m0.z; msgw[3] = m0.w;
-      msgw[4] = m1.x; msgw[5] = m1.y; msgw[6] = m1.z; msgw[7] = m1.w;
-    }
+    load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, valid ? idx : (uint64_t)(n - 1), pkw, sigw, msgw);
     bool fallback = false;
     uint32_t f = verify_one_half_comb<WA, PREFETCH, CB>(pkw, sigw, msgw, comb_b, vt, fallback);
-    if (fallback) f = verify_one_full_comb<WA, PREFETCH, CB>(pkw, sigw, msgw, comb_b, vt);
+    bool deferred = false;
+    if constexpr (DEFER) {
+      deferred = fallback && valid;
+      if (deferred) fb_list[atomicAdd(&ctr->fb_count, 1u)] = idx;
+    } else {
+      if (fallback) f = verify_one_full_comb<WA, PREFETCH, CB>(pkw, sigw, msgw, comb_b, vt);
+    }
 
-    if (valid && flags_out) flags_out[idx] = (uint8_t)f;
+    if (valid && !deferred && flags_out) flags_out[idx] = (uint8_t)f;
     if (strict_bits) {
       // lanes 0 and 1 store the two 32-bit halves of the wave's ballot
-      const uint64_t mask = __ballot(valid && (f & kStrictOk));
+      const uint64_t mask = __ballot(valid && !deferred && (f & kStrictOk));
       const uint32_t w = base / 32u + lane;
       if (lane < 2u && w < (n + 31u) / 32u) strict_bits[w] = lane ? (uint32_t)(mask >> 32) : (uint32_t)mask;
+    }
+  }
+}
+
+// The deferred full-length items of the preceding hsv_verify_hc_kernel<...,
+// DEFER = true> launch (same stream, same workspace).
+template <int WA, int WAVES, int CB>
+__global__ void __launch_bounds__(kBlock, WAVES)
+hsv_verify_fb_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
+                     const uint8_t *__restrict__ sig, uint64_t sig_stride,
+                     const uint8_t *__restrict__ msg, uint64_t msg_stride,
+                     uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
+                     uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b,
+                     HcCounters *__restrict__ ctr, const uint32_t *__restrict__ fb_list) {
+  constexpr int kEnt = (1 << (WA - 1)) + 1;
+  GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)(blockIdx.x * kBlock + threadIdx.x) * vt_lane_uint4<WA>()};
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t cnt = __builtin_amdgcn_readfirstlane(ctr->fb_count);
+  for (;;) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&ctr->fb_next, 64u);
+    base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
+    if (base >= cnt) break;
+    const uint32_t j = base + lane;
+    const bool valid = j < cnt;
+    const uint32_t idx = fb_list[valid ? j : base];
+    uint32_t pkw[8], sigw[16], msgw[8];
+    load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, idx, pkw, sigw, msgw);
+    const uint32_t f = verify_one_full_comb<WA, false, CB>(pkw, sigw, msgw, comb_b, vt);
+    if (valid) {
+      if (flags_out) flags_out[idx] = (uint8_t)f;
+      if (strict_bits && (f & kStrictOk)) atomicOr(&strict_bits[idx >> 5], 1u << (idx & 31u));
+    }
+  }
+}
+
+// Two-pass form (hsv_verify_hc.hpp, prep_scalars / verify_one_prepped).
+// Pass 1: one lane per item, scalar work only; records to `rec` (SoA, row
+// stride n), fallback items appended to fb_list.
+template <int WA>
+__global__ void __launch_bounds__(kBlock)
+hsv_prep_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const uint8_t *__restrict__ sig,
+                uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
+                uint32_t *__restrict__ rec, HcCounters *__restrict__ ctr, uint32_t *__restrict__ fb_list) {
+  const uint32_t idx = blockIdx.x * kBlock + threadIdx.x;
+  if (idx >= n) return;
+  uint32_t pkw[8], sigw[16], msgw[8];
+  load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, idx, pkw, sigw, msgw);
+  if (prep_scalars<WA>(pkw, sigw, msgw, rec + idx, n)) fb_list[atomicAdd(&ctr->fb_count, 1u)] = idx;
+}
+
+// Pass 2: persistent grid, 64-item batches from ctr->next over a virtual
+// range [fallback items | all items].  Fallback batches come first and run
+// the full-length path; in the regular range a fallback item's lane computes
+// nothing it stores.  strict_bits is zeroed before the launch and every
+// batch ORs its bits in (a word can receive bits from both ranges).
+template <int WA, int WAVES, int CB>
+__global__ void __launch_bounds__(kBlock, WAVES)
+hsv_verify_hp_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const uint8_t *__restrict__ sig,
+                     uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
+                     uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
+                     uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b,
+                     const uint32_t *__restrict__ rec, HcCounters *__restrict__ ctr,
+                     const uint32_t *__restrict__ fb_list) {
+  constexpr int kEnt = (1 << (WA - 1)) + 1;
+  GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)(blockIdx.x * kBlock + threadIdx.x) * vt_lane_uint4<WA>()};
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t nfb = __builtin_amdgcn_readfirstlane(ctr->fb_count);
+  const uint32_t fb_end = (nfb + 63u) & ~63u;
+  const uint32_t words = (n + 31u) / 32u;
+  for (;;) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&ctr->next, 64u);
+    base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
+    if (base >= fb_end + n) break;
+    if (base < fb_end) {
+      const uint32_t j = base + lane;
+      const bool valid = j < nfb;
+      const uint32_t idx = fb_list[valid ? j : base];
+      uint32_t pkw[8], sigw[16], msgw[8];
+      load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, idx, pkw, sigw, msgw);
+      const uint32_t f = verify_one_full_comb<WA, false, CB>(pkw, sigw, msgw, comb_b, vt);
+      if (valid) {
+        if (flags_out) flags_out[idx] = (uint8_t)f;
+        if (strict_bits && (f & kStrictOk)) atomicOr(&strict_bits[idx >> 5], 1u << (idx & 31u));
+      }
+      continue;
+    }
+    const uint32_t b0 = base - fb_end;
+    const uint32_t idx = b0 + lane;
+    const bool valid = idx < n;
+    const uint32_t li = valid ? idx : n - 1u;
+    uint32_t pkw[8], rw[8];
+    {
+      const uint4 *p = reinterpret_cast<const uint4 *>(pk + (uint64_t)li * pk_stride);
+      const uint4 *r = reinterpret_cast<const uint4 *>(sig + (uint64_t)li * sig_stride);
+      const uint4 p0 = p[0], p1 = p[1], r0 = r[0], r1 = r[1];
+      pkw[0] = p0.x; pkw[1] = p0.y; pkw[2] = p0.z; pkw[3] = p0.w;
+      pkw[4] = p1.x; pkw[5] = p1.y; pkw[6] = p1.z; pkw[7] = p1.w;
+      rw[0] = r0.x; rw[1] = r0.y; rw[2] = r0.z; rw[3] = r0.w;
+      rw[4] = r1.x; rw[5] = r1.y; rw[6] = r1.z; rw[7] = r1.w;
+    }
+    const uint32_t meta = rec[18ull * n + li];
+    const bool own = valid && !(meta & kPrepFallback);
+    const uint32_t f = verify_one_prepped<WA, CB>(pkw, rw, rec + li, n, meta, comb_b, vt);
+    if (own && flags_out) flags_out[idx] = (uint8_t)f;
+    if (strict_bits) {
+      const uint64_t mask = __ballot(own && (f & kStrictOk));
+      const uint32_t w = b0 / 32u + lane;
+      const uint32_t part = lane ? (uint32_t)(mask >> 32) : (uint32_t)mask;
+      if (lane < 2u && w < words && part) atomicOr(&strict_bits[w], part);
     }
   }
 }
@@ -303,18 +439,23 @@ __global__ void __launch_bounds__(256) hsv_mad_peak_kernel(uint32_t *sink, uint3
 //  14: as 11, 2 waves/SIMD, no prefetch
 //  15: as 13 with the wide (16-bit digit, 48 MiB) comb table of B
 //  16: as 14 with the wide comb table
-extern "C" int hsv_num_variants(void) { return 17; }
+//  17: as 15, full-length fallback items deferred to a second launch
+//  18: as 16, fallback deferred
+//  19: two passes: scalar prepass, then the point pass with the fallback
+//      items dealt out first (WA 4, 3 waves/SIMD, wide comb)
+//  20: as 19, 2 waves/SIMD
+extern "C" int hsv_num_variants(void) { return 21; }
 
 namespace {
 
 // Persistent-grid launch of hsv_verify_mt_kernel with a stream-ordered
 // workspace for the per-lane tables (freed on the same stream).
-template <int WA, int WB, int WAVES, bool COMB, bool PREFETCH = true, int CB = 8>
+template <int WA, int WB, int WAVES, bool COMB, bool PREFETCH = true, int CB = 8, bool DEFER = false>
 hipError_t launch_mt(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
                      const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
                      uint32_t *strict_bits, const uint32_t *comb_b, hipStream_t stream) {
   const void *kern;
-  if constexpr (COMB) kern = reinterpret_cast<const void *>(hsv::hsv_verify_hc_kernel<WA, WAVES, PREFETCH, CB>);
+  if constexpr (COMB) kern = reinterpret_cast<const void *>(hsv::hsv_verify_hc_kernel<WA, WAVES, PREFETCH, CB, DEFER>);
   else kern = reinterpret_cast<const void *>(hsv::hsv_verify_mt_kernel<WA, WB, WAVES>);
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -342,24 +483,96 @@ hipError_t launch_mt(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
   }
   const uint32_t blocks_needed = (n + hsv::kBlock - 1) / hsv::kBlock;
   const uint32_t grid = std::min<uint32_t>(blocks_needed, (uint32_t)resident);
+  // workspace: per-lane tables | counters (256 B) | deferred-item list (4 B per item)
   const size_t ws_bytes = (size_t)grid * hsv::kBlock * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
+  const size_t fb_bytes = DEFER ? (size_t)n * sizeof(uint32_t) : 0;
   void *ws = nullptr;
-  e = hipMallocAsync(&ws, ws_bytes + 256, stream);  // + the work counter of the comb kernel
+  e = hipMallocAsync(&ws, ws_bytes + 256 + fb_bytes, stream);
   if (e != hipSuccess) return e;
-  uint32_t *next = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(ws) + ws_bytes);
+  uint8_t *ws8 = static_cast<uint8_t *>(ws);
+  hsv::HcCounters *ctr = reinterpret_cast<hsv::HcCounters *>(ws8 + ws_bytes);
+  uint32_t *fb_list = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256);
+  uint4 *vt_ws = reinterpret_cast<uint4 *>(ws);
   if constexpr (COMB) {
-    e = hipMemsetAsync(next, 0, sizeof(uint32_t), stream);
+    e = hipMemsetAsync(ctr, 0, sizeof(hsv::HcCounters), stream);
     if (e != hipSuccess) return e;
-  }
-  if constexpr (COMB)
-    hipLaunchKernelGGL((hsv::hsv_verify_hc_kernel<WA, WAVES, PREFETCH, CB>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
-                       pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits,
-                       reinterpret_cast<uint4 *>(ws), comb_b, next);
-  else
+    hipLaunchKernelGGL((hsv::hsv_verify_hc_kernel<WA, WAVES, PREFETCH, CB, DEFER>), dim3(grid), dim3(hsv::kBlock), 0,
+                       stream, pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, vt_ws,
+                       comb_b, ctr, fb_list);
+    e = hipGetLastError();
+    if (DEFER && e == hipSuccess) {
+      hipLaunchKernelGGL((hsv::hsv_verify_fb_kernel<WA, WAVES, CB>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
+                         pk_stride, sig, sig_stride, msg, msg_stride, flags_out, strict_bits, vt_ws, comb_b, ctr,
+                         fb_list);
+      e = hipGetLastError();
+    }
+  } else {
     hipLaunchKernelGGL((hsv::hsv_verify_mt_kernel<WA, WB, WAVES>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
-                       pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits,
-                       reinterpret_cast<uint4 *>(ws));
-  e = hipGetLastError();
+                       pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, vt_ws);
+    e = hipGetLastError();
+  }
+  const hipError_t ef = hipFreeAsync(ws, stream);
+  return e != hipSuccess ? e : ef;
+}
+
+// Two-pass launch (variants 19/20): prepass over all items, then the
+// persistent point pass.  Workspace: per-lane tables | counters (256 B) |
+// fallback list (4 B per item) | prep records (kPrepWords x 4 B per item).
+template <int WA, int WAVES, int CB>
+hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
+                     const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
+                     uint32_t *strict_bits, const uint32_t *comb_b, hipStream_t stream) {
+  const void *kern = reinterpret_cast<const void *>(hsv::hsv_verify_hp_kernel<WA, WAVES, CB>);
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  static std::mutex mu;
+  static std::unordered_map<int, int> slots_per_dev;
+  int resident = 0;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = slots_per_dev.find(dev);
+    if (it == slots_per_dev.end()) {
+      int bpc = 0, cus = 0;
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kern, hsv::kBlock, 0);
+      if (e != hipSuccess) return e;
+      e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (e != hipSuccess) return e;
+      hipMemPool_t pool;
+      if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+        uint64_t keep = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+      }
+      it = slots_per_dev.emplace(dev, std::max(1, bpc) * std::max(1, cus)).first;
+    }
+    resident = it->second;
+  }
+  const uint32_t blocks_needed = (n + hsv::kBlock - 1) / hsv::kBlock;
+  const uint32_t grid = std::min<uint32_t>(blocks_needed, (uint32_t)resident);
+  const size_t ws_bytes = (size_t)grid * hsv::kBlock * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
+  const size_t fb_bytes = (size_t)n * sizeof(uint32_t);
+  const size_t rec_bytes = (size_t)n * hsv::kPrepWords * sizeof(uint32_t);
+  void *ws = nullptr;
+  e = hipMallocAsync(&ws, ws_bytes + 256 + fb_bytes + rec_bytes, stream);
+  if (e != hipSuccess) return e;
+  uint8_t *ws8 = static_cast<uint8_t *>(ws);
+  uint4 *vt_ws = reinterpret_cast<uint4 *>(ws);
+  hsv::HcCounters *ctr = reinterpret_cast<hsv::HcCounters *>(ws8 + ws_bytes);
+  uint32_t *fb_list = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256);
+  uint32_t *rec = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256 + fb_bytes);
+  e = hipMemsetAsync(ctr, 0, sizeof(hsv::HcCounters), stream);
+  if (e == hipSuccess && strict_bits) e = hipMemsetAsync(strict_bits, 0, (size_t)((n + 31u) / 32u) * 4u, stream);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL((hsv::hsv_prep_kernel<WA>), dim3(blocks_needed), dim3(hsv::kBlock), 0, stream, pk, pk_stride,
+                       sig, sig_stride, msg, msg_stride, n, rec, ctr, fb_list);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL((hsv::hsv_verify_hp_kernel<WA, WAVES, CB>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
+                       pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, vt_ws, comb_b, rec,
+                       ctr, fb_list);
+    e = hipGetLastError();
+  }
   const hipError_t ef = hipFreeAsync(ws, stream);
   return e != hipSuccess ? e : ef;
 }
@@ -401,6 +614,14 @@ extern "C" hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t
       return launch_mt<4, 4, 3, true, false, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
     case 16: if (!comb_b) return hipErrorInvalidValue;
       return launch_mt<4, 4, 2, true, false, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
+    case 17: if (!comb_b) return hipErrorInvalidValue;
+      return launch_mt<4, 4, 3, true, false, 16, true>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
+    case 18: if (!comb_b) return hipErrorInvalidValue;
+      return launch_mt<4, 4, 2, true, false, 16, true>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
+    case 19: if (!comb_b) return hipErrorInvalidValue;
+      return launch_hp<4, 3, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
+    case 20: if (!comb_b) return hipErrorInvalidValue;
+      return launch_hp<4, 2, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
 #undef HSV_LAUNCH_MT
     default: return hipErrorInvalidValue;
   }
@@ -434,6 +655,6 @@ extern "C" double hsv_launch_mad_peak(int device_cus) {
 
 extern "C" int hsv_variant_needs_comb(int variant) {
   if (variant >= 10 && variant <= 14) return 8;
-  if (variant >= 15 && variant <= 16) return 16;
+  if (variant >= 15 && variant <= 20) return 16;
   return 0;
 }

@@ -184,4 +184,74 @@ HSV_INL uint32_t verify_one_half_comb(const uint32_t pk[8], const uint32_t sig[1
   return flags_byte(s_ok, a_ok, r_ok, small_a, small_r, same);
 }
 
+// ---- two-pass form: scalar prepass + point pass ---------------------------
+// The prepass (one lane per item) does everything that depends only on the
+// scalars: s < l, SHA-512, k mod l, the lattice reduction, the recoded
+// digits of c1 and |c0| and b = (c1 s) mod l, and writes them to a
+// structure-of-arrays record (word j of item i at rec[j * stride + i]).
+// Items without a short pair are flagged there and listed, so the point pass
+// can deal them out first: their full-length work then overlaps the bulk of
+// the batch instead of trailing it.
+constexpr int kPrepWords = 19;  // d(c1)[5] | d(|c0|)[5] | b[8] | meta
+enum : uint32_t { kPrepSOk = 1u, kPrepC0Neg = 2u, kPrepFallback = 4u };
+
+template <int WA>
+HSV_INL bool prep_scalars(const uint32_t pk[8], const uint32_t sig[16], const uint32_t msg[8], uint32_t *rec,
+                          uint64_t stride) {
+  using G = HalfCombWindows<WA>;
+  const uint32_t s_ok = sc_is_canonical(sig + 8);
+  uint32_t h[16];
+  sha512_96(sig, pk, msg, h);
+  const sc k = sc_reduce512(h);
+  const LatOut lat = lattice_reduce(k);
+  uint32_t d[5];
+  recode_top5<WA, G::NW>(lat.c1, d);
+  HSV_UNROLL
+  for (int i = 0; i < 5; ++i) rec[i * stride] = d[i];
+  recode_top5<WA, G::NW>(lat.c0, d);
+  HSV_UNROLL
+  for (int i = 0; i < 5; ++i) rec[(5 + i) * stride] = d[i];
+  const sc b = sc_mul_small(lat.c1, sig + 8);
+  HSV_UNROLL
+  for (int i = 0; i < 8; ++i) rec[(10 + i) * stride] = b.v[i];
+  rec[18 * stride] = (s_ok ? kPrepSOk : 0u) | (lat.c0_neg ? kPrepC0Neg : 0u) | (lat.ok ? 0u : kPrepFallback);
+  return !lat.ok;
+}
+
+// Point pass of a prepped item: the half-size equation of
+// verify_one_half_comb with the scalars read back from the record.
+// `rb` is R (the first 32 bytes of the signature).
+template <int WA, int CB, class VT>
+HSV_INL uint32_t verify_one_prepped(const uint32_t pk[8], const uint32_t rb[8], const uint32_t *rec,
+                                    uint64_t stride, const uint32_t meta, const uint32_t *tb, VT &vt) {
+  using G = HalfCombWindows<WA>;
+  constexpr int TS = 1 << (WA - 1);
+  uint32_t a_ok, small_a, r_ok, small_r;
+  {
+    fe x, y;
+    r_ok = ge_decompress(rb, x, y);
+    small_r = r_ok & y_is_small_order(y);
+    vt_build<TS>(vt, 0, fe_carry(fe_neg(x)), y);
+  }
+  {
+    fe x, y;
+    a_ok = ge_decompress(pk, x, y);
+    small_a = a_ok & y_is_small_order(y);
+    vt_build<TS>(vt, 1, fe_carry(fe_neg(x)), y);
+  }
+  uint32_t d[2][5];
+  HSV_UNROLL
+  for (int i = 0; i < 5; ++i) {
+    d[0][i] = rec[i * stride];
+    d[1][i] = rec[(5 + i) * stride];
+  }
+  ge_ext q = straus_vt<WA, G::NW, 5, 2, false>(d, vt, (meta & kPrepC0Neg) ? 1u : 0u);
+  uint32_t b[8];
+  HSV_UNROLL
+  for (int i = 0; i < 8; ++i) b[i] = rec[(10 + i) * stride];
+  q = comb_add_b<CB>(q, b, tb);
+  const uint32_t same = fe_is_zero(q.X) & fe_eq(q.Y, q.Z);
+  return flags_byte(meta & kPrepSOk, a_ok, r_ok, small_a, small_r, same);
+}
+
 }  // namespace hsv

@@ -281,6 +281,15 @@ int main(int argc, char **argv) {
         f = verify_one_full_comb<3>(pw, sw, mw, comb_b(), vt);
         break;
       }
+      case 21: {  // two-pass form (GPU variants 19/20): scalar prepass record, then the point pass
+        HostVarTab vt;
+        uint32_t rec[kPrepWords];
+        if (prep_scalars<4>(pw, sw, mw, rec, 1))
+          f = verify_one_full_comb<4, true, 16>(pw, sw, mw, comb16_b(), vt) | 0x100u;
+        else
+          f = verify_one_prepped<4, 16>(pw, sw, rec, 1, rec[18], comb16_b(), vt);
+        break;
+      }
       default: f = verify_one<3, 9>(pw, sw, mw, bt); break;
     }
     printf("%02x\n", f & 0xffu);

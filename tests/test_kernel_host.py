@@ -105,7 +105,7 @@ def test_radix32_field_matches_golden(core_host32, golden):
     assert (got == golden["flags"]).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 4, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20])
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21])
 def test_verify_core_all_geometries_match_golden(core_host, golden, variant):
     lines = [f"{bytes(p).hex()} {bytes(s).hex()} {bytes(m).hex()}"
              for p, s, m in zip(golden["pk"], golden["sig"], golden["msg"])]
