@@ -311,6 +311,8 @@ def main():
             "peak_probe": probe / 1e12,
             "work_per_verify": f"{WORK_MACS} u32 MACs (SURVEY 8(d)); {IO_BYTES} HBM bytes algorithmic",
             "kernel_ms": kernel_ms,
+            "kernels": ("hsv_prep_kernel + hsv_verify_hp_kernel (one verify launch: scalar prepass, point pass)"
+                        if verifier.get_variant() in (19, 20) else "hsv_verify_hc_kernel"),
         },
         "checks": {"honest_all_accepted": honest_ok, "corrupted_all_rejected": corrupt_rejected,
                    "strict_accepted_global": global_accepted},

@@ -15,16 +15,24 @@ import csv, glob, json, collections
 out = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     f = glob.glob(f"gpurun_out/pmc_traffic_{c}/**/*counter_collection.csv", recursive=True)[0]
-    per = collections.OrderedDict()
-    name = None
+    # one verify launch = its prepass (hsv_prep_kernel, two-pass variants) +
+    # the verify kernel, summed per launch; the warm-up launch is dropped
+    per, names = collections.OrderedDict(), {}
     for r in csv.DictReader(open(f)):
-        if "hsv_verify" not in r["Kernel_Name"]:
+        k = r["Kernel_Name"]
+        if "hsv_verify" not in k and "hsv_prep" not in k:
             continue
-        name = r["Kernel_Name"]
+        names[r["Dispatch_Id"]] = k
         per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
-    vals = list(per.values())[1:]  # drop the warm-up launch
+    launches, cur, name = [], 0.0, None
+    for d in sorted(per, key=int):
+        cur += per[d]
+        if "hsv_verify" in names[d]:
+            launches.append(cur)
+            cur, name = 0.0, names[d]
+    vals = launches[1:]
     out[c] = sum(vals) / len(vals) * 1024.0  # rocprofv3 reports kilobytes
-    out["kernel"] = name
+    out["kernel"] = name + (" + hsv_prep_kernel" if any("hsv_prep" in v for v in names.values()) else "")
 bench = json.load(open("gpurun_out/pmc_traffic_FETCH_SIZE.json"))
 json.dump({"variant": bench["config"]["kernel_variant"], "n": bench["config"]["batch_per_gpu"],
            "fetch_bytes_per_launch": out["FETCH_SIZE"], "write_bytes_per_launch": out["WRITE_SIZE"],
