@@ -22,6 +22,9 @@ Reported beside it:
                 over a bounded sample of the same workload.
   qc_latency    p50/p99 of the host-buffer QC call (hsv_verify_batch_packed:
                 H2D + kernel + D2H) for 67 (n=100) and 667 (n=1000) votes.
+  mempool_tx    2^20 client transactions of 512 B (message || pk || sig,
+                mempool/src/batch_maker.rs:79-85) in HBM: tx/s of digest +
+                verification, with the C port beside it.
 """
 import argparse
 import ctypes
@@ -191,6 +194,49 @@ def qc_cpu(reps=3):
     return {"n1000_votes667_p50_ms": float(np.median(ts) * 1e3), "cores": 1, "kind": "port"}
 
 
+def mempool_bench(dev, n=1 << 20, tx_size=512, cpu_sample=1 << 17):
+    """Mempool transactions: n client transactions of
+    tx_size bytes (the reference benchmark's default, benchmark/fabfile.py),
+    resident in HBM; one step = digest records + verification
+    (hsv_verify_transactions_device).  Beside it: the C port on host threads
+    over the first cpu_sample transactions, flag-for-flag against the GPU."""
+    import torch
+    from hsverify import mempool, synth
+    w = synth.transactions(n, tx_size=tx_size, seed=9)
+    d = torch.from_numpy(w.txs.reshape(-1)).to(dev)
+    flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    mempool.verify_transactions_device(d, None, tx_size=tx_size, n=n, flags=flags)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    steps = 5
+    e0.record(stream)
+    for _ in range(steps):
+        mempool.verify_transactions_device(d, None, tx_size=tx_size, n=n, flags=flags)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / steps
+    f = flags.cpu().numpy()
+    res = {"txs": n, "tx_size": tx_size, "ms_per_step": ms, "tx_per_s": n / (ms * 1e-3),
+           "honest_all_accepted": bool((f[w.honest] & 1).all()),
+           "corrupted_all_rejected": bool(not (f[~w.honest] & 1).any())}
+    so = os.path.join(ROOT, "oracle", "_build", "libhsv_oracle.so")
+    if os.path.exists(so):
+        lib = ctypes.CDLL(so)
+        lib.oracle_verify_tx_many.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                              ctypes.c_void_p, ctypes.c_int]
+        m = min(cpu_sample, n)
+        threads = max(1, min(16, os.cpu_count() or 1))
+        buf = np.ascontiguousarray(w.txs[:m])
+        out = np.zeros(m, np.uint8)
+        t0 = time.perf_counter()
+        lib.oracle_verify_tx_many(buf.ctypes.data, None, tx_size, m, out.ctypes.data, threads)
+        dt = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": m / dt, "unit": "tx/s", "cores": threads, "kind": "port",
+                               "sample": f"first {m} transactions", "sample_parity_vs_gpu": bool((out == f[:m]).all())}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -323,6 +369,7 @@ def main():
     if not a.no_qc:
         out["qc_latency"] = qc_latency(a.qc_reps)
         out["committee_cache"] = committee_bench(a.qc_reps, dev)
+        out["mempool_tx"] = mempool_bench(dev)
         if world == 1 and not a.no_cpu_baseline:
             out["qc_cpu_baseline"] = qc_cpu()
     print(json.dumps(out), flush=True)

@@ -44,3 +44,18 @@ uint64_t hsv_comb16_tmp_bytes(void);
 #ifdef __cplusplus
 }
 #endif
+
+// ---- mempool transactions (hsv_mempool.hip) -------------------------------
+#ifdef __cplusplus
+extern "C" {
+#endif
+// 128-byte records pk || R || s || SHA-512(message)[..32] for n transactions
+// (offsets[i]..offsets[i+1] of txs, or fixed tx_size when offsets is NULL).
+hipError_t hsv_launch_tx_records(const uint8_t *txs, const uint64_t *offsets, uint64_t tx_size, uint32_t n,
+                                 uint8_t *records, hipStream_t stream);
+// flags 0 (and STRICT_OK bit cleared) for transactions shorter than 96 bytes
+hipError_t hsv_launch_tx_mask(const uint64_t *offsets, uint32_t n, uint8_t *flags, uint32_t *strict_bits,
+                              hipStream_t stream);
+#ifdef __cplusplus
+}
+#endif

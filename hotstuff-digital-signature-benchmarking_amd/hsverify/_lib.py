@@ -63,6 +63,9 @@ def _declare(lib):
         "hsv_verify_device": (ctypes.c_int, [c_u8p, sz, c_u8p, sz, c_u8p, sz, sz, c_u8p, ctypes.c_void_p]),
         "hsv_verify_device_bits": (ctypes.c_int, [c_u8p, sz, c_u8p, sz, c_u8p, sz, sz, c_u8p, c_u8p,
                                                   ctypes.c_void_p]),
+        "hsv_verify_transactions": (ctypes.c_int, [c_u8p, c_u8p, sz, c_u8p]),
+        "hsv_verify_transactions_fixed": (ctypes.c_int, [c_u8p, sz, sz, c_u8p]),
+        "hsv_verify_transactions_device": (ctypes.c_int, [c_u8p, c_u8p, sz, sz, c_u8p, c_u8p, ctypes.c_void_p]),
         "hsv_public_key": (ctypes.c_int, [c_u8p, c_u8p]),
         "hsv_sign": (ctypes.c_int, [c_u8p, c_u8p, sz, c_u8p]),
         "hsv_sign_many": (ctypes.c_int, [c_u8p, c_u8p, sz, sz, c_u8p, c_u8p, ctypes.c_int]),

@@ -145,3 +145,45 @@ def tc_votes(committee: int, seed: int = 0, corrupt_frac: float = 0.0, round_: i
     w = Workload(pk, sig, msgs, np.ones(quorum, bool), np.full(quorum, -1, np.int8))
     corrupt(w, corrupt_frac, rng)
     return w
+
+
+@dataclass
+class TxWorkload:
+    txs: np.ndarray       # (n, tx_size) uint8: message || pk || sig
+    honest: np.ndarray    # (n,) bool
+    kind: np.ndarray      # (n,) int8: -1 honest, else CORRUPTIONS index
+
+    @property
+    def n(self) -> int:
+        return self.txs.shape[0]
+
+
+def transactions(n: int, tx_size: int = 512, seed: int = 0, corrupt_frac: float = 0.05,
+                 nthreads: int = 0) -> TxWorkload:
+    """Mempool workload: n client transactions of tx_size
+    bytes (the reference benchmark's default is 512, benchmark/fabfile.py),
+    each message || pk || Signature::new(Digest(SHA-512(message)[..32]))
+    (mempool/src/batch_maker.rs:79-85).  Corruptions as `corrupt`; the
+    "wrong_digest" kind flips a message byte instead."""
+    if tx_size < 96:
+        raise ValueError("a transaction carries pk and signature: tx_size >= 96")
+    mlen = tx_size - 96
+    rng = np.random.default_rng(seed)
+    seeds = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    msgs = rng.integers(0, 256, size=(n, mlen), dtype=np.uint8)
+    digests = np.empty((n, 32), np.uint8)
+    for i in range(n):
+        digests[i] = np.frombuffer(hashlib.sha512(msgs[i].tobytes()).digest()[:32], np.uint8)
+    pk, sig = sign_many(seeds, digests, nthreads)
+    w = Workload(pk, sig, digests, np.ones(n, bool), np.full(n, -1, np.int8))
+    corrupt(w, corrupt_frac, rng)
+    bad_msg = np.nonzero(w.kind == CORRUPTIONS.index("wrong_digest"))[0]
+    if mlen:
+        for i in bad_msg:
+            b = int(rng.integers(0, mlen * 8))
+            msgs[i, b // 8] ^= np.uint8(1 << (b % 8))
+    else:  # no message bytes to flip: corrupt the signature's s instead
+        for i in bad_msg:
+            w.sig[i, 32] ^= np.uint8(1)
+    txs = np.concatenate([msgs, w.pk, w.sig], axis=1)
+    return TxWorkload(np.ascontiguousarray(txs), w.honest, w.kind)

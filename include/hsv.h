@@ -130,6 +130,31 @@ int hsv_committee_verify_device(const hsv_committee *c, const uint32_t *d_key_id
                                 size_t sig_stride, const uint8_t *d_msg, size_t msg_stride, size_t m,
                                 uint8_t *d_flags, void *stream);
 
+/* ---- mempool transactions -------------------------- */
+/* A client transaction is  message || pk (32 B) || sig (64 B, R||s)  and its
+ * signature is checked over Digest(SHA-512(message)[..32]) with
+ * Signature::verify, as in the reference's transaction check
+ * (mempool/src/batch_maker.rs:79-85, consensus/src/core.rs:121-127).  The
+ * per-transaction flags are hsv_verify's flags for that (pk, sig, digest);
+ * HSV_STRICT_OK is the reference's `signature.verify(..).is_ok()`.
+ * Transactions shorter than 96 bytes (the reference's slice would panic) are
+ * rejected with HSV_ERR_INVALID_ARG by the host-buffer calls. */
+
+/* Ragged batch: transaction i is txs[offsets[i] .. offsets[i+1]) (n+1
+ * offsets).  flags_out: n bytes. */
+int hsv_verify_transactions(const uint8_t *txs, const uint64_t *offsets, size_t n, uint8_t *flags_out);
+
+/* Fixed-size batch (the benchmark client's transactions all have the same
+ * size, node/src/client.rs): transaction i is txs[i*tx_size .. (i+1)*tx_size). */
+int hsv_verify_transactions_fixed(const uint8_t *txs, size_t tx_size, size_t n, uint8_t *flags_out);
+
+/* Device-resident, stream-ordered form.  d_offsets (n+1 entries, relative to
+ * d_txs) or NULL for fixed-size transactions of tx_size bytes.  Any alignment
+ * of d_txs.  Transactions shorter than 96 bytes get flags 0.  Outputs as
+ * hsv_verify_device_bits (either may be NULL, not both). */
+int hsv_verify_transactions_device(const uint8_t *d_txs, const uint64_t *d_offsets, size_t tx_size, size_t n,
+                                   uint8_t *d_flags, uint32_t *d_strict_bits, void *stream);
+
 /* ---- signing (host CPU; not on the hot path) ---------------------------- */
 /* Public key for a 32-byte secret seed (dalek Keypair from SecretKey). */
 int hsv_public_key(const uint8_t seed[32], uint8_t pk_out[32]);

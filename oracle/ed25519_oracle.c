@@ -591,3 +591,48 @@ int oracle_verify_batch(const uint8_t digest[32], const uint8_t *pk, const uint8
   }
   return 1;
 }
+
+/* Mempool transaction check (reference mempool/src/batch_maker.rs:79-85):
+ * tx = message || pk (32) || sig (64); flags of verify over
+ * Digest(SHA-512(message)[..32]).  Transaction i = txs[offsets[i]..offsets[i+1]);
+ * offsets NULL = fixed size tx_size.  A transaction shorter than 96 bytes gets
+ * flags 0 (the reference's slice would panic). */
+typedef struct {
+  const uint8_t *txs;
+  const uint64_t *offsets;
+  size_t tx_size, lo, hi;
+  uint8_t *flags;
+} txjob_t;
+
+static void *tx_worker(void *arg) {
+  txjob_t *j = (txjob_t *)arg;
+  for (size_t i = j->lo; i < j->hi; ++i) {
+    const uint64_t a = j->offsets ? j->offsets[i] : (uint64_t)i * j->tx_size;
+    const uint64_t b = j->offsets ? j->offsets[i + 1] : a + j->tx_size;
+    if (b < a || b - a < 96) {
+      j->flags[i] = 0;
+      continue;
+    }
+    const uint8_t *tx = j->txs + a;
+    const size_t mlen = (size_t)(b - a - 96);
+    uint8_t h[64];
+    sha512(h, tx, mlen);
+    j->flags[i] = oracle_verify_flags(tx + mlen, tx + mlen + 32, h, 32);
+  }
+  return NULL;
+}
+
+int oracle_verify_tx_many(const uint8_t *txs, const uint64_t *offsets, size_t tx_size, size_t n, uint8_t *flags,
+                          int nthreads) {
+  pthread_once(&g_once, init_consts);
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  txjob_t jobs[256];
+  for (int t = 0; t < nthreads; ++t) {
+    jobs[t] = (txjob_t){txs, offsets, tx_size, n * t / nthreads, n * (t + 1) / nthreads, flags};
+    pthread_create(&th[t], NULL, tx_worker, &jobs[t]);
+  }
+  for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  return 0;
+}

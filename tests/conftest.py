@@ -47,7 +47,33 @@ def oracle_lib():
                                        ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int]
     lib.oracle_verify_batch.restype = ctypes.c_int
     lib.oracle_verify_batch.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    lib.oracle_verify_tx_many.restype = ctypes.c_int
+    lib.oracle_verify_tx_many.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                          ctypes.c_void_p, ctypes.c_int]
     return lib
+
+
+def oracle_tx_flags(lib, buf, offsets=None, tx_size=0, n=None, nthreads=None):
+    """Transaction flags via the C oracle: buf u8, offsets u64 (n+1) or fixed tx_size."""
+    buf = np.ascontiguousarray(buf, np.uint8)
+    if n is None:
+        n = len(offsets) - 1 if offsets is not None else buf.size // tx_size
+    out = np.zeros(n, np.uint8)
+    nt = nthreads or min(16, os.cpu_count() or 1)
+    lib.oracle_verify_tx_many(buf.ctypes.data, offsets.ctypes.data if offsets is not None else None, tx_size, n,
+                              out.ctypes.data, nt)
+    return out
+
+
+@pytest.fixture(scope="session")
+def tx_golden():
+    """Mempool transaction vectors (tests/golden/make_tx_golden.py): txs (list of
+    bytes), flags (u8 array), cases."""
+    with open(os.path.join(GOLDEN, "tx_vectors.json")) as f:
+        vecs = json.load(f)["vectors"]
+    return {"txs": [bytes.fromhex(v["tx"]) for v in vecs],
+            "flags": np.array([v["flags"] for v in vecs], np.uint8),
+            "cases": [v["case"] for v in vecs]}
 
 
 def oracle_flags(lib, pk, sig, msg, nthreads=None):

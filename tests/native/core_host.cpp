@@ -16,6 +16,7 @@
 #include "hsv_lattice.hpp"
 #include "hsv_verify_core.hpp"
 #include "hsv_verify_hc.hpp"
+#include "hsv_txhash.hpp"
 #include <vector>
 
 using namespace hsv;
@@ -149,6 +150,29 @@ int main(int argc, char **argv) {
       sha512_96(rw, aw, mw, h);
       sc k = sc_reduce512(h);
       for (int i = 7; i >= 0; --i) printf("%08x", k.v[i]);
+      printf("\n");
+    }
+    return 0;
+  }
+  if (argc > 1 && strcmp(argv[1], "--txrec") == 0) {
+    // lines: shift tx_hex -> 128-byte record pk||sig||SHA-512(message)[..32] (hex)
+    // The transaction is placed at byte `shift` of a 16-aligned buffer whose
+    // other bytes are 0xa5, so realignment errors and stray reads show up.
+    std::string shs, txs;
+    while (std::cin >> shs >> txs) {
+      const size_t sh = (size_t)atoi(shs.c_str()), len = txs.size() / 2;
+      std::vector<uint32_t> buf((sh + len + 64) / 4 + 8, 0xa5a5a5a5u);
+      uint8_t *bytes = reinterpret_cast<uint8_t *>(buf.data());
+      parse_hex(txs, bytes + sh, len);
+      const uint64_t q_last = (sh + len - 1) >> 4;
+      auto ld = [&](uint64_t k, uint32_t w[4]) {
+        if (k > q_last) { fprintf(stderr, "load past the transaction\n"); exit(3); }
+        memcpy(w, bytes + 16 * k, 16);
+      };
+      uint32_t rec[32];
+      tx_record(ld, sh, len, rec);
+      for (int i = 0; i < 32; ++i)
+        for (int b = 0; b < 4; ++b) printf("%02x", (rec[i] >> (8 * b)) & 0xffu);
       printf("\n");
     }
     return 0;

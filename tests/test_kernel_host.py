@@ -166,3 +166,24 @@ def test_lattice_fallback_records(core_host, fallback_records, variant):
     assert (got == fb["flags"]).all()
     # 24 challenges x (honest, flipped s, s + l) keep k; the mixed-order key changes it
     assert r.stderr.count("fallback") >= 48
+
+
+def test_transaction_record_matches_hashlib(core_host):
+    """Mempool transaction records (csrc/hsv_txhash.hpp):
+    pk || sig || SHA-512(message)[..32] for tx = message || pk || sig
+    (mempool/src/batch_maker.rs:79-85), over every SHA-512 padding boundary
+    and every start alignment within a 16-byte chunk."""
+    import hashlib
+    rnd = random.Random(8)
+    mlens = [0, 1, 7, 8, 9, 15, 16, 17, 63, 64, 110, 111, 112, 113, 127, 128, 129, 200, 238, 239, 240,
+             241, 255, 256, 257, 416, 1000, 2048 + 5]
+    lines, exp = [], []
+    for mlen in mlens:
+        for sh in (0, 1, 2, 3, 4, 5, 7, 8, 11, 12, 13, 15):
+            tx = rnd.randbytes(mlen + 96)
+            lines.append(f"{sh} {tx.hex()}")
+            msg, pk, sig = tx[:mlen], tx[mlen:mlen + 32], tx[mlen + 32:]
+            exp.append((pk + sig + hashlib.sha512(msg).digest()[:32]).hex())
+    got = _run(core_host, ["--txrec"], lines)
+    bad = [(lines[i][:12], len(lines[i])) for i in range(len(exp)) if got[i] != exp[i]]
+    assert not bad, bad[:5]
