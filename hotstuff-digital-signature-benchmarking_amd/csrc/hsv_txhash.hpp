@@ -34,15 +34,19 @@ HSV_INL uint32_t tx_funnel(uint32_t lo, uint32_t hi, uint32_t sh) {
 
 // The NW little-endian words of bytes [a, a + 4*NW) of the stream, where
 // a = 16*q0 + sh16 (sh16 in 0..15) and ld(q, w) fills the aligned chunk q.
-// Chunks above q_last hold no byte of the object and read as zero.
+// Chunk indices are clamped to q_last (the last chunk holding a byte of the
+// transaction), so every load is in bounds and unconditional; words built from
+// a clamped chunk lie past the transaction's end and callers never use them
+// (message padding replaces them, and the pk || sig words end at the end).
 template <int NW, class LoadChunk>
 HSV_INL void tx_load_words(LoadChunk &ld, uint64_t q0, uint32_t sh16, uint64_t q_last, uint32_t out[NW]) {
   constexpr int NQ = NW / 4 + 1;  // chunks covering 4*NW bytes at any offset
   uint32_t raw[4 * NQ + 1];
   HSV_UNROLL
   for (int k = 0; k < NQ; ++k) {
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
-    if (q0 + (uint64_t)k <= q_last) ld(q0 + (uint64_t)k, w);
+    uint32_t w[4];
+    const uint64_t qk = q0 + (uint64_t)k;
+    ld(qk < q_last ? qk : q_last, w);
     raw[4 * k + 0] = w[0];
     raw[4 * k + 1] = w[1];
     raw[4 * k + 2] = w[2];
