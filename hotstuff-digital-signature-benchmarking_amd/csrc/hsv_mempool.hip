@@ -6,8 +6,9 @@
 //     digest  = Digest(SHA-512(message)[..32])
 //     Signature::from_bytes(sig[..32], sig[32..64]).verify(&digest, &PublicKey(pk))
 //
-// Stage 1 (hsv_tx_record_kernel, one lane per transaction) hashes the message
-// and writes the 128-byte record pk || R || s || digest; stage 2 is the
+// Stage 1 (hsv_tx_record_kernel, one lane per transaction, loads staged through
+// LDS by the whole wave) hashes the message and writes the 128-byte record
+// pk || R || s || digest; stage 2 is the
 // generic verification launch over those records (strides 128, the same
 // kernels and flags as hsv_verify_device).  The record pass is a small
 // fraction of a verification: a 512-byte transaction is 4 SHA-512 blocks
@@ -37,26 +38,96 @@ __device__ __forceinline__ bool tx_span(const uint64_t *offsets, uint64_t tx_siz
   return hi >= lo && hi - lo >= 96;
 }
 
+constexpr int kTxWaves = kTxBlock / 64;
+constexpr int kTxQ = 9;                   // 16-B chunks under a 128-B window at any offset
+constexpr uint64_t kNoChunk = ~0ull;      // lane without a transaction: loads nothing
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// The wave's NQ chunks starting at chunk first(t) (clamped to last(t)) for each
+// of its 64 transactions t, staged through LDS with consecutive lanes reading
+// consecutive chunks of one transaction (one load instruction covers about
+// 64/NQ transactions' runs instead of 64 scattered lines); lane l gets the raw
+// words of its own transaction.
+template <int NQ>
+__device__ __forceinline__ void tx_stage_chunks(const uint4 *__restrict__ q, uint4 *stage, uint32_t lane,
+                                                uint64_t first, uint64_t last, uint32_t raw[4 * NQ + 1]) {
+  HSV_UNROLL
+  for (int it = 0; it < NQ; ++it) {
+    const uint32_t e = (uint32_t)it * 64u + lane;  // = t * NQ + c
+    const uint32_t t = e / NQ, c = e - t * NQ;
+    const uint64_t f = shfl_u64(first, (int)t), l = shfl_u64(last, (int)t);
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (l != kNoChunk) {
+      const uint64_t k = f + c;
+      v = q[k < l ? k : l];
+    }
+    stage[e] = v;
+  }
+  __builtin_amdgcn_wave_barrier();
+  HSV_UNROLL
+  for (int k = 0; k < NQ; ++k) {
+    const uint4 v = stage[lane * NQ + k];
+    raw[4 * k] = v.x;
+    raw[4 * k + 1] = v.y;
+    raw[4 * k + 2] = v.z;
+    raw[4 * k + 3] = v.w;
+  }
+  raw[4 * NQ] = 0u;
+  __builtin_amdgcn_wave_barrier();  // every lane has read before the next staging round
+}
+
+// One lane per transaction; the wave's loads are cooperative (tx_stage_chunks).
+// Waves are independent: each loops over its own longest message.
 __global__ void __launch_bounds__(kTxBlock) hsv_tx_record_kernel(const uint8_t *__restrict__ txs,
                                                                   const uint64_t *__restrict__ offsets,
                                                                   uint64_t tx_size, uint32_t n,
                                                                   uint4 *__restrict__ rec) {
+  __shared__ uint4 stage_all[kTxWaves][64 * kTxQ];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  if (blockIdx.x * kTxBlock + wv * 64u >= n) return;  // whole wave past the end
+  uint4 *stage = stage_all[wv];
   const uint32_t i = blockIdx.x * kTxBlock + threadIdx.x;
-  if (i >= n) return;
-  uint64_t lo, hi;
+  uint64_t lo = 0, hi = 0;
+  const bool ok = i < n && tx_span(offsets, tx_size, i, lo, hi);
+  const uintptr_t base = reinterpret_cast<uintptr_t>(txs);
+  const uint4 *q = reinterpret_cast<const uint4 *>(base & ~uintptr_t(15));
+  const uint64_t start = (uint64_t)(base & 15u) + lo;
+  const uint64_t mlen = ok ? hi - lo - 96 : 0;
+  const uint64_t q_last = ok ? (start + (hi - lo) - 1) >> 4 : kNoChunk;
   uint32_t r[32];
-  if (tx_span(offsets, tx_size, i, lo, hi)) {
-    const uintptr_t base = reinterpret_cast<uintptr_t>(txs);
-    const uint4 *q = reinterpret_cast<const uint4 *>(base & ~uintptr_t(15));
-    auto ld = [q](uint64_t k, uint32_t w[4]) {
-      const uint4 v = q[k];
-      w[0] = v.x;
-      w[1] = v.y;
-      w[2] = v.z;
-      w[3] = v.w;
-    };
-    tx_record(ld, (uint64_t)(base & 15u) + lo, hi - lo, r);
-  } else {
+  // pk || R || s: the last 96 bytes (7 chunks at any offset)
+  {
+    const uint64_t tail = start + mlen;
+    uint32_t raw[4 * 7 + 1];
+    tx_stage_chunks<7>(q, stage, lane, tail >> 4, q_last, raw);
+    tx_realign<24>(raw, (uint32_t)(tail & 15u), r);
+  }
+  // SHA-512 of the message, block by block
+  uint64_t h[8];
+  sha512_init(h);
+  const uint64_t nblocks = tx_num_blocks(mlen);
+  uint32_t wave_blocks = (uint32_t)nblocks;
+  HSV_UNROLL
+  for (int m = 1; m < 64; m <<= 1) wave_blocks = max(wave_blocks, (uint32_t)__shfl_xor((int)wave_blocks, m, 64));
+  const uint32_t sh16 = (uint32_t)(start & 15u);
+  HSV_NOUNROLL
+  for (uint32_t b = 0; b < wave_blocks; ++b) {
+    uint32_t raw[4 * kTxQ + 1];
+    tx_stage_chunks<kTxQ>(q, stage, lane, (start >> 4) + 8ull * b, q_last, raw);
+    if (b < nblocks) {
+      uint32_t words[32];
+      tx_realign<32>(raw, sh16, words);
+      tx_compress_block(h, words, mlen, b, nblocks);
+    }
+  }
+  tx_digest_words(h, r + 24);
+  if (i >= n) return;
+  if (!ok) {
     HSV_UNROLL
     for (int j = 0; j < 32; ++j) r[j] = 0u;
   }

@@ -37,7 +37,18 @@ static const uint64_t kSha512K[80] = {
     0x28db77f523047d84ull, 0x32caab7b40c72493ull, 0x3c9ebe0a15c9bebcull, 0x431d67c49c100d4cull,
     0x4cc5d4becb3e42b6ull, 0x597f299cfc657e2aull, 0x5fcb6fab3ad6faecull, 0x6c44198c4a475817ull};
 
-HSV_INL uint64_t sha_rotr(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit rotate; on gfx950 two v_alignbit_b32 on the halves (n is a constant
+// at every call site, so the branch folds)
+HSV_INL uint64_t sha_rotr(uint64_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  if (n < 32)
+    return ((uint64_t)__builtin_amdgcn_alignbit(lo, hi, n) << 32) | __builtin_amdgcn_alignbit(hi, lo, n);
+  return ((uint64_t)__builtin_amdgcn_alignbit(hi, lo, n - 32) << 32) | __builtin_amdgcn_alignbit(lo, hi, n - 32);
+#else
+  return (x >> n) | (x << (64 - n));
+#endif
+}
 
 HSV_INL uint32_t bswap32(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0x0000ff00u) | ((x << 8) & 0x00ff0000u) | (x << 24);
@@ -50,30 +61,39 @@ HSV_INL void sha512_init(uint64_t h[8]) {
   h[6] = 0x1f83d9abfb41bd6bull; h[7] = 0x5be0cd19137e2179ull;
 }
 
+// One SHA-512 round with message word wj and round constant kj.
+HSV_INL void sha512_round(uint64_t &a, uint64_t &b, uint64_t &c, uint64_t &d, uint64_t &e, uint64_t &f,
+                          uint64_t &g, uint64_t &hh, uint64_t wj, uint64_t kj) {
+  const uint64_t S1 = sha_rotr(e, 14) ^ sha_rotr(e, 18) ^ sha_rotr(e, 41);
+  const uint64_t ch = (e & f) ^ (~e & g);
+  const uint64_t t1 = hh + S1 + ch + kj + wj;
+  const uint64_t S0 = sha_rotr(a, 28) ^ sha_rotr(a, 34) ^ sha_rotr(a, 39);
+  const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
+  hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+}
+
 // One compression of the 16-word block w (big-endian words already assembled).
+// Rounds 0-15 use w directly; rounds 16-79 run as a loop of four 16-round
+// groups that extend the schedule in place.  No branch inside a group: a
+// per-round "first group?" test made the compiler copy the whole w array and
+// state through phi moves every round.
 HSV_INL void sha512_compress(uint64_t h[8], uint64_t w[16]) {
   uint64_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+  HSV_UNROLL
+  for (int j = 0; j < 16; ++j) {
+    sha512_round(a, b, c, d, e, f, g, hh, w[j], kSha512K[j]);
+    // 16 rounds rotate the eight state names back to where they started
+  }
   HSV_NOUNROLL
-  for (int blk = 0; blk < 5; ++blk) {
+  for (int blk = 1; blk < 5; ++blk) {
     HSV_UNROLL
     for (int j = 0; j < 16; ++j) {
-      uint64_t wj;
-      if (blk == 0) {
-        wj = w[j];
-      } else {
-        uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
-        uint64_t s0 = sha_rotr(w15, 1) ^ sha_rotr(w15, 8) ^ (w15 >> 7);
-        uint64_t s1 = sha_rotr(w2, 19) ^ sha_rotr(w2, 61) ^ (w2 >> 6);
-        wj = w[j] + s0 + w[(j + 9) & 15] + s1;
-        w[j] = wj;
-      }
-      uint64_t S1 = sha_rotr(e, 14) ^ sha_rotr(e, 18) ^ sha_rotr(e, 41);
-      uint64_t ch = (e & f) ^ (~e & g);
-      uint64_t t1 = hh + S1 + ch + kSha512K[blk * 16 + j] + wj;
-      uint64_t S0 = sha_rotr(a, 28) ^ sha_rotr(a, 34) ^ sha_rotr(a, 39);
-      uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
-      uint64_t t2 = S0 + mj;
-      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+      const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+      const uint64_t s0 = sha_rotr(w15, 1) ^ sha_rotr(w15, 8) ^ (w15 >> 7);
+      const uint64_t s1 = sha_rotr(w2, 19) ^ sha_rotr(w2, 61) ^ (w2 >> 6);
+      const uint64_t wj = w[j] + s0 + w[(j + 9) & 15] + s1;
+      w[j] = wj;
+      sha512_round(a, b, c, d, e, f, g, hh, wj, kSha512K[blk * 16 + j]);
     }
   }
   h[0] += a; h[1] += b; h[2] += c; h[3] += d;
