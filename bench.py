@@ -58,7 +58,9 @@ def pmc_traffic(variant, n):
             t = json.load(f)
     except (OSError, ValueError):
         return None, None
-    if t.get("variant") != variant or t.get("n") != n:
+    # variant 21 runs variant 19's kernels above 2^13 items (its pair form is for small batches)
+    same = {variant, 19} if (variant == 21 and n > (1 << 13)) else {variant}
+    if t.get("variant") not in same or t.get("n") != n:
         return None, None
     return 2 * t["fetch_bytes_per_launch"] + t["write_bytes_per_launch"], t.get("source")
 
@@ -358,7 +360,7 @@ def main():
             "work_per_verify": f"{WORK_MACS} u32 MACs (SURVEY 8(d)); {IO_BYTES} HBM bytes algorithmic",
             "kernel_ms": kernel_ms,
             "kernels": ("hsv_prep_kernel + hsv_verify_hp_kernel (one verify launch: scalar prepass, point pass)"
-                        if verifier.get_variant() in (19, 20) else "hsv_verify_hc_kernel"),
+                        if verifier.get_variant() in (19, 20, 21) else "hsv_verify_hc_kernel"),
         },
         "checks": {"honest_all_accepted": honest_ok, "corrupted_all_rejected": corrupt_rejected,
                    "strict_accepted_global": global_accepted},

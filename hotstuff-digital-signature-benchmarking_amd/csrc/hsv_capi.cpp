@@ -60,7 +60,9 @@ struct Global {
   bool inited = false;
   int ndev = 0;
   std::vector<DevCtx *> ctx;
-  std::atomic<int> variant{19};  // fastest measured: scalar prepass + half-size point pass, wide B comb, WA=4, 3 waves/SIMD
+  // fastest measured: scalar prepass + half-size point pass, wide B comb, WA=4,
+  // 3 waves/SIMD; two lanes per item for batches of at most 2^13 (QC latency)
+  std::atomic<int> variant{21};
 };
 
 Global &G() {

@@ -396,6 +396,122 @@ hsv_verify_hp_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const u
   }
 }
 
+// ---- latency form for small batches: two lanes per item ------------------
+// A lone wave issues one VALU instruction per 4 clocks whatever its lane
+// count, so a QC of 67 or 667 votes costs one verification's instruction
+// count end to end.  Here the even lane of a pair owns R and the odd lane A:
+// each decompresses its own point, builds its own table, runs a one-scalar
+// Straus loop (c1 for R, |c0| for A: 34 windows, 4 doublings + 1 addition)
+// and half of the wide B comb (digits 0-7 / 8-15); the two partial sums meet
+// through a lane swap and one addition.  Per lane that is one root chain
+// instead of two and half the additions, with the same 136 doublings.
+
+// q += sum of comb digits [8h, 8h + 8) of s (CB = 16) or [16h, 16h + 16) (CB = 8)
+template <int CB>
+__device__ __forceinline__ ge_ext comb_add_b_half(ge_ext q, const uint32_t s[8], const uint32_t *tb, uint32_t h) {
+  constexpr int NP = 256 / CB, HALF = NP / 2;
+  constexpr int ENT = 1 << (CB - 1);
+  uint32_t sr[9];
+  recode_add<9, CB, NP>(s, 8, sr);
+  HSV_UNROLL
+  for (int i = 0; i < 4; ++i) sr[i] = h ? sr[i + 4] : sr[i];  // the upper 128 bits for h = 1
+  HSV_NOUNROLL
+  for (int j = 0; j < HALF; ++j) {
+    const uint32_t cb = sr[0] & ((1u << CB) - 1u);
+    HSV_UNROLL
+    for (int i = 0; i < 3; ++i) sr[i] = (sr[i] >> CB) | (sr[i + 1] << (32 - CB));
+    sr[3] >>= CB;
+    const CombPosTab tpb{tb + (uint64_t)(j + (int)h * HALF) * ENT * kCombEntryWords};
+    q = ge_add_niels<true>(q, select_niels<CB>(tpb, cb));
+  }
+  return q;
+}
+
+__device__ __forceinline__ fe fe_swap_pair(const fe &a) {
+  fe r;
+  HSV_UNROLL
+  for (int i = 0; i < kFeLimbs; ++i) r.v[i] = (uint32_t)__shfl_xor((int)a.v[i], 1, 64);
+  return r;
+}
+
+// Pair-lane point pass of a prepped (non-fallback) item; both lanes of the
+// pair return the item's flag byte.  p = lane parity: 0 owns R, 1 owns A.
+template <int WA, int CB, class VT>
+__device__ __forceinline__ uint32_t verify_pair_prepped(uint32_t p, const uint32_t pk[8], const uint32_t rb[8],
+                                                        const uint32_t *rec, uint64_t stride, uint32_t meta,
+                                                        const uint32_t *tb, VT &vt) {
+  using G = HalfCombWindows<WA>;
+  constexpr int TS = 1 << (WA - 1);
+  uint32_t pt[8];
+  HSV_UNROLL
+  for (int i = 0; i < 8; ++i) pt[i] = p ? pk[i] : rb[i];
+  uint32_t ok, small;
+  {
+    fe x, y;
+    ok = ge_decompress(pt, x, y);
+    small = ok & y_is_small_order(y);
+    vt_build<TS>(vt, 0, fe_carry(fe_neg(x)), y);
+  }
+  uint32_t d[1][5];
+  HSV_UNROLL
+  for (int i = 0; i < 5; ++i) d[0][i] = rec[(uint64_t)(i + 5 * (int)p) * stride];
+  ge_ext q = straus_vt<WA, G::NW, 5, 1, false>(d, vt, (p && (meta & kPrepC0Neg)) ? 1u : 0u);
+  uint32_t b[8];
+  HSV_UNROLL
+  for (int i = 0; i < 8; ++i) b[i] = rec[(10 + i) * stride];
+  q = comb_add_b_half<CB>(q, b, tb, p);
+  ge_ext o;
+  o.X = fe_swap_pair(q.X);
+  o.Y = fe_swap_pair(q.Y);
+  o.Z = fe_swap_pair(q.Z);
+  o.T = fe_swap_pair(q.T);
+  q = ge_add_cached_rt(q, ge_to_cached(o), false);
+  const uint32_t ok_o = (uint32_t)__shfl_xor((int)ok, 1, 64), small_o = (uint32_t)__shfl_xor((int)small, 1, 64);
+  const uint32_t r_ok = p ? ok_o : ok, small_r = p ? small_o : small;
+  const uint32_t a_ok = p ? ok : ok_o, small_a = p ? small : small_o;
+  const uint32_t same = fe_is_zero(q.X) & fe_eq(q.Y, q.Z);
+  return flags_byte(meta & kPrepSOk, a_ok, r_ok, small_a, small_r, same);
+}
+
+// Pass 2 of the latency form: a plain grid of 2n lanes; lane t works on item
+// t / 2.  Fallback items (no short lattice pair) run the full-length path on
+// both lanes of their pair.
+template <int WA, int CB>
+__global__ void __launch_bounds__(kBlock)
+hsv_verify_pair_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const uint8_t *__restrict__ sig,
+                       uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
+                       uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
+                       uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b,
+                       const uint32_t *__restrict__ rec) {
+  constexpr int kEnt = (1 << (WA - 1)) + 1;
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)t * vt_lane_uint4<WA>()};
+  const uint32_t p = t & 1u, idx = t >> 1;
+  const bool valid = idx < n;
+  const uint32_t li = valid ? idx : n - 1u;
+  const uint32_t meta = rec[18ull * n + li];
+  uint32_t f;
+  if (meta & kPrepFallback) {
+    uint32_t pkw[8], sigw[16], msgw[8];
+    load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, li, pkw, sigw, msgw);
+    f = verify_one_full_comb<WA, false, CB>(pkw, sigw, msgw, comb_b, vt);
+  } else {
+    uint32_t pkw[8], rw[8];
+    const uint4 *pp = reinterpret_cast<const uint4 *>(pk + (uint64_t)li * pk_stride);
+    const uint4 *rp = reinterpret_cast<const uint4 *>(sig + (uint64_t)li * sig_stride);
+    const uint4 p0 = pp[0], p1 = pp[1], r0 = rp[0], r1 = rp[1];
+    pkw[0] = p0.x; pkw[1] = p0.y; pkw[2] = p0.z; pkw[3] = p0.w;
+    pkw[4] = p1.x; pkw[5] = p1.y; pkw[6] = p1.z; pkw[7] = p1.w;
+    rw[0] = r0.x; rw[1] = r0.y; rw[2] = r0.z; rw[3] = r0.w;
+    rw[4] = r1.x; rw[5] = r1.y; rw[6] = r1.z; rw[7] = r1.w;
+    f = verify_pair_prepped<WA, CB>(p, pkw, rw, rec + li, n, meta, comb_b, vt);
+  }
+  if (valid && p == 0u) {
+    if (flags_out) flags_out[idx] = (uint8_t)f;
+    if (strict_bits && (f & kStrictOk)) atomicOr(&strict_bits[idx >> 5], 1u << (idx & 31u));
+  }
+}
+
 // ---- v_mad_u64_u32 issue-rate probe -------------------------------------
 // 8 independent accumulation chains, 16 mads per asm statement (the compiler
 // puts an s_nop after every asm statement that writes an SGPR, so one mad per
@@ -444,7 +560,9 @@ __global__ void __launch_bounds__(256) hsv_mad_peak_kernel(uint32_t *sink, uint3
 //  19: two passes: scalar prepass, then the point pass with the fallback
 //      items dealt out first (WA 4, 3 waves/SIMD, wide comb)
 //  20: as 19, 2 waves/SIMD
-extern "C" int hsv_num_variants(void) { return 21; }
+//  21: as 19 for batches above 2^13 items; at or below, the latency form:
+//      prepass, then two lanes per item (hsv_verify_pair_kernel)
+extern "C" int hsv_num_variants(void) { return 22; }
 
 namespace {
 
@@ -577,6 +695,47 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
   return e != hipSuccess ? e : ef;
 }
 
+// Latency form (variant 21 below kPairMax items): prepass, then the pair
+// kernel on a plain grid of 2n lanes.  Workspace: per-lane tables | counters
+// (256 B) | fallback list | prep records.
+// At 2^12 items the pair form is 27 % faster end to end; at 2^15 it is 7 %
+// slower (the grid no longer fits one wave per SIMD), profiles/r01o_qc_latency.json.
+constexpr uint32_t kPairMax = 1u << 13;
+
+template <int WA, int CB>
+hipError_t launch_pair(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
+                       const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
+                       uint32_t *strict_bits, const uint32_t *comb_b, hipStream_t stream) {
+  const uint32_t lanes = 2u * n;
+  const uint32_t grid = (lanes + hsv::kBlock - 1) / hsv::kBlock;
+  const uint32_t prep_grid = (n + hsv::kBlock - 1) / hsv::kBlock;
+  const size_t ws_bytes = (size_t)grid * hsv::kBlock * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
+  const size_t fb_bytes = (size_t)n * sizeof(uint32_t);
+  const size_t rec_bytes = (size_t)n * hsv::kPrepWords * sizeof(uint32_t);
+  void *ws = nullptr;
+  hipError_t e = hipMallocAsync(&ws, ws_bytes + 256 + fb_bytes + rec_bytes, stream);
+  if (e != hipSuccess) return e;
+  uint8_t *ws8 = static_cast<uint8_t *>(ws);
+  uint4 *vt_ws = reinterpret_cast<uint4 *>(ws);
+  hsv::HcCounters *ctr = reinterpret_cast<hsv::HcCounters *>(ws8 + ws_bytes);
+  uint32_t *fb_list = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256);
+  uint32_t *rec = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256 + fb_bytes);
+  e = hipMemsetAsync(ctr, 0, sizeof(hsv::HcCounters), stream);
+  if (e == hipSuccess && strict_bits) e = hipMemsetAsync(strict_bits, 0, (size_t)((n + 31u) / 32u) * 4u, stream);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL((hsv::hsv_prep_kernel<WA>), dim3(prep_grid), dim3(hsv::kBlock), 0, stream, pk, pk_stride,
+                       sig, sig_stride, msg, msg_stride, n, rec, ctr, fb_list);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL((hsv::hsv_verify_pair_kernel<WA, CB>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
+                       pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, vt_ws, comb_b, rec);
+    e = hipGetLastError();
+  }
+  const hipError_t ef = hipFreeAsync(ws, stream);
+  return e != hipSuccess ? e : ef;
+}
+
 }  // namespace
 
 extern "C" hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t pk_stride,
@@ -622,6 +781,10 @@ extern "C" hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t
       return launch_hp<4, 3, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
     case 20: if (!comb_b) return hipErrorInvalidValue;
       return launch_hp<4, 2, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
+    case 21: if (!comb_b) return hipErrorInvalidValue;
+      if (n <= kPairMax)
+        return launch_pair<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
+      return launch_hp<4, 3, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
 #undef HSV_LAUNCH_MT
     default: return hipErrorInvalidValue;
   }
@@ -655,6 +818,6 @@ extern "C" double hsv_launch_mad_peak(int device_cus) {
 
 extern "C" int hsv_variant_needs_comb(int variant) {
   if (variant >= 10 && variant <= 14) return 8;
-  if (variant >= 15 && variant <= 20) return 16;
+  if (variant >= 15 && variant <= 21) return 16;
   return 0;
 }
