@@ -8,6 +8,8 @@
 //                          64 mixed additions from the key's table and the B
 //                          table, then R decompression and the projective
 //                          comparison.  Same flag byte as hsv_verify_kernel.
+//  hsv_comb_verify_quad_kernel  the same check with four lanes per vote,
+//                          for batches of at most 2^12 votes (QC latency).
 #include <hip/hip_runtime.h>
 
 #include "hsv_comb.hpp"
@@ -68,6 +70,105 @@ hsv_comb_verify_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__re
   flags_out[i] = kvalid ? (uint8_t)f : (uint8_t)0;
 }
 
+// Latency form of hsv_comb_verify_kernel for small batches (a QC is 67 or
+// 667 votes): four lanes per vote.  Lane g of a quad adds the comb entries of
+// positions 8g .. 8g+7 for both k (the key's table) and s (the B table): 16
+// mixed additions instead of 64; the quad's partial sums meet through two
+// lane-swap + addition rounds.  Every lane of the quad hashes and decompresses
+// R itself (same instruction stream, no extra latency), so flags come out of
+// lane 0 exactly as verify_one_comb computes them.
+constexpr int kCombQuad = 4;
+constexpr int kCombPosPerLane = kCombPos / kCombQuad;
+
+__device__ __forceinline__ ge_ext ge_swap_xor(const ge_ext &p, int m) {
+  ge_ext r;
+  HSV_UNROLL
+  for (int i = 0; i < kFeLimbs; ++i) {
+    r.X.v[i] = (uint32_t)__shfl_xor((int)p.X.v[i], m, 64);
+    r.Y.v[i] = (uint32_t)__shfl_xor((int)p.Y.v[i], m, 64);
+    r.Z.v[i] = (uint32_t)__shfl_xor((int)p.Z.v[i], m, 64);
+    r.T.v[i] = (uint32_t)__shfl_xor((int)p.T.v[i], m, 64);
+  }
+  return r;
+}
+
+__global__ void __launch_bounds__(256)
+hsv_comb_verify_quad_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__restrict__ sig,
+                            uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride,
+                            uint32_t m, const uint8_t *__restrict__ pks, const uint8_t *__restrict__ key_flags,
+                            uint32_t nkeys, const uint32_t *__restrict__ tables,
+                            const uint32_t *__restrict__ btable, uint8_t *__restrict__ flags_out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i0 = t / kCombQuad, g = t % kCombQuad;
+  const bool valid = i0 < m;
+  const uint32_t i = valid ? i0 : m - 1u;  // whole quads past the end compute a copy
+  const uint32_t kidx = key_idx[i];
+  const bool kvalid = kidx < nkeys;
+  const uint32_t kk = kvalid ? kidx : 0u;
+  uint32_t pkw[8], sigw[16], msgw[8];
+  {
+    const uint4 *p = reinterpret_cast<const uint4 *>(pks + (uint64_t)kk * 32);
+    const uint4 *sp = reinterpret_cast<const uint4 *>(sig + (uint64_t)i * sig_stride);
+    const uint4 *gp = reinterpret_cast<const uint4 *>(msg + (uint64_t)i * msg_stride);
+    const uint4 p0 = p[0], p1 = p[1];
+    const uint4 s0 = sp[0], s1 = sp[1], s2 = sp[2], s3 = sp[3];
+    const uint4 m0 = gp[0], m1 = gp[1];
+    pkw[0] = p0.x; pkw[1] = p0.y; pkw[2] = p0.z; pkw[3] = p0.w;
+    pkw[4] = p1.x; pkw[5] = p1.y; pkw[6] = p1.z; pkw[7] = p1.w;
+    sigw[0] = s0.x; sigw[1] = s0.y; sigw[2] = s0.z; sigw[3] = s0.w;
+    sigw[4] = s1.x; sigw[5] = s1.y; sigw[6] = s1.z; sigw[7] = s1.w;
+    sigw[8] = s2.x; sigw[9] = s2.y; sigw[10] = s2.z; sigw[11] = s2.w;
+    sigw[12] = s3.x; sigw[13] = s3.y; sigw[14] = s3.z; sigw[15] = s3.w;
+    msgw[0] = m0.x; msgw[1] = m0.y; msgw[2] = m0.z; msgw[3] = m0.w;
+    msgw[4] = m1.x; msgw[5] = m1.y; msgw[6] = m1.z; msgw[7] = m1.w;
+  }
+  const uint32_t s_ok = sc_is_canonical(sigw + 8);
+  uint32_t h[16];
+  sha512_96(sigw, pkw, msgw, h);
+  const sc k = sc_reduce512(h);
+  uint32_t kr[9], sr[9];
+  recode_add<9, 8, kCombPos>(k.v, 8, kr);
+  recode_add<9, 8, kCombPos>(sigw + 8, 8, sr);
+  // this lane's 8 digits = bytes 8g .. 8g+7 = words 2g, 2g+1 (selects, no register indexing)
+  uint64_t kd = 0, sd = 0;
+  HSV_UNROLL
+  for (int q4 = 0; q4 < kCombQuad; ++q4) {
+    const bool me = g == (uint32_t)q4;
+    kd = me ? ((uint64_t)kr[2 * q4 + 1] << 32) | kr[2 * q4] : kd;
+    sd = me ? ((uint64_t)sr[2 * q4 + 1] << 32) | sr[2 * q4] : sd;
+  }
+  const uint32_t *ta = tables + (uint64_t)kk * kCombTableWords;
+  ge_ext q = ge_identity();
+  HSV_NOUNROLL
+  for (int jj = 0; jj < kCombPosPerLane; ++jj) {
+    const uint32_t j = g * kCombPosPerLane + (uint32_t)jj;
+    const uint32_t ca = (uint32_t)kd & 0xffu, cb = (uint32_t)sd & 0xffu;
+    kd >>= 8;
+    sd >>= 8;
+    const CombPosTab tpa{ta + (uint64_t)j * kCombEnt * kCombEntryWords};
+    const CombPosTab tpb{btable + (uint64_t)j * kCombEnt * kCombEntryWords};
+    q = ge_add_niels<true>(q, select_niels<8>(tpa, ca));
+    q = ge_add_niels<true>(q, select_niels<8>(tpb, cb));
+  }
+  q = ge_add_cached_rt(q, ge_to_cached(ge_swap_xor(q, 1)), true);
+  q = ge_add_cached_rt(q, ge_to_cached(ge_swap_xor(q, 2)), false);
+
+  fe rx, ry;
+  const uint32_t r_ok = ge_decompress(sigw, rx, ry);
+  const uint32_t small_r = r_ok & y_is_small_order(ry);
+  const uint32_t same = ge_eq_affine(q, rx, ry);
+  const uint32_t kf = key_flags[kk];
+  const uint32_t a_ok = (kf & kKeyAOk) ? 1u : 0u;
+  const uint32_t small_a = a_ok & ((kf & kKeySmallA) ? 1u : 0u);
+  const uint32_t parse_ok = s_ok & a_ok & r_ok;
+  const uint32_t eq_ok = parse_ok & same;
+  const uint32_t strict_ok = eq_ok & (small_a ^ 1u) & (small_r ^ 1u);
+  const uint32_t f = (strict_ok ? kStrictOk : 0u) | (eq_ok ? kEqOk : 0u) | (parse_ok ? kParseOk : 0u) |
+                     (small_a ? kSmallA : 0u) | (small_r ? kSmallR : 0u) | (s_ok ? kSOk : 0u) |
+                     (a_ok ? kAOk : 0u) | (r_ok ? kROk : 0u);
+  if (valid && g == 0u) flags_out[i0] = kvalid ? (uint8_t)f : (uint8_t)0;
+}
+
 // one lane per (position j, chunk c) of the wide B table; j is wave-uniform
 // (256 chunks per position)
 __global__ void __launch_bounds__(256) hsv_comb16_build_kernel(uint32_t *__restrict__ table,
@@ -106,12 +207,22 @@ extern "C" hipError_t hsv_launch_comb_build(const uint8_t *encs, uint32_t nkeys,
   return hipGetLastError();
 }
 
+// batches up to this many votes take the four-lanes-per-vote form
+static constexpr uint32_t kCombQuadMax = 1u << 12;
+
 extern "C" hipError_t hsv_launch_comb_verify(const uint32_t *key_idx, const uint8_t *sig, uint64_t sig_stride,
                                              const uint8_t *msg, uint64_t msg_stride, uint32_t m,
                                              const uint8_t *pks, const uint8_t *key_flags, uint32_t nkeys,
                                              const uint32_t *tables, const uint32_t *btable,
                                              uint8_t *flags_out, hipStream_t stream) {
   if (m == 0) return hipSuccess;
+  if (m <= kCombQuadMax) {  // latency form: four lanes per vote
+    const uint64_t lanes = (uint64_t)m * hsv::kCombQuad;
+    hipLaunchKernelGGL(hsv::hsv_comb_verify_quad_kernel, dim3((uint32_t)((lanes + 255u) / 256u)), dim3(256), 0,
+                       stream, key_idx, sig, sig_stride, msg, msg_stride, m, pks, key_flags, nkeys, tables, btable,
+                       flags_out);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(hsv::hsv_comb_verify_kernel, dim3((m + 255u) / 256u), dim3(256), 0, stream, key_idx, sig,
                      sig_stride, msg, msg_stride, m, pks, key_flags, nkeys, tables, btable, flags_out);
   return hipGetLastError();

@@ -87,3 +87,22 @@ def test_committee_device_api(mods, golden):
         c.verify_device(idx, sig, msg, flags)
         torch.cuda.synchronize()
         assert (flags.cpu().numpy() == golden["flags"]).all()
+
+
+def test_committee_quad_and_single_lane_forms_agree(mods, golden):
+    """Batches of at most 2^12 votes take the four-lanes-per-vote kernel
+    (hsv_comb_verify_quad_kernel), larger ones the one-lane kernel: the golden
+    set tiled to 3 x 2193 = 6579 votes goes through the one-lane form, its
+    first 4096 and a ragged 4095 through the quad form; all must equal the
+    golden flags (and a lone vote, the smallest quad grid)."""
+    committee, _, _, _ = mods
+    keys = sorted({bytes(k) for k in golden["pk"]})
+    kidx = {k: i for i, k in enumerate(keys)}
+    idx = np.array([kidx[bytes(k)] for k in golden["pk"]], np.uint32)
+    rep = np.arange(3 * len(idx)) % len(idx)
+    with committee.Committee(np.frombuffer(b"".join(keys), np.uint8).reshape(-1, 32)) as c:
+        for m in (len(rep), 4096, 4095, 1):
+            sel = rep[:m]
+            got = c.verify_flags(idx[sel], golden["sig"][sel], golden["msg"][sel])
+            bad = np.nonzero(got != golden["flags"][sel])[0]
+            assert bad.size == 0, (m, [golden["cases"][sel[i]] for i in bad[:8]])
