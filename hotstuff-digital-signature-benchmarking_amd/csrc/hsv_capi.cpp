@@ -657,6 +657,8 @@ int run_tx_host(const uint8_t *txs, const uint64_t *offsets, size_t tx_size, siz
 
 extern "C" {
 
+int hsv_set_error(int code, const char *msg) { return fail(code, msg ? msg : ""); }
+
 int hsv_verify_transactions(const uint8_t *txs, const uint64_t *offsets, size_t n, uint8_t *flags_out) {
   if (n && !offsets) return fail(HSV_ERR_INVALID_ARG, "null offsets");
   return run_tx_host(txs, offsets, 0, n, flags_out);

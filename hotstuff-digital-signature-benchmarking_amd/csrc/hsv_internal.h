@@ -59,3 +59,13 @@ hipError_t hsv_launch_tx_mask(const uint64_t *offsets, uint32_t n, uint8_t *flag
 #ifdef __cplusplus
 }
 #endif
+
+// ---- error reporting shared by the C-ABI translation units -----------------
+#ifdef __cplusplus
+extern "C" {
+#endif
+// sets hsv_last_error() on the calling thread; returns code
+int hsv_set_error(int code, const char *msg);
+#ifdef __cplusplus
+}
+#endif

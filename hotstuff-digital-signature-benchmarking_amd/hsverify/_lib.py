@@ -36,6 +36,7 @@ ERRORS = {
     -3: "HSV_ERR_INVALID_ARG",
     -4: "HSV_ERR_ALLOC",
     -5: "HSV_ERR_ALIGN",
+    -6: "HSV_ERR_PARSE",
 }
 
 
@@ -66,6 +67,8 @@ def _declare(lib):
         "hsv_verify_transactions": (ctypes.c_int, [c_u8p, c_u8p, sz, c_u8p]),
         "hsv_verify_transactions_fixed": (ctypes.c_int, [c_u8p, sz, sz, c_u8p]),
         "hsv_verify_transactions_device": (ctypes.c_int, [c_u8p, c_u8p, sz, sz, c_u8p, c_u8p, ctypes.c_void_p]),
+        "hsv_qc_verify_bincode": (ctypes.c_int, [c_u8p, sz, ctypes.POINTER(ctypes.c_size_t), c_u8p]),
+        "hsv_tc_verify_bincode": (ctypes.c_int, [c_u8p, sz, ctypes.POINTER(ctypes.c_size_t), c_u8p]),
         "hsv_public_key": (ctypes.c_int, [c_u8p, c_u8p]),
         "hsv_sign": (ctypes.c_int, [c_u8p, c_u8p, sz, c_u8p]),
         "hsv_sign_many": (ctypes.c_int, [c_u8p, c_u8p, sz, sz, c_u8p, c_u8p, ctypes.c_int]),

@@ -10,6 +10,10 @@
  *   (batched strict API)                     -> hsv_verify
  *   crypto::Signature::new           crypto/src/lib.rs:185-191  -> hsv_sign
  *   crypto::generate_keypair         crypto/src/lib.rs:167-175  -> hsv_public_key
+ *   mempool transaction check  mempool/src/batch_maker.rs:79-85 -> hsv_verify_transactions*
+ *   QC / TC signature checks from wire bytes
+ *                        consensus/src/messages.rs:180-198, 290-315 -> hsv_qc_verify_bincode,
+ *                                                                   hsv_tc_verify_bincode
  *
  * Plain pointers and sizes only.  All inputs are borrowed for the duration of
  * the call; the library never retains a caller pointer.  Every entry point is
@@ -50,6 +54,7 @@ extern "C" {
 #define HSV_ERR_INVALID_ARG (-3)
 #define HSV_ERR_ALLOC (-4)
 #define HSV_ERR_ALIGN (-5)
+#define HSV_ERR_PARSE (-6) /* malformed wire bytes (hsv_*_bincode) */
 
 /* ---- lifecycle ---------------------------------------------------------- */
 /* Optional: contexts are created lazily on first use.  device = -1 selects
@@ -154,6 +159,29 @@ int hsv_verify_transactions_fixed(const uint8_t *txs, size_t tx_size, size_t n, 
  * hsv_verify_device_bits (either may be NULL, not both). */
 int hsv_verify_transactions_device(const uint8_t *d_txs, const uint64_t *d_offsets, size_t tx_size, size_t n,
                                    uint8_t *d_flags, uint32_t *d_strict_bits, void *stream);
+
+/* ---- wire formats ---------------------------------- */
+/* Certificates verified straight from their bincode bytes (bincode 1.3
+ * defaults: little-endian, u64 lengths; PublicKey is its base64 string,
+ * crypto/src/lib.rs:94-101).  Only the signature part of the reference's
+ * verify is done here; the quorum/stake checks stay with the caller, who can
+ * get the decoded keys back.  Returns 1 = Ok, 0 = Err (a signature fails),
+ * HSV_ERR_PARSE for malformed bytes, other < 0 for infrastructure errors. */
+
+/* consensus::QC (consensus/src/messages.rs:162-167): hash (32) | round (u64)
+ * | votes Vec<(PublicKey, Signature)>.  Checks
+ * Signature::verify_batch(&qc.digest(), &qc.votes) (messages.rs:196-197),
+ * qc.digest() = SHA-512(hash || round_le)[..32] (messages.rs:201-207).
+ * n_votes_out (optional): number of votes; pks_out (optional, 32 B per vote):
+ * the decoded keys, in order. */
+int hsv_qc_verify_bincode(const uint8_t *buf, size_t len, size_t *n_votes_out, uint8_t *pks_out);
+
+/* consensus::TC (messages.rs:281-285): round (u64) | votes
+ * Vec<(PublicKey, Signature, Round)>.  Checks every vote with
+ * Signature::verify over SHA-512(round_le || high_qc_round_le)[..32]
+ * (messages.rs:306-313); 1 iff all pass.  flags_out (optional, one byte per
+ * vote): the per-vote HSV_* flags. */
+int hsv_tc_verify_bincode(const uint8_t *buf, size_t len, size_t *n_votes_out, uint8_t *flags_out);
 
 /* ---- signing (host CPU; not on the hot path) ---------------------------- */
 /* Public key for a 32-byte secret seed (dalek Keypair from SecretKey). */
