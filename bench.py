@@ -121,6 +121,25 @@ def qc_latency(reps):
         ts = np.array(ts) * 1e3
         res[f"n{committee}_votes{w.n}"] = {"p50_ms": float(np.percentile(ts, 50)),
                                             "p99_ms": float(np.percentile(ts, 99)), "reps": reps}
+    # the same C3 QC handed over as its bincode wire bytes (hsv_qc_verify_bincode:
+    # parse + base64 keys + qc.digest() on the host, verification on the GPU)
+    from hsverify import wire
+    import hashlib
+    w = synth.qc_votes(1000, seed=1000)
+    block_hash = hashlib.sha512(b"block" + (1000).to_bytes(4, "little")).digest()[:32]
+    buf = wire.encode_qc(block_hash, 1, [(bytes(p), bytes(q)) for p, q in zip(w.pk, w.sig)])
+    nv = ctypes.c_size_t(0)
+    for _ in range(10):
+        assert lib.hsv_qc_verify_bincode(buf, len(buf), ctypes.byref(nv), None) == 1
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        rc = lib.hsv_qc_verify_bincode(buf, len(buf), ctypes.byref(nv), None)
+        ts.append(time.perf_counter() - t0)
+        assert rc == 1
+    ts = np.array(ts) * 1e3
+    res["n1000_votes667_bincode"] = {"p50_ms": float(np.percentile(ts, 50)), "p99_ms": float(np.percentile(ts, 99)),
+                                     "reps": reps, "bytes": len(buf)}
     return res
 
 
