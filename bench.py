@@ -106,7 +106,7 @@ def qc_latency(reps):
     from hsverify import _lib, synth
     lib = _lib.load()
     res = {}
-    for committee in (100, 1000):
+    for committee in (4, 100, 1000):
         w = synth.qc_votes(committee, seed=committee)
         packed = np.concatenate([w.pk, w.sig], axis=1).tobytes()
         digest = bytes(w.msg)
@@ -121,6 +121,20 @@ def qc_latency(reps):
         ts = np.array(ts) * 1e3
         res[f"n{committee}_votes{w.n}"] = {"p50_ms": float(np.percentile(ts, 50)),
                                             "p99_ms": float(np.percentile(ts, 99)), "reps": reps}
+    # one strict verification (Vote::verify / Block::verify, consensus/src/messages.rs:136-146)
+    w = synth.qc_votes(4, seed=4)
+    pk0, sig0, d0 = bytes(w.pk[0]), bytes(w.sig[0]), bytes(w.msg)
+    for _ in range(10):
+        assert lib.hsv_verify_strict(d0, pk0, sig0) == 1
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        rc = lib.hsv_verify_strict(d0, pk0, sig0)
+        ts.append(time.perf_counter() - t0)
+        assert rc == 1
+    ts = np.array(ts) * 1e3
+    res["single_verify_strict"] = {"p50_ms": float(np.percentile(ts, 50)), "p99_ms": float(np.percentile(ts, 99)),
+                                   "reps": reps}
     # the same C3 QC handed over as its bincode wire bytes (hsv_qc_verify_bincode:
     # parse + base64 keys + qc.digest() on the host, verification on the GPU)
     from hsverify import wire
@@ -198,21 +212,35 @@ def committee_bench(reps, dev, n_votes=1 << 20):
     return res
 
 
-def qc_cpu(reps=3):
-    """Single-core C port verify_batch rule for the n=1000 QC (667 votes)."""
+def qc_cpu(reps=5):
+    """Single-core C port verify_batch rule for the C1 / C2 / C3 QCs (3, 67 and
+    667 votes): the reference's QC::verify path timed on one host core."""
     from hsverify import synth
     so = os.path.join(ROOT, "oracle", "_build", "libhsv_oracle.so")
     lib = ctypes.CDLL(so)
     lib.oracle_verify_batch.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
-    w = synth.qc_votes(1000, seed=1000)
-    pk, sig = np.ascontiguousarray(w.pk), np.ascontiguousarray(w.sig)
+    res = {"cores": 1, "kind": "port"}
+    for committee in (4, 100, 1000):
+        w = synth.qc_votes(committee, seed=committee)
+        pk, sig = np.ascontiguousarray(w.pk), np.ascontiguousarray(w.sig)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            ok = lib.oracle_verify_batch(bytes(w.msg), pk.ctypes.data, sig.ctypes.data, w.n)
+            ts.append(time.perf_counter() - t0)
+            assert ok == 1
+        res[f"n{committee}_votes{w.n}_p50_ms"] = float(np.median(ts) * 1e3)
+    lib.oracle_verify_flags.restype = ctypes.c_uint8
+    lib.oracle_verify_flags.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
+    w = synth.qc_votes(4, seed=4)
     ts = []
-    for _ in range(reps):
+    for _ in range(50):
         t0 = time.perf_counter()
-        ok = lib.oracle_verify_batch(bytes(w.msg), pk.ctypes.data, sig.ctypes.data, w.n)
+        f = lib.oracle_verify_flags(bytes(w.pk[0]), bytes(w.sig[0]), bytes(w.msg), 32)
         ts.append(time.perf_counter() - t0)
-        assert ok == 1
-    return {"n1000_votes667_p50_ms": float(np.median(ts) * 1e3), "cores": 1, "kind": "port"}
+        assert f & 1
+    res["single_verify_strict_p50_ms"] = float(np.median(ts) * 1e3)
+    return res
 
 
 def mempool_bench(dev, n=1 << 20, tx_size=512, cpu_sample=1 << 17):
