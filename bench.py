@@ -298,9 +298,17 @@ def main():
     ap.add_argument("--qc-reps", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-qc", action="store_true")
+    ap.add_argument("--global-n", type=int, default=None,
+                    help="C5 strong scaling: total triples split over the ranks (e.g. 16777216 = 2^24); "
+                         "default: weak scaling with --n per GPU")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    strong = a.global_n is not None
+    if strong:
+        if a.global_n % world:
+            raise SystemExit("--global-n must be divisible by the number of ranks")
+        a.n = a.global_n // world
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
@@ -382,12 +390,14 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": elapsed / a.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (seeded keys/digests, RFC 8032 signatures, 5% corrupted)",
         "config": {
-            "workload": "C4: 2^20 independent (pk, 32-B digest, sig) triples per GPU, inputs resident in HBM",
+            "workload": (f"C5: {a.n * world} independent triples split over {world} GPU(s), inputs resident in HBM"
+                         if strong else
+                         "C4: 2^20 independent (pk, 32-B digest, sig) triples per GPU, inputs resident in HBM"),
             "batch_per_gpu": a.n,
             "global_batch": a.n * world,
             "parallelism": f"dp{world} (contiguous shards, no collective on the data path)",
