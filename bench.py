@@ -286,6 +286,21 @@ def mempool_bench(dev, n=1 << 20, tx_size=512, cpu_sample=1 << 17):
     return res
 
 
+def host_api_bench(w, reps=3):
+    """The drop-in boundary hands over host buffers: hsv_verify on the C4 batch
+    from numpy arrays (pinned staging, H2D, kernels, D2H), PCIe-inclusive."""
+    from hsverify import verifier
+    verifier.verify_flags(w.pk, w.sig, w.msg)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        f = verifier.verify_flags(w.pk, w.sig, w.msg)
+        ts.append(time.perf_counter() - t0)
+    ms = float(np.median(ts) * 1e3)
+    return {"items": int(w.n), "ms": ms, "verif_per_s": w.n / (ms * 1e-3),
+            "honest_all_accepted": bool((f[w.honest] & 1).all())}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -431,6 +446,7 @@ def main():
         out["mempool_tx"] = mempool_bench(dev)
         if world == 1 and not a.no_cpu_baseline:
             out["qc_cpu_baseline"] = qc_cpu()
+        out["host_api"] = host_api_bench(w)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

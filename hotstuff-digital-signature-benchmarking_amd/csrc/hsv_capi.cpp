@@ -48,6 +48,7 @@ struct DevCtx {
   uint32_t *d_btable = nullptr;  // comb table of B (committee path), built lazily
   uint32_t *d_btable16 = nullptr;  // wide comb table of B (generic kernels 15, 16), built lazily
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // second pipeline stage of large host batches
   uint8_t *d_buf = nullptr;
   size_t d_cap = 0;
   uint8_t *h_buf = nullptr;
@@ -177,26 +178,52 @@ int comb_table_for(DevCtx &c, int variant, const uint32_t **out) {
 
 // Host records: item i at pk + i*pk_stride, sig + i*sig_stride, msg + i*msg_stride
 // (msg_stride 0 = shared).  Runs [0, n) on one device, chunk by chunk.
+// Batches of at least 2 * kPipeChunk items run as a two-stage pipeline: two
+// staging buffers and two streams, so the host packs chunk i+1 and the DMA
+// engine copies it while the kernels verify chunk i.
+constexpr size_t kPipeChunk = size_t(1) << 18;  // 32 MiB of inputs per pipelined chunk
+
 int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t *sig,
                   size_t sig_stride, const uint8_t *msg, size_t msg_stride, size_t n,
                   uint8_t *flags_out) {
   std::lock_guard<std::mutex> lk(c.mu);
-  const size_t chunk = std::min(n, kChunk);
+  const bool pipe = n >= 2 * kPipeChunk;
+  const size_t chunk = pipe ? kPipeChunk : std::min(n, kChunk);
+  const int nbuf = pipe ? 2 : 1;
   const size_t pk_off = 0;
   const size_t sig_off = round_up(chunk * 32, kAlign);
   const size_t msg_off = sig_off + round_up(chunk * 64, kAlign);
   const size_t msg_bytes = msg_stride ? chunk * 32 : 32;
   const size_t flag_off = msg_off + round_up(msg_bytes, kAlign);
   const size_t total = flag_off + round_up(chunk, kAlign);
-  int rc = ctx_prepare(c, total, total);
+  int rc = ctx_prepare(c, total * nbuf, total * nbuf);
   if (rc != HSV_OK) return rc;
+  if (pipe && !c.stream2) {
+    const hipError_t e = hipStreamCreateWithFlags(&c.stream2, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail("hipStreamCreate", e);
+  }
   const int variant = G().variant.load();
   const uint32_t *comb_b = nullptr;
   rc = comb_table_for(c, variant, &comb_b);
   if (rc != HSV_OK) return rc;
-  for (size_t base = 0; base < n; base += chunk) {
+  size_t pend_base[2] = {0, 0}, pend_m[2] = {0, 0};
+  // wait for buffer b's chunk and hand its flags to the caller
+  auto retire = [&](int b) -> int {
+    if (pend_m[b] == 0) return HSV_OK;
+    const hipError_t e = hipStreamSynchronize(b ? c.stream2 : c.stream);
+    if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
+    std::memcpy(flags_out + pend_base[b], c.h_buf + (size_t)b * total + flag_off, pend_m[b]);
+    pend_m[b] = 0;
+    return HSV_OK;
+  };
+  int b = 0;
+  for (size_t base = 0; base < n; base += chunk, b = (b + 1) % nbuf) {
     const size_t m = std::min(chunk, n - base);
-    uint8_t *h = c.h_buf;
+    rc = retire(b);
+    if (rc != HSV_OK) return rc;
+    hipStream_t s = b ? c.stream2 : c.stream;
+    uint8_t *h = c.h_buf + (size_t)b * total;
+    uint8_t *d = c.d_buf + (size_t)b * total;
     // pack into the dense layout the kernel reads (pk 32 | sig 64 | msg 32)
     if (pk_stride == 32) std::memcpy(h + pk_off, pk + base * 32, m * 32);
     else for (size_t i = 0; i < m; ++i) std::memcpy(h + pk_off + 32 * i, pk + (base + i) * pk_stride, 32);
@@ -206,16 +233,19 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
     else if (msg_stride == 32) std::memcpy(h + msg_off, msg + base * 32, m * 32);
     else for (size_t i = 0; i < m; ++i) std::memcpy(h + msg_off + 32 * i, msg + (base + i) * msg_stride, 32);
     const size_t in_bytes = msg_off + (msg_stride ? m * 32 : 32);
-    hipError_t e = hipMemcpyAsync(c.d_buf, h, in_bytes, hipMemcpyHostToDevice, c.stream);
+    hipError_t e = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return hip_fail("hipMemcpyAsync H2D", e);
-    e = hsv_launch_verify(variant, c.d_buf + pk_off, 32, c.d_buf + sig_off, 64, c.d_buf + msg_off,
-                          msg_stride ? 32 : 0, (uint32_t)m, c.d_buf + flag_off, nullptr, comb_b, c.stream);
+    e = hsv_launch_verify(variant, d + pk_off, 32, d + sig_off, 64, d + msg_off, msg_stride ? 32 : 0,
+                          (uint32_t)m, d + flag_off, nullptr, comb_b, s);
     if (e != hipSuccess) return hip_fail("verify kernel launch", e);
-    e = hipMemcpyAsync(h + flag_off, c.d_buf + flag_off, m, hipMemcpyDeviceToHost, c.stream);
+    e = hipMemcpyAsync(h + flag_off, d + flag_off, m, hipMemcpyDeviceToHost, s);
     if (e != hipSuccess) return hip_fail("hipMemcpyAsync D2H", e);
-    e = hipStreamSynchronize(c.stream);
-    if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
-    std::memcpy(flags_out + base, h + flag_off, m);
+    pend_base[b] = base;
+    pend_m[b] = m;
+  }
+  for (int k = 0; k < nbuf; ++k) {
+    rc = retire(k);
+    if (rc != HSV_OK) return rc;
   }
   return HSV_OK;
 }
@@ -268,6 +298,7 @@ void hsv_shutdown(void) {
     std::lock_guard<std::mutex> lk2(c->mu);
     if (hipSetDevice(c->device) == hipSuccess) {
       if (c->stream) (void)hipStreamDestroy(c->stream);
+      if (c->stream2) (void)hipStreamDestroy(c->stream2);
       if (c->d_buf) (void)hipFree(c->d_buf);
       if (c->h_buf) (void)hipHostFree(c->h_buf);
       if (c->d_btable) (void)hipFree(c->d_btable);
@@ -275,7 +306,7 @@ void hsv_shutdown(void) {
     }
     c->d_btable = nullptr;
     c->d_btable16 = nullptr;
-    c->stream = nullptr;
+    c->stream = c->stream2 = nullptr;
     c->d_buf = c->h_buf = nullptr;
     c->d_cap = c->h_cap = 0;
   }

@@ -276,3 +276,23 @@ def test_c4_full_size_properties(api, oracle_lib):
     sample = np.sort(rng.choice(n, 8192, replace=False))
     exp = oracle_flags(oracle_lib, w.pk[sample], w.sig[sample], w.msg[sample])
     assert (f[sample] == exp).all()
+
+
+def test_host_api_pipelined_chunks_match_device_api(api, oracle_lib):
+    """Host batches of >= 2^19 items run as a two-stream pipeline of 2^18-item
+    chunks (hsv_capi.cpp run_on_device): an uneven tail chunk, every flag equal
+    to the device-resident launch, and an oracle-checked sample."""
+    import torch
+    _, verifier, synth = api
+    n = (1 << 19) + (1 << 18) + 12345
+    w = synth.independent_triples(n, seed=77, corrupt_frac=0.05)
+    got = verifier.verify_flags(w.pk, w.sig, w.msg)
+    dev = torch.device("cuda:0")
+    pk, sig, msg = (torch.from_numpy(a).to(dev) for a in (w.pk, w.sig, w.msg))
+    flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+    verifier.verify_device(pk, sig, msg, flags)
+    torch.cuda.synchronize()
+    assert (got == flags.cpu().numpy()).all()
+    assert (got[w.honest] & o.STRICT_OK).all() and not (got[~w.honest] & o.STRICT_OK).any()
+    sample = np.sort(np.random.default_rng(3).choice(n, 4096, replace=False))
+    assert (got[sample] == oracle_flags(oracle_lib, w.pk[sample], w.sig[sample], w.msg[sample])).all()
