@@ -183,11 +183,31 @@ int comb_table_for(DevCtx &c, int variant, const uint32_t **out) {
 // engine copies it while the kernels verify chunk i.
 constexpr size_t kPipeChunk = size_t(1) << 18;  // 32 MiB of inputs per pipelined chunk
 
+// memcpy into pinned staging; large copies are split over a few host threads
+// (one thread copies ~10 GB/s, slower than the GPU consumes a chunk)
+void stage_copy(uint8_t *dst, const uint8_t *src, size_t bytes) {
+  constexpr size_t kSplit = size_t(8) << 20;
+  const size_t nt = std::min<size_t>(4, bytes / kSplit);
+  if (nt < 2) {
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  std::vector<std::thread> th;
+  const size_t part = (bytes / nt + 63) & ~size_t(63);
+  for (size_t t = 1; t < nt; ++t) {
+    const size_t lo = std::min(bytes, t * part), hi = std::min(bytes, (t + 1) * part);
+    if (hi > lo) th.emplace_back([=] { std::memcpy(dst + lo, src + lo, hi - lo); });
+  }
+  std::memcpy(dst, src, std::min(bytes, part));
+  for (auto &x : th) x.join();
+}
+
 int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t *sig,
                   size_t sig_stride, const uint8_t *msg, size_t msg_stride, size_t n,
                   uint8_t *flags_out) {
   std::lock_guard<std::mutex> lk(c.mu);
-  const bool pipe = n >= 2 * kPipeChunk;
+  static const bool no_pipe = std::getenv("HSV_NO_PIPELINE") != nullptr;  // measurement switch
+  const bool pipe = !no_pipe && n >= 2 * kPipeChunk;
   const size_t chunk = pipe ? kPipeChunk : std::min(n, kChunk);
   const int nbuf = pipe ? 2 : 1;
   const size_t pk_off = 0;
@@ -225,12 +245,12 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
     uint8_t *h = c.h_buf + (size_t)b * total;
     uint8_t *d = c.d_buf + (size_t)b * total;
     // pack into the dense layout the kernel reads (pk 32 | sig 64 | msg 32)
-    if (pk_stride == 32) std::memcpy(h + pk_off, pk + base * 32, m * 32);
+    if (pk_stride == 32) stage_copy(h + pk_off, pk + base * 32, m * 32);
     else for (size_t i = 0; i < m; ++i) std::memcpy(h + pk_off + 32 * i, pk + (base + i) * pk_stride, 32);
-    if (sig_stride == 64) std::memcpy(h + sig_off, sig + base * 64, m * 64);
+    if (sig_stride == 64) stage_copy(h + sig_off, sig + base * 64, m * 64);
     else for (size_t i = 0; i < m; ++i) std::memcpy(h + sig_off + 64 * i, sig + (base + i) * sig_stride, 64);
     if (msg_stride == 0) std::memcpy(h + msg_off, msg, 32);
-    else if (msg_stride == 32) std::memcpy(h + msg_off, msg + base * 32, m * 32);
+    else if (msg_stride == 32) stage_copy(h + msg_off, msg + base * 32, m * 32);
     else for (size_t i = 0; i < m; ++i) std::memcpy(h + msg_off + 32 * i, msg + (base + i) * msg_stride, 32);
     const size_t in_bytes = msg_off + (msg_stride ? m * 32 : 32);
     hipError_t e = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s);
