@@ -652,7 +652,7 @@ int run_tx_on_device(DevCtx &c, const uint8_t *txs, const uint64_t *offsets, siz
     const size_t bytes = tx_bytes(offsets, tx_size, a, ch.second);
     const size_t first = offsets ? (size_t)offsets[a] : a * tx_size;
     uint8_t *h = c.h_buf;
-    std::memcpy(h, txs + first, bytes);
+    stage_copy(h, txs + first, bytes);
     size_t in_bytes = bytes;
     if (offsets) {
       uint64_t *ho = reinterpret_cast<uint64_t *>(h + off_off);
