@@ -102,10 +102,14 @@ def _cpu_model():
     return "unknown"
 
 
-def qc_latency(reps):
+def qc_latency(reps, auto=True):
+    """auto: the drop-in default, hsv_verify_batch_packed with its automatic
+    committee cache in steady state (the same keys every round, as consensus
+    has); auto=False: the generic kernels only."""
     from hsverify import _lib, synth
     lib = _lib.load()
-    res = {}
+    lib.hsv_set_auto_committee(1 if auto else 0)
+    res = {"automatic_committee_cache": bool(auto)}
     for committee in (4, 100, 1000):
         w = synth.qc_votes(committee, seed=committee)
         packed = np.concatenate([w.pk, w.sig], axis=1).tobytes()
@@ -441,7 +445,9 @@ def main():
         threads = max(1, min(16, os.cpu_count() or 1))
         out["cpu_baseline"] = cpu_baseline(w, f, a.cpu_sample, threads)
     if not a.no_qc:
-        out["qc_latency"] = qc_latency(a.qc_reps)
+        out["qc_latency"] = qc_latency(a.qc_reps, auto=True)
+        out["qc_latency_generic"] = qc_latency(a.qc_reps, auto=False)
+        _lib.load().hsv_set_auto_committee(1)
         out["committee_cache"] = committee_bench(a.qc_reps, dev)
         out["mempool_tx"] = mempool_bench(dev)
         if world == 1 and not a.no_cpu_baseline:

@@ -14,6 +14,7 @@
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -301,6 +302,8 @@ int run_host(const uint8_t *pk, size_t pk_stride, const uint8_t *sig, size_t sig
 
 }  // namespace
 
+void release_auto_committee();  // hsv_verify_batch_packed's cache, defined below
+
 extern "C" {
 
 int hsv_init(int device) {
@@ -312,6 +315,7 @@ int hsv_init(int device) {
 }
 
 void hsv_shutdown(void) {
+  release_auto_committee();
   Global &g = G();
   std::lock_guard<std::mutex> lk(g.mu);
   for (DevCtx *c : g.ctx) {
@@ -370,21 +374,24 @@ static int batch_verdict(const std::vector<uint8_t> &flags) {
   return 1;
 }
 
-int hsv_verify_batch(const uint8_t digest[32], const uint8_t *pk, const uint8_t *sig, size_t n) {
-  if (n == 0) return 1;  // dalek verify_batch over zero items is Ok
+// crypto::Signature::verify_batch through the generic kernels
+static int verify_batch_generic(const uint8_t digest[32], const uint8_t *pk, size_t pk_stride, const uint8_t *sig,
+                                size_t sig_stride, size_t n) {
   std::vector<uint8_t> flags(n);
-  int rc = run_host(pk, 32, sig, 64, digest, 0, n, flags.data());
+  int rc = run_host(pk, pk_stride, sig, sig_stride, digest, 0, n, flags.data());
   if (rc != HSV_OK) return rc;
   return batch_verdict(flags);
 }
 
-int hsv_verify_batch_packed(const uint8_t digest[32], const uint8_t *votes, size_t n) {
-  if (n == 0) return 1;
-  if (!votes) return fail(HSV_ERR_INVALID_ARG, "null votes");
-  std::vector<uint8_t> flags(n);
-  int rc = run_host(votes, 96, votes + 32, 96, digest, 0, n, flags.data());
-  if (rc != HSV_OK) return rc;
-  return batch_verdict(flags);
+int hsv_verify_batch(const uint8_t digest[32], const uint8_t *pk, const uint8_t *sig, size_t n) {
+  if (n == 0) return 1;  // dalek verify_batch over zero items is Ok
+  if (!digest || !pk || !sig) return fail(HSV_ERR_INVALID_ARG, "null argument");
+  std::vector<uint8_t> packed(n * 96);
+  for (size_t i = 0; i < n; ++i) {
+    std::memcpy(packed.data() + 96 * i, pk + 32 * i, 32);
+    std::memcpy(packed.data() + 96 * i + 32, sig + 64 * i, 64);
+  }
+  return hsv_verify_batch_packed(digest, packed.data(), n);
 }
 
 int hsv_verify_device_bits(const uint8_t *d_pk, size_t pk_stride, const uint8_t *d_sig,
@@ -575,7 +582,7 @@ int hsv_committee_verify_batch_packed(hsv_committee *cm, const uint8_t digest[32
   std::vector<uint8_t> sigs(m * 64);
   for (size_t i = 0; i < m; ++i) {
     const int64_t k = hsv_committee_index(cm, votes + 96 * i);
-    if (k < 0) return hsv_verify_batch_packed(digest, votes, m);  // a non-member key: generic kernel
+    if (k < 0) return verify_batch_generic(digest, votes, 96, votes + 32, 96, m);  // a non-member key: generic kernel
     idx[i] = (uint32_t)k;
     std::memcpy(sigs.data() + 64 * i, votes + 96 * i + 32, 64);
   }
@@ -583,6 +590,143 @@ int hsv_committee_verify_batch_packed(hsv_committee *cm, const uint8_t digest[32
   int rc = hsv_committee_verify(cm, idx.data(), sigs.data(), digest, 0, m, flags.data());
   if (rc != HSV_OK) return rc;
   return batch_verdict(flags);
+}
+
+}  // extern "C"
+
+// ---- automatic committee cache behind the drop-in verify_batch ------------
+// Consensus keys are fixed per epoch (consensus/src/config.rs:39-43), so the
+// keys of every QC repeat round after round.  verify_batch therefore keeps one
+// committee key cache of its own: once a batch carries keys that were already
+// seen in an earlier batch, it builds comb tables for the union of the cached
+// keys and the batch's keys (one-time cost, ~4 ms per 1000 keys), and from
+// then on batches whose keys are all cached take the committee kernels
+// (four lanes per vote below 2^12 votes).  Flags are identical to the generic
+// path's (tests/test_committee.py), so the verdict is unchanged.
+// HSV_AUTO_COMMITTEE=0 or hsv_set_auto_committee(0) turns it off.
+namespace {
+
+constexpr size_t kAutoMaxKeys = 8192;  // 3 GiB of tables at most
+
+struct AutoCommittee {
+  std::mutex mu;
+  std::shared_ptr<hsv_committee> cm;
+  std::unordered_map<std::string, uint32_t> seen;  // uncached key -> batches it appeared in
+  std::atomic<int> enabled{-1};                   // -1: read HSV_AUTO_COMMITTEE on first use
+};
+
+AutoCommittee &AC() {
+  static AutoCommittee a;
+  return a;
+}
+
+bool auto_enabled() {
+  AutoCommittee &a = AC();
+  int e = a.enabled.load();
+  if (e < 0) {
+    const char *v = std::getenv("HSV_AUTO_COMMITTEE");
+    e = (v && v[0] == '0') ? 0 : 1;
+    a.enabled.store(e);
+  }
+  return e == 1;
+}
+
+void add_batch_keys(const uint8_t *votes, size_t n, std::vector<std::string> &keys,
+                    std::unordered_map<std::string, bool> &have) {
+  for (size_t i = 0; i < n; ++i) {
+    std::string k(reinterpret_cast<const char *>(votes + 96 * i), 32);
+    if (!have.count(k)) {
+      have[k] = true;
+      keys.push_back(k);
+    }
+  }
+}
+
+// The cache to verify this batch with, or nullptr (generic path).  May build
+// or rebuild the cache; rc receives an infrastructure error.
+std::shared_ptr<hsv_committee> auto_committee_for(const uint8_t *votes, size_t n, int &rc) {
+  rc = HSV_OK;
+  AutoCommittee &a = AC();
+  std::lock_guard<std::mutex> lk(a.mu);
+  std::vector<std::string> missing;
+  for (size_t i = 0; i < n; ++i) {
+    const uint8_t *pk = votes + 96 * i;
+    if (!a.cm || hsv_committee_index(a.cm.get(), pk) < 0)
+      missing.emplace_back(reinterpret_cast<const char *>(pk), 32);
+  }
+  if (missing.empty()) return a.cm;
+  bool recurring = false;
+  for (const std::string &k : missing) recurring |= ++a.seen[k] >= 2;
+  if (a.seen.size() > 4 * kAutoMaxKeys) a.seen.clear();
+  if (!recurring) return nullptr;
+  // rebuild over the cached keys and this batch's keys
+  std::vector<std::string> keys;
+  std::unordered_map<std::string, bool> have;
+  if (a.cm) {
+    for (const auto &kv : a.cm->index) {
+      keys.push_back(kv.first);
+      have[kv.first] = true;
+    }
+  }
+  add_batch_keys(votes, n, keys, have);
+  if (keys.size() > kAutoMaxKeys) {  // a new epoch: keep only this batch's keys
+    keys.clear();
+    have.clear();
+    add_batch_keys(votes, n, keys, have);
+  }
+  std::vector<uint8_t> flat(keys.size() * 32);
+  for (size_t i = 0; i < keys.size(); ++i) std::memcpy(flat.data() + 32 * i, keys[i].data(), 32);
+  hsv_committee *c = nullptr;
+  rc = hsv_committee_create(flat.data(), keys.size(), &c);
+  if (rc != HSV_OK) return nullptr;
+  a.cm = std::shared_ptr<hsv_committee>(c, [](hsv_committee *p) { hsv_committee_destroy(p); });
+  a.seen.clear();
+  return a.cm;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hsv_verify_batch_packed(const uint8_t digest[32], const uint8_t *votes, size_t n) {
+  if (n == 0) return 1;
+  if (!digest || !votes) return fail(HSV_ERR_INVALID_ARG, "null argument");
+  if (n >= 2 && auto_enabled()) {
+    int rc = ensure_init();
+    if (rc != HSV_OK) return rc;
+    std::shared_ptr<hsv_committee> cm = auto_committee_for(votes, n, rc);
+    if (rc != HSV_OK) return rc;
+    if (cm) return hsv_committee_verify_batch_packed(cm.get(), digest, votes, n);
+  }
+  return verify_batch_generic(digest, votes, 96, votes + 32, 96, n);
+}
+
+}  // extern "C"
+
+void release_auto_committee() {
+  AutoCommittee &a = AC();
+  std::lock_guard<std::mutex> lk(a.mu);
+  a.cm.reset();
+  a.seen.clear();
+}
+
+extern "C" {
+
+int hsv_set_auto_committee(int enable) {
+  AutoCommittee &a = AC();
+  std::lock_guard<std::mutex> lk(a.mu);
+  a.enabled.store(enable ? 1 : 0);
+  if (!enable) {
+    a.cm.reset();
+    a.seen.clear();
+  }
+  return HSV_OK;
+}
+
+size_t hsv_auto_committee_size(void) {
+  AutoCommittee &a = AC();
+  std::lock_guard<std::mutex> lk(a.mu);
+  return a.cm ? a.cm->n : 0;
 }
 
 }  // extern "C"

@@ -90,6 +90,17 @@ int hsv_verify_batch(const uint8_t digest[32], const uint8_t *pk, const uint8_t 
 /* Same, votes packed as n 96-byte records pk(32)||R(32)||s(32). */
 int hsv_verify_batch_packed(const uint8_t digest[32], const uint8_t *votes, size_t n);
 
+/* Automatic committee cache behind hsv_verify_batch[_packed] (on by default;
+ * env HSV_AUTO_COMMITTEE=0 turns it off).  Consensus keys repeat every round
+ * (consensus/src/config.rs Committee), so once a batch carries keys seen in an
+ * earlier batch, comb tables are built for them (one-time cost, ~4 ms per 1000
+ * keys, at most 8192 keys) and later batches of cached keys take the
+ * committee kernels.  Verdicts are identical either way.  enable = 0 also
+ * drops the cache. */
+int hsv_set_auto_committee(int enable);
+/* Number of keys in the automatic cache (0 when none). */
+size_t hsv_auto_committee_size(void);
+
 /* ---- verification, device-resident buffers (stream-ordered, async) ------ */
 /* Inputs already in HBM of the current device.  Record i reads
  * pk + i*pk_stride (32 B), sig + i*sig_stride (64 B), msg + i*msg_stride

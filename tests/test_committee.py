@@ -106,3 +106,48 @@ def test_committee_quad_and_single_lane_forms_agree(mods, golden):
             got = c.verify_flags(idx[sel], golden["sig"][sel], golden["msg"][sel])
             bad = np.nonzero(got != golden["flags"][sel])[0]
             assert bad.size == 0, (m, [golden["cases"][sel[i]] for i in bad[:8]])
+
+
+def test_auto_committee_behind_verify_batch(mods):
+    """hsv_verify_batch[_packed] caches recurring keys (consensus keys repeat
+    every round): first sight goes through the generic kernels, the second
+    batch with the same keys builds the cache, later ones use it; verdicts are
+    the same either way, a non-member key falls back to the generic path, and
+    switching the cache off drops it."""
+    _, crypto, synth, _ = mods
+    from hsverify import _lib
+    lib = _lib.load()
+    lib.hsv_set_auto_committee(0)
+    lib.hsv_set_auto_committee(1)
+    try:
+        w = synth.qc_votes(100, seed=41)
+        packed = np.concatenate([w.pk, w.sig], 1).tobytes()
+        d = bytes(w.msg)
+        assert lib.hsv_verify_batch_packed(d, packed, w.n) == 1
+        assert lib.hsv_auto_committee_size() == 0          # seen once: no cache yet
+        assert lib.hsv_verify_batch_packed(d, packed, w.n) == 1
+        assert lib.hsv_auto_committee_size() == w.n        # recurring keys: cache built
+        for pos in (40, 70):                               # corrupted s / R through the cache
+            bad = bytearray(packed)
+            bad[96 * 5 + pos] ^= 1
+            assert lib.hsv_verify_batch_packed(d, bytes(bad), w.n) == 0
+        c3 = synth.qc_votes(100, seed=41, corrupt_frac=0.05)   # every corruption kind, same keys mostly
+        p3 = np.concatenate([c3.pk, c3.sig], 1).tobytes()
+        lib.hsv_set_auto_committee(0)
+        generic = lib.hsv_verify_batch_packed(bytes(c3.msg) if c3.msg.ndim == 1 else bytes(c3.msg[0]), p3, c3.n)
+        lib.hsv_set_auto_committee(1)
+        for _ in range(3):
+            got = lib.hsv_verify_batch_packed(bytes(c3.msg) if c3.msg.ndim == 1 else bytes(c3.msg[0]), p3, c3.n)
+            assert got == generic == 0
+        # the reference's crypto test shapes through the Python mirror, twice (second time cached)
+        keys = [crypto.generate_keypair(lambda n, s=s: s) for s in o.reference_key_seeds()]
+        digest = crypto.Digest(o.test_digest(b"Hello, world!"))
+        votes = [(pk, crypto.Signature.new(digest, sk)) for pk, sk in keys[:3]]
+        for _ in range(3):
+            assert crypto.Signature.verify_batch(digest, votes).is_ok()
+            assert crypto.Signature.verify_batch(digest, votes[:2] + [(keys[2][0], crypto.Signature.default())]).is_err()
+        assert lib.hsv_auto_committee_size() >= 3
+    finally:
+        lib.hsv_set_auto_committee(0)
+        assert lib.hsv_auto_committee_size() == 0
+        lib.hsv_set_auto_committee(1)
