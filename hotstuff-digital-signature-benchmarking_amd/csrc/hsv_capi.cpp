@@ -303,6 +303,11 @@ int run_host(const uint8_t *pk, size_t pk_stride, const uint8_t *sig, size_t sig
 }  // namespace
 
 void release_auto_committee();  // hsv_verify_batch_packed's cache, defined below
+// Strict verification of small batches whose keys are all in that cache, via
+// the committee kernels: HSV_OK when done, 1 when the caller should take the
+// generic path, < 0 on an error.
+int auto_committee_try(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, size_t msg_stride, size_t n,
+                       uint8_t *flags_out);
 
 extern "C" {
 
@@ -358,12 +363,16 @@ int hsv_get_variant(void) { return G().variant.load(); }
 int hsv_verify(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, size_t msg_stride,
                size_t n, uint8_t *flags_out) {
   if (msg_stride != 0 && msg_stride != 32) return fail(HSV_ERR_INVALID_ARG, "msg_stride must be 0 or 32");
+  if (n && pk && sig && msg && flags_out) {
+    const int rc = auto_committee_try(pk, sig, msg, msg_stride, n, flags_out);
+    if (rc != 1) return rc;  // handled (HSV_OK) or an error
+  }
   return run_host(pk, 32, sig, 64, msg, msg_stride, n, flags_out);
 }
 
 int hsv_verify_strict(const uint8_t digest[32], const uint8_t pk[32], const uint8_t sig[64]) {
   uint8_t f = 0;
-  int rc = run_host(pk, 32, sig, 64, digest, 0, 1, &f);
+  int rc = hsv_verify(pk, sig, digest, 0, 1, &f);
   if (rc != HSV_OK) return rc;
   return (f & HSV_STRICT_OK) ? 1 : 0;
 }
@@ -606,7 +615,8 @@ int hsv_committee_verify_batch_packed(hsv_committee *cm, const uint8_t digest[32
 // HSV_AUTO_COMMITTEE=0 or hsv_set_auto_committee(0) turns it off.
 namespace {
 
-constexpr size_t kAutoMaxKeys = 8192;  // 3 GiB of tables at most
+constexpr size_t kAutoMaxKeys = 8192;      // 3 GiB of tables at most
+constexpr size_t kCommitteeTryMax = 4096;  // hsv_verify / verify_strict batches that try the cache
 
 struct AutoCommittee {
   std::mutex mu;
@@ -702,6 +712,27 @@ int hsv_verify_batch_packed(const uint8_t digest[32], const uint8_t *votes, size
 }
 
 }  // extern "C"
+
+int auto_committee_try(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, size_t msg_stride, size_t n,
+                       uint8_t *flags_out) {
+  // only the latency range (a vote, a TC); large batches of fresh keys would
+  // pay a hash lookup per item for nothing
+  if (n > kCommitteeTryMax || !auto_enabled()) return 1;
+  std::shared_ptr<hsv_committee> cm;
+  {
+    AutoCommittee &a = AC();
+    std::lock_guard<std::mutex> lk(a.mu);
+    cm = a.cm;
+  }
+  if (!cm) return 1;
+  std::vector<uint32_t> idx(n);
+  for (size_t i = 0; i < n; ++i) {
+    const int64_t k = hsv_committee_index(cm.get(), pk + 32 * i);
+    if (k < 0) return 1;
+    idx[i] = (uint32_t)k;
+  }
+  return hsv_committee_verify(cm.get(), idx.data(), sig, msg, msg_stride, n, flags_out);
+}
 
 void release_auto_committee() {
   AutoCommittee &a = AC();

@@ -147,6 +147,24 @@ def test_auto_committee_behind_verify_batch(mods):
             assert crypto.Signature.verify_batch(digest, votes).is_ok()
             assert crypto.Signature.verify_batch(digest, votes[:2] + [(keys[2][0], crypto.Signature.default())]).is_err()
         assert lib.hsv_auto_committee_size() >= 3
+        # strict verification of cached keys (Vote::verify, TC-style per-vote digests) takes the
+        # committee kernels: flags equal the generic path's on every corruption kind
+        from hsverify import verifier
+        t = synth.tc_votes(100, seed=41, corrupt_frac=0.3)
+        member = np.array([lib.hsv_committee_index is not None] * t.n)
+        cached = verifier.verify_flags(t.pk, t.sig, t.msg)
+        lib.hsv_set_auto_committee(0)
+        generic = verifier.verify_flags(t.pk, t.sig, t.msg)
+        lib.hsv_set_auto_committee(1)
+        assert member.all() and (cached == generic).all()
+        for _ in range(2):   # repopulate the cache with the QC keys, then single strict verifies
+            assert lib.hsv_verify_batch_packed(d, packed, w.n) == 1
+        assert lib.hsv_auto_committee_size() == w.n
+        assert lib.hsv_verify_strict(d, bytes(w.pk[3]), bytes(w.sig[3])) == 1
+        s_bad = bytearray(w.sig[3]); s_bad[10] ^= 4
+        assert lib.hsv_verify_strict(d, bytes(w.pk[3]), bytes(s_bad)) == 0
+        both = verifier.verify_flags(w.pk, w.sig, np.repeat(w.msg[None], w.n, 0))
+        assert (both & o.STRICT_OK).all()
     finally:
         lib.hsv_set_auto_committee(0)
         assert lib.hsv_auto_committee_size() == 0
