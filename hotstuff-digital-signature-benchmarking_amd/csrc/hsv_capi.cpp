@@ -40,6 +40,7 @@ int hip_fail(const char *where, hipError_t e) {
 constexpr size_t kAlign = 256;
 constexpr size_t kChunk = size_t(1) << 22;     // items per launch (512 MiB of inputs max)
 constexpr size_t kShardMin = size_t(1) << 16;  // shard host batches across GPUs above this
+constexpr size_t kZeroCopyMax = size_t(1) << 12;  // committee batches read straight from pinned memory
 
 size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -569,6 +570,21 @@ int hsv_committee_verify(hsv_committee *cm, const uint32_t *key_idx, const uint8
     std::memcpy(h + idx_off, key_idx + base, k * 4);
     std::memcpy(h + sig_off, sig + base * 64, k * 64);
     std::memcpy(h + msg_off, msg + base * msg_stride, msg_bytes);
+    // small batches (a QC, a vote): the kernel reads the pinned staging buffer
+    // and writes the flags back through its device mapping (zero-copy), which
+    // saves the two copy launches on the latency path
+    void *hd = nullptr;
+    if (k <= kZeroCopyMax && hipHostGetDevicePointer(&hd, h, 0) == hipSuccess && hd) {
+      uint8_t *dh = static_cast<uint8_t *>(hd);
+      hipError_t e = hsv_launch_comb_verify(reinterpret_cast<const uint32_t *>(dh + idx_off), dh + sig_off, 64,
+                                            dh + msg_off, msg_stride ? 32 : 0, (uint32_t)k, cm->d_pks, cm->d_kflags,
+                                            cm->n, cm->d_tables, c.d_btable, dh + flag_off, c.stream);
+      if (e != hipSuccess) return hip_fail("committee verify launch", e);
+      e = hipStreamSynchronize(c.stream);
+      if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
+      std::memcpy(flags_out + base, h + flag_off, k);
+      continue;
+    }
     hipError_t e = hipMemcpyAsync(c.d_buf, h, msg_off + msg_bytes, hipMemcpyHostToDevice, c.stream);
     if (e != hipSuccess) return hip_fail("hipMemcpyAsync H2D", e);
     e = hsv_launch_comb_verify(reinterpret_cast<const uint32_t *>(c.d_buf + idx_off), c.d_buf + sig_off, 64,
