@@ -512,6 +512,81 @@ hsv_verify_pair_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const
   }
 }
 
+// Point pass with a pair-lane tail (variant 22): as hsv_verify_hp_kernel, but
+// the last n_tail items (a multiple-of-64 boundary, about one round of the
+// persistent grid) are dealt out as 32-item batches run two lanes per item
+// (verify_pair_prepped).  A pair batch finishes in ~72 % of a 64-item batch's
+// time, so the final partial round of the grid is shorter.  Virtual range:
+// [fallback items | n - n_tail items in 64-batches | n_tail items, 64 units per 32].
+template <int WA, int WAVES, int CB>
+__global__ void __launch_bounds__(kBlock, WAVES)
+hsv_verify_hpt_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const uint8_t *__restrict__ sig,
+                      uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
+                      uint32_t n_tail, uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
+                      uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b,
+                      const uint32_t *__restrict__ rec, HcCounters *__restrict__ ctr,
+                      const uint32_t *__restrict__ fb_list) {
+  constexpr int kEnt = (1 << (WA - 1)) + 1;
+  GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)(blockIdx.x * kBlock + threadIdx.x) * vt_lane_uint4<WA>()};
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t nfb = __builtin_amdgcn_readfirstlane(ctr->fb_count);
+  const uint32_t fb_end = (nfb + 63u) & ~63u;
+  const uint32_t n_reg = n - n_tail;  // multiple of 64 (launch_hpt)
+  const uint32_t tail_start = fb_end + n_reg;
+  const uint32_t v_end = tail_start + 2u * n_tail;
+  const uint32_t words = (n + 31u) / 32u;
+  for (;;) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&ctr->next, 64u);
+    base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
+    if (base >= v_end) break;
+    if (base < fb_end) {
+      const uint32_t j = base + lane;
+      const bool valid = j < nfb;
+      const uint32_t idx = fb_list[valid ? j : base];
+      uint32_t pkw[8], sigw[16], msgw[8];
+      load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, idx, pkw, sigw, msgw);
+      const uint32_t f = verify_one_full_comb<WA, false, CB>(pkw, sigw, msgw, comb_b, vt);
+      if (valid) {
+        if (flags_out) flags_out[idx] = (uint8_t)f;
+        if (strict_bits && (f & kStrictOk)) atomicOr(&strict_bits[idx >> 5], 1u << (idx & 31u));
+      }
+      continue;
+    }
+    const bool tail = base >= tail_start;
+    const uint32_t p = tail ? (lane & 1u) : 0u;
+    const uint32_t idx = tail ? n_reg + (base - tail_start) / 2u + lane / 2u : base - fb_end + lane;
+    const bool valid = idx < n;
+    const uint32_t li = valid ? idx : n - 1u;
+    uint32_t pkw[8], rw[8];
+    {
+      const uint4 *pp = reinterpret_cast<const uint4 *>(pk + (uint64_t)li * pk_stride);
+      const uint4 *rp = reinterpret_cast<const uint4 *>(sig + (uint64_t)li * sig_stride);
+      const uint4 p0 = pp[0], p1 = pp[1], r0 = rp[0], r1 = rp[1];
+      pkw[0] = p0.x; pkw[1] = p0.y; pkw[2] = p0.z; pkw[3] = p0.w;
+      pkw[4] = p1.x; pkw[5] = p1.y; pkw[6] = p1.z; pkw[7] = p1.w;
+      rw[0] = r0.x; rw[1] = r0.y; rw[2] = r0.z; rw[3] = r0.w;
+      rw[4] = r1.x; rw[5] = r1.y; rw[6] = r1.z; rw[7] = r1.w;
+    }
+    const uint32_t meta = rec[18ull * n + li];
+    const bool own = valid && !(meta & kPrepFallback) && p == 0u;
+    uint32_t f;
+    if (tail) f = verify_pair_prepped<WA, CB>(p, pkw, rw, rec + li, n, meta, comb_b, vt);
+    else f = verify_one_prepped<WA, CB>(pkw, rw, rec + li, n, meta, comb_b, vt);
+    if (own && flags_out) flags_out[idx] = (uint8_t)f;
+    if (strict_bits) {
+      if (tail) {
+        if (own && (f & kStrictOk)) atomicOr(&strict_bits[idx >> 5], 1u << (idx & 31u));
+      } else {
+        const uint64_t mask = __ballot(own && (f & kStrictOk));
+        const uint32_t w = (base - fb_end) / 32u + lane;
+        const uint32_t part = lane ? (uint32_t)(mask >> 32) : (uint32_t)mask;
+        if (lane < 2u && w < words && part) atomicOr(&strict_bits[w], part);
+      }
+    }
+  }
+}
+
 // ---- v_mad_u64_u32 issue-rate probe -------------------------------------
 // 8 independent accumulation chains, 16 mads per asm statement (the compiler
 // puts an s_nop after every asm statement that writes an SGPR, so one mad per
@@ -562,7 +637,8 @@ __global__ void __launch_bounds__(256) hsv_mad_peak_kernel(uint32_t *sink, uint3
 //  20: as 19, 2 waves/SIMD
 //  21: as 19 for batches above 2^13 items; at or below, the latency form:
 //      prepass, then two lanes per item (hsv_verify_pair_kernel)
-extern "C" int hsv_num_variants(void) { return 22; }
+//  22: as 21 with a pair-lane tail in the large-batch point pass (hsv_verify_hpt_kernel)
+extern "C" int hsv_num_variants(void) { return 23; }
 
 namespace {
 
@@ -636,11 +712,13 @@ hipError_t launch_mt(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
 // Two-pass launch (variants 19/20): prepass over all items, then the
 // persistent point pass.  Workspace: per-lane tables | counters (256 B) |
 // fallback list (4 B per item) | prep records (kPrepWords x 4 B per item).
-template <int WA, int WAVES, int CB>
+template <int WA, int WAVES, int CB, bool TAIL = false>
 hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
                      const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
                      uint32_t *strict_bits, const uint32_t *comb_b, hipStream_t stream) {
-  const void *kern = reinterpret_cast<const void *>(hsv::hsv_verify_hp_kernel<WA, WAVES, CB>);
+  const void *kern;
+  if constexpr (TAIL) kern = reinterpret_cast<const void *>(hsv::hsv_verify_hpt_kernel<WA, WAVES, CB>);
+  else kern = reinterpret_cast<const void *>(hsv::hsv_verify_hp_kernel<WA, WAVES, CB>);
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
@@ -686,9 +764,18 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
     e = hipGetLastError();
   }
   if (e == hipSuccess) {
-    hipLaunchKernelGGL((hsv::hsv_verify_hp_kernel<WA, WAVES, CB>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
-                       pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, vt_ws, comb_b, rec,
-                       ctr, fb_list);
+    if constexpr (TAIL) {
+      // about one round of the grid as pair batches; the regular range stays a multiple of 64
+      const uint32_t target = grid * (hsv::kBlock / 64u) * 32u;
+      const uint32_t n_tail = n > 2u * target ? n - ((n - target) & ~63u) : 0u;
+      hipLaunchKernelGGL((hsv::hsv_verify_hpt_kernel<WA, WAVES, CB>), dim3(grid), dim3(hsv::kBlock), 0, stream,
+                         pk, pk_stride, sig, sig_stride, msg, msg_stride, n, n_tail, flags_out, strict_bits, vt_ws,
+                         comb_b, rec, ctr, fb_list);
+    } else {
+      hipLaunchKernelGGL((hsv::hsv_verify_hp_kernel<WA, WAVES, CB>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
+                         pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, vt_ws, comb_b, rec,
+                         ctr, fb_list);
+    }
     e = hipGetLastError();
   }
   const hipError_t ef = hipFreeAsync(ws, stream);
@@ -785,6 +872,10 @@ extern "C" hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t
       if (n <= kPairMax)
         return launch_pair<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
       return launch_hp<4, 3, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
+    case 22: if (!comb_b) return hipErrorInvalidValue;
+      if (n <= kPairMax)
+        return launch_pair<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
+      return launch_hp<4, 3, 16, true>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
 #undef HSV_LAUNCH_MT
     default: return hipErrorInvalidValue;
   }
@@ -818,6 +909,6 @@ extern "C" double hsv_launch_mad_peak(int device_cus) {
 
 extern "C" int hsv_variant_needs_comb(int variant) {
   if (variant >= 10 && variant <= 14) return 8;
-  if (variant >= 15 && variant <= 21) return 16;
+  if (variant >= 15 && variant <= 22) return 16;
   return 0;
 }
