@@ -209,6 +209,7 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
                   uint8_t *flags_out) {
   std::lock_guard<std::mutex> lk(c.mu);
   static const bool no_pipe = std::getenv("HSV_NO_PIPELINE") != nullptr;  // measurement switch
+  static const bool no_zero_copy = std::getenv("HSV_NO_ZERO_COPY") != nullptr;  // measurement switch
   const bool pipe = !no_pipe && n >= 2 * kPipeChunk;
   const size_t chunk = pipe ? kPipeChunk : std::min(n, kChunk);
   const int nbuf = pipe ? 2 : 1;
@@ -255,6 +256,20 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
     else if (msg_stride == 32) stage_copy(h + msg_off, msg + base * 32, m * 32);
     else for (size_t i = 0; i < m; ++i) std::memcpy(h + msg_off + 32 * i, msg + (base + i) * msg_stride, 32);
     const size_t in_bytes = msg_off + (msg_stride ? m * 32 : 32);
+    // small batches (a QC of non-cached keys, a single vote): as on the
+    // committee path, the kernels read the pinned staging buffer and write the
+    // flags through its device mapping, so no copy launches sit on the
+    // latency path
+    void *hd = nullptr;
+    if (!no_zero_copy && n <= kZeroCopyMax && hipHostGetDevicePointer(&hd, h, 0) == hipSuccess && hd) {
+      uint8_t *dh = static_cast<uint8_t *>(hd);
+      hipError_t e = hsv_launch_verify(variant, dh + pk_off, 32, dh + sig_off, 64, dh + msg_off,
+                                       msg_stride ? 32 : 0, (uint32_t)m, dh + flag_off, nullptr, comb_b, s);
+      if (e != hipSuccess) return hip_fail("verify kernel launch", e);
+      pend_base[b] = base;
+      pend_m[b] = m;
+      continue;
+    }
     hipError_t e = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return hip_fail("hipMemcpyAsync H2D", e);
     e = hsv_launch_verify(variant, d + pk_off, 32, d + sig_off, 64, d + msg_off, msg_stride ? 32 : 0,
