@@ -173,6 +173,17 @@ def test_random_batch_vs_c_oracle(api, oracle_lib):
 
 
 # ---- ragged sizes, shared digests, layouts ------------------------------------
+@pytest.mark.parametrize("n", [1, 4095, 4096, 4097])
+def test_zero_copy_boundary_vs_c_oracle(api, oracle_lib, n):
+    """Host batches of <= 2^12 fresh keys are read from pinned memory by the
+    kernels (zero-copy); 4097 takes the copy path.  Both must match the oracle."""
+    _, verifier, synth = api
+    w = synth.independent_triples(n, seed=1000 + n, corrupt_frac=0.2)
+    got = verifier.verify_flags(w.pk, w.sig, w.msg)
+    exp = oracle_flags(oracle_lib, w.pk, w.sig, w.msg)
+    assert (got == exp).all()
+
+
 @pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 256, 257, 1000])
 def test_ragged_sizes(api, golden, n):
     _, verifier, _ = api
