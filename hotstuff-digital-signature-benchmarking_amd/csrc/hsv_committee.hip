@@ -4,7 +4,9 @@
 //                          8j doublings (j is wave-uniform: keys are padded to
 //                          a multiple of 64 per position), 127 additions, one
 //                          batched inversion -> 128 affine Niels entries.
-//  hsv_comb_verify_kernel  one verification per lane against a cached key:
+//  hsv_comb_verify_kernel  one verification per lane against a cached key
+//                          (key i's table at key_tables[i], so a cache can
+//                          grow by appending table blocks without moving them):
 //                          64 mixed additions from the key's table and the B
 //                          table, then R decompression and the projective
 //                          comparison.  Same flag byte as hsv_verify_kernel.
@@ -41,7 +43,7 @@ __global__ void __launch_bounds__(256, 2)
 hsv_comb_verify_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__restrict__ sig,
                        uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride,
                        uint32_t m, const uint8_t *__restrict__ pks, const uint8_t *__restrict__ key_flags,
-                       uint32_t nkeys, const uint32_t *__restrict__ tables,
+                       uint32_t nkeys, const uint32_t *const *__restrict__ key_tables,
                        const uint32_t *__restrict__ btable, uint8_t *__restrict__ flags_out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
@@ -65,8 +67,7 @@ hsv_comb_verify_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__re
     msgw[0] = m0.x; msgw[1] = m0.y; msgw[2] = m0.z; msgw[3] = m0.w;
     msgw[4] = m1.x; msgw[5] = m1.y; msgw[6] = m1.z; msgw[7] = m1.w;
   }
-  const uint32_t f = verify_one_comb(pkw, key_flags[kk], sigw, msgw,
-                                     tables + (uint64_t)kk * kCombTableWords, btable);
+  const uint32_t f = verify_one_comb(pkw, key_flags[kk], sigw, msgw, key_tables[kk], btable);
   flags_out[i] = kvalid ? (uint8_t)f : (uint8_t)0;
 }
 
@@ -96,7 +97,7 @@ __global__ void __launch_bounds__(256)
 hsv_comb_verify_quad_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__restrict__ sig,
                             uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride,
                             uint32_t m, const uint8_t *__restrict__ pks, const uint8_t *__restrict__ key_flags,
-                            uint32_t nkeys, const uint32_t *__restrict__ tables,
+                            uint32_t nkeys, const uint32_t *const *__restrict__ key_tables,
                             const uint32_t *__restrict__ btable, uint8_t *__restrict__ flags_out) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t i0 = t / kCombQuad, g = t % kCombQuad;
@@ -137,7 +138,7 @@ hsv_comb_verify_quad_kernel(const uint32_t *__restrict__ key_idx, const uint8_t 
     kd = me ? ((uint64_t)kr[2 * q4 + 1] << 32) | kr[2 * q4] : kd;
     sd = me ? ((uint64_t)sr[2 * q4 + 1] << 32) | sr[2 * q4] : sd;
   }
-  const uint32_t *ta = tables + (uint64_t)kk * kCombTableWords;
+  const uint32_t *ta = key_tables[kk];
   ge_ext q = ge_identity();
   HSV_NOUNROLL
   for (int jj = 0; jj < kCombPosPerLane; ++jj) {
@@ -213,18 +214,18 @@ static constexpr uint32_t kCombQuadMax = 1u << 12;
 extern "C" hipError_t hsv_launch_comb_verify(const uint32_t *key_idx, const uint8_t *sig, uint64_t sig_stride,
                                              const uint8_t *msg, uint64_t msg_stride, uint32_t m,
                                              const uint8_t *pks, const uint8_t *key_flags, uint32_t nkeys,
-                                             const uint32_t *tables, const uint32_t *btable,
+                                             const uint32_t *const *key_tables, const uint32_t *btable,
                                              uint8_t *flags_out, hipStream_t stream) {
   if (m == 0) return hipSuccess;
   if (m <= kCombQuadMax) {  // latency form: four lanes per vote
     const uint64_t lanes = (uint64_t)m * hsv::kCombQuad;
     hipLaunchKernelGGL(hsv::hsv_comb_verify_quad_kernel, dim3((uint32_t)((lanes + 255u) / 256u)), dim3(256), 0,
-                       stream, key_idx, sig, sig_stride, msg, msg_stride, m, pks, key_flags, nkeys, tables, btable,
+                       stream, key_idx, sig, sig_stride, msg, msg_stride, m, pks, key_flags, nkeys, key_tables, btable,
                        flags_out);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(hsv::hsv_comb_verify_kernel, dim3((m + 255u) / 256u), dim3(256), 0, stream, key_idx, sig,
-                     sig_stride, msg, msg_stride, m, pks, key_flags, nkeys, tables, btable, flags_out);
+                     sig_stride, msg, msg_stride, m, pks, key_flags, nkeys, key_tables, btable, flags_out);
   return hipGetLastError();
 }
 

@@ -1,0 +1,594 @@
+// Committee key cache behind the C ABI:
+//   * hsv_committee_*: an explicit committee (tables for a given key list);
+//   * the automatic cache behind hsv_verify_batch[_packed] / small strict
+//     batches, which learns the recurring consensus keys by itself.
+//
+// Both hand the committee kernels (hsv_committee.hip) a device array of
+// per-key table pointers, so the automatic cache grows by appending 64-key
+// table blocks: existing tables never move, a build for new keys never copies
+// the old ones, and peak table memory is one copy of the cache.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "hsv.h"
+#include "hsv_host.h"
+#include "hsv_internal.h"
+
+namespace hsvh {
+namespace {
+
+// ---- key index -----------------------------------------------------------------
+using Key32 = std::array<uint8_t, 32>;
+
+Key32 key_of(const uint8_t *p) {
+  Key32 k;
+  std::memcpy(k.data(), p, 32);
+  return k;
+}
+
+// Keys are attacker-chosen bytes (they arrive in certificates from the
+// network), so the hash is keyed with a per-process random seed.
+struct KeyHash {
+  static uint64_t seed() {
+    static const uint64_t s = [] {
+      std::random_device rd;
+      return ((uint64_t)rd() << 32) ^ rd() ^ 0x9e3779b97f4a7c15ull;
+    }();
+    return s;
+  }
+  size_t operator()(const Key32 &k) const {
+    uint64_t h = seed();
+    for (int i = 0; i < 4; ++i) {
+      uint64_t w;
+      std::memcpy(&w, k.data() + 8 * i, 8);
+      h = (h ^ w) * 0xbf58476d1ce4e5b9ull;
+      h ^= h >> 31;
+    }
+    return (size_t)h;
+  }
+};
+
+using KeyIndex = std::unordered_map<Key32, uint32_t, KeyHash>;
+
+// ---- committee tables on one device ----------------------------------------------
+struct CommitteeDev {
+  int device = 0;
+  uint32_t n = 0;
+  const uint8_t *d_pks = nullptr;
+  const uint8_t *d_kflags = nullptr;
+  const uint32_t *const *d_tabptr = nullptr;
+};
+
+// Votes by member index on the committee's device, through a slot of that
+// device: the kernels read the pinned staging buffer directly for batches of
+// at most kZeroCopyMax votes (the latency path), otherwise via copies.
+int committee_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t *sig, const uint8_t *msg,
+                  size_t msg_stride, size_t m, uint8_t *flags_out) {
+  int rc = ensure_init();
+  if (rc != HSV_OK) return rc;
+  DevCtx &c = ctx(cd.device);
+  DeviceGuard guard(c.device);
+  if (guard.status() != hipSuccess) return hip_fail("hipSetDevice", guard.status());
+  rc = ensure_btable(c);  // also after an hsv_shutdown
+  if (rc != HSV_OK) return rc;
+  SlotLease lease(c);
+  Slot &s = lease.slot();
+  for (size_t base = 0; base < m; base += kChunk) {
+    const size_t k = std::min(kChunk, m - base);
+    const size_t idx_off = 0;
+    const size_t sig_off = round_up(k * 4, kAlign);
+    const size_t msg_off = sig_off + round_up(k * 64, kAlign);
+    const size_t msg_bytes = msg_stride ? k * 32 : 32;
+    const size_t flag_off = msg_off + round_up(msg_bytes, kAlign);
+    const size_t total = flag_off + round_up(k, kAlign);
+    rc = slot_prepare(s, total, total);
+    if (rc != HSV_OK) return rc;
+    uint8_t *h = s.h_buf;
+    std::memcpy(h + idx_off, key_idx + base, k * 4);
+    std::memcpy(h + sig_off, sig + base * 64, k * 64);
+    std::memcpy(h + msg_off, msg + base * msg_stride, msg_bytes);
+    void *hd = nullptr;
+    uint8_t *dbuf = s.d_buf;
+    const bool zero_copy = k <= kZeroCopyMax && hipHostGetDevicePointer(&hd, h, 0) == hipSuccess && hd;
+    if (zero_copy) {
+      dbuf = static_cast<uint8_t *>(hd);
+    } else {
+      const hipError_t e = hipMemcpyAsync(s.d_buf, h, msg_off + msg_bytes, hipMemcpyHostToDevice, s.stream);
+      if (e != hipSuccess) return hip_fail("hipMemcpyAsync H2D", e);
+    }
+    hipError_t e = hsv_launch_comb_verify(reinterpret_cast<const uint32_t *>(dbuf + idx_off), dbuf + sig_off, 64,
+                                          dbuf + msg_off, msg_stride ? 32 : 0, (uint32_t)k, cd.d_pks, cd.d_kflags, cd.n,
+                                          cd.d_tabptr, c.d_btable, dbuf + flag_off, s.stream);
+    if (e != hipSuccess) return hip_fail("committee verify launch", e);
+    if (!zero_copy) {
+      e = hipMemcpyAsync(h + flag_off, s.d_buf + flag_off, k, hipMemcpyDeviceToHost, s.stream);
+      if (e != hipSuccess) return hip_fail("hipMemcpyAsync D2H", e);
+    }
+    e = hipStreamSynchronize(s.stream);
+    if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
+    std::memcpy(flags_out + base, h + flag_off, k);
+  }
+  return HSV_OK;
+}
+
+// Builds comb tables for `nkeys` encodings already in HBM at d_encs into
+// tables[i] (device pointers, host array), flags into d_kflags, on stream st.
+// Keys are built in runs of contiguous table memory.
+hipError_t build_tables(const uint8_t *d_encs, uint32_t nkeys, uint32_t *const *tables, uint8_t *d_kflags,
+                        uint32_t *d_tmp, uint32_t tmp_keys, hipStream_t st) {
+  const uint64_t words = hsv_comb_table_bytes() / 4;
+  uint32_t i = 0;
+  while (i < nkeys) {
+    uint32_t j = i + 1;
+    while (j < nkeys && j - i < tmp_keys && tables[j] == tables[j - 1] + words) ++j;
+    const hipError_t e = hsv_launch_comb_build(d_encs + (size_t)i * 32, j - i, 1, tables[i], d_tmp, d_kflags + i, st);
+    if (e != hipSuccess) return e;
+    i = j;
+  }
+  return hipSuccess;
+}
+
+}  // namespace
+}  // namespace hsvh
+
+using namespace hsvh;
+
+// ---- explicit committee ------------------------------------------------------------
+struct hsv_committee {
+  CommitteeDev dev;
+  uint8_t *d_pks = nullptr;
+  uint8_t *d_kflags = nullptr;
+  uint32_t *d_tables = nullptr;
+  uint32_t **d_tabptr = nullptr;
+  KeyIndex index;
+};
+
+extern "C" {
+
+int hsv_committee_create(const uint8_t *pks, size_t n, hsv_committee **out) {
+  if (!out || (!pks && n)) return fail(HSV_ERR_INVALID_ARG, "null argument");
+  if (n > (1u << 20)) return fail(HSV_ERR_INVALID_ARG, "committee too large");
+  int rc = ensure_init();
+  if (rc != HSV_OK) return rc;
+  const int dev = home_device();
+  DeviceGuard guard(dev);
+  if (guard.status() != hipSuccess) return hip_fail("hipSetDevice", guard.status());
+  rc = ensure_btable(ctx(dev));
+  if (rc != HSV_OK) return rc;
+  std::unique_ptr<hsv_committee> cm(new hsv_committee());
+  cm->dev.device = dev;
+  cm->dev.n = (uint32_t)n;
+  for (size_t i = 0; i < n; ++i) cm->index.emplace(key_of(pks + 32 * i), (uint32_t)i);
+  if (n) {
+    const uint64_t words = hsv_comb_table_bytes() / 4;
+    uint32_t *d_tmp = nullptr;
+    hipStream_t st = nullptr;
+    std::vector<uint32_t *> ptrs(n);
+    hipError_t e = hipMalloc(&cm->d_pks, n * 32);
+    if (e == hipSuccess) e = hipMalloc(&cm->d_kflags, n);
+    if (e == hipSuccess) e = hipMalloc(&cm->d_tables, n * hsv_comb_table_bytes());
+    if (e == hipSuccess) e = hipMalloc(&cm->d_tabptr, n * sizeof(uint32_t *));
+    if (e == hipSuccess) e = hipMalloc(&d_tmp, hsv_comb_tmp_bytes(std::min<uint32_t>((uint32_t)n, 1024)));
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    for (size_t i = 0; e == hipSuccess && i < n; ++i) ptrs[i] = cm->d_tables + i * words;
+    if (e == hipSuccess) e = hipMemcpyAsync(cm->d_pks, pks, n * 32, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(cm->d_tabptr, ptrs.data(), n * sizeof(uint32_t *), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess)
+      e = build_tables(cm->d_pks, (uint32_t)n, ptrs.data(), cm->d_kflags, d_tmp, std::min<uint32_t>((uint32_t)n, 1024), st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (st) (void)hipStreamDestroy(st);
+    if (d_tmp) (void)hipFree(d_tmp);
+    if (e != hipSuccess) {
+      hsv_committee_destroy(cm.release());
+      return hip_fail("building committee tables", e);
+    }
+    cm->dev.d_pks = cm->d_pks;
+    cm->dev.d_kflags = cm->d_kflags;
+    cm->dev.d_tabptr = cm->d_tabptr;
+  }
+  *out = cm.release();
+  return HSV_OK;
+}
+
+void hsv_committee_destroy(hsv_committee *cm) {
+  if (!cm) return;
+  DeviceGuard guard(cm->dev.device);
+  if (cm->d_pks) (void)hipFree(cm->d_pks);
+  if (cm->d_kflags) (void)hipFree(cm->d_kflags);
+  if (cm->d_tables) (void)hipFree(cm->d_tables);
+  if (cm->d_tabptr) (void)hipFree(cm->d_tabptr);
+  delete cm;
+}
+
+size_t hsv_committee_size(const hsv_committee *cm) { return cm ? cm->dev.n : 0; }
+
+int64_t hsv_committee_index(const hsv_committee *cm, const uint8_t pk[32]) {
+  if (!cm || !pk) return -1;
+  auto it = cm->index.find(key_of(pk));
+  return it == cm->index.end() ? -1 : (int64_t)it->second;
+}
+
+int hsv_committee_verify_device(const hsv_committee *cm, const uint32_t *d_key_idx, const uint8_t *d_sig,
+                                size_t sig_stride, const uint8_t *d_msg, size_t msg_stride, size_t m, uint8_t *d_flags,
+                                void *stream) {
+  if (m == 0) return HSV_OK;
+  if (!cm || !d_key_idx || !d_sig || !d_msg || !d_flags) return fail(HSV_ERR_INVALID_ARG, "null argument");
+  if (((reinterpret_cast<uintptr_t>(d_sig) | reinterpret_cast<uintptr_t>(d_msg) | sig_stride | msg_stride) & 15u) != 0)
+    return fail(HSV_ERR_ALIGN, "device pointers and strides must be multiples of 16");
+  if (sig_stride < 64 || (msg_stride != 0 && msg_stride < 32)) return fail(HSV_ERR_INVALID_ARG, "record strides overlap");
+  if (m > 0xffffffffu) return fail(HSV_ERR_INVALID_ARG, "batch too large");
+  int rc = ensure_init();
+  if (rc != HSV_OK) return rc;
+  const int pd = pointer_device(d_sig);
+  if (pd >= 0 && pd != cm->dev.device)
+    return fail(HSV_ERR_INVALID_ARG, "inputs live on device " + std::to_string(pd) + ", the committee on device " +
+                                         std::to_string(cm->dev.device));
+  DevCtx &c = ctx(cm->dev.device);
+  DeviceGuard guard(c.device);
+  if (guard.status() != hipSuccess) return hip_fail("hipSetDevice", guard.status());
+  rc = ensure_btable(c);  // the B table is rebuilt if hsv_shutdown released it
+  if (rc != HSV_OK) return rc;
+  const hipError_t e = hsv_launch_comb_verify(d_key_idx, d_sig, sig_stride, d_msg, msg_stride, (uint32_t)m, cm->dev.d_pks,
+                                              cm->dev.d_kflags, cm->dev.n, cm->dev.d_tabptr, c.d_btable, d_flags,
+                                              reinterpret_cast<hipStream_t>(stream));
+  return e == hipSuccess ? HSV_OK : hip_fail("committee verify launch", e);
+}
+
+int hsv_committee_verify(hsv_committee *cm, const uint32_t *key_idx, const uint8_t *sig, const uint8_t *msg,
+                         size_t msg_stride, size_t m, uint8_t *flags_out) {
+  if (m == 0) return HSV_OK;
+  if (!cm || !key_idx || !sig || !msg || !flags_out) return fail(HSV_ERR_INVALID_ARG, "null argument");
+  if (msg_stride != 0 && msg_stride != 32) return fail(HSV_ERR_INVALID_ARG, "msg_stride must be 0 or 32");
+  return committee_run(cm->dev, key_idx, sig, msg, msg_stride, m, flags_out);
+}
+
+int hsv_committee_verify_batch_packed(hsv_committee *cm, const uint8_t digest[32], const uint8_t *votes, size_t m) {
+  if (m == 0) return 1;
+  if (!cm || !digest || !votes) return fail(HSV_ERR_INVALID_ARG, "null argument");
+  std::vector<uint32_t> idx(m);
+  std::vector<uint8_t> sigs(m * 64);
+  for (size_t i = 0; i < m; ++i) {
+    const int64_t k = hsv_committee_index(cm, votes + 96 * i);
+    if (k < 0) {  // a non-member key: the generic kernels
+      std::vector<uint8_t> flags(m);
+      const int rc = run_host(votes, 96, votes + 32, 96, digest, 0, m, flags.data());
+      return rc != HSV_OK ? rc : batch_verdict(flags.data(), m);
+    }
+    idx[i] = (uint32_t)k;
+    std::memcpy(sigs.data() + 64 * i, votes + 96 * i + 32, 64);
+  }
+  std::vector<uint8_t> flags(m);
+  const int rc = committee_run(cm->dev, idx.data(), sigs.data(), digest, 0, m, flags.data());
+  return rc != HSV_OK ? rc : batch_verdict(flags.data(), m);
+}
+
+}  // extern "C"
+
+// ---- automatic committee cache behind the drop-in verify_batch ---------------------
+// Consensus keys are fixed per epoch (consensus/src/config.rs:39-43), so the
+// keys of every QC repeat round after round.  A key missing from the cache
+// is counted once per batch it appears in; from its second batch on it is
+// queued, and a background thread builds the queued keys' tables on a stream
+// of its own, appends them to the cache and publishes a new immutable view.
+// A verify call never waits for a build: it takes the committee kernels when
+// every key of its batch is in the published view and the generic kernels
+// otherwise, with identical flags either way (tests/test_committee.py).
+// Capacity kAutoMaxKeys keys; batches larger than that are never counted.
+// When the cache is full and batches keep missing it (a new epoch), it is
+// dropped and relearnt.  A failed build is a cache miss, never an error.
+// HSV_AUTO_COMMITTEE=0 or hsv_set_auto_committee(0) turns it off.
+namespace hsvh {
+namespace {
+
+constexpr uint32_t kAutoMaxKeys = 8192;      // 3 GiB of tables at most
+constexpr uint32_t kBlockKeys = 64;          // tables allocated 64 keys (24 MiB) at a time
+constexpr size_t kCommitteeTryMax = 4096;    // hsv_verify / verify_strict batches that try the cache
+constexpr uint32_t kResetAfterMisses = 256;  // missing batches against a full cache before a relearn
+constexpr int kMaxBuildFailures = 3;         // then the cache stays off until hsv_set_auto_committee(1)
+
+struct AutoStore {  // append-only device storage, freed with the last view using it
+  int device = 0;
+  uint8_t *d_pks = nullptr;
+  uint8_t *d_kflags = nullptr;
+  uint32_t **d_tabptr = nullptr;
+  uint32_t *d_tmp = nullptr;
+  hipStream_t stream = nullptr;  // builds only
+  std::vector<uint32_t *> blocks;
+  ~AutoStore() {
+    DeviceGuard guard(device);
+    if (stream) (void)hipStreamDestroy(stream);
+    for (uint32_t *b : blocks) (void)hipFree(b);
+    if (d_pks) (void)hipFree(d_pks);
+    if (d_kflags) (void)hipFree(d_kflags);
+    if (d_tabptr) (void)hipFree(d_tabptr);
+    if (d_tmp) (void)hipFree(d_tmp);
+  }
+};
+
+struct AutoView {  // immutable snapshot: keys [0, n) of `store` are built
+  std::shared_ptr<AutoStore> store;
+  CommitteeDev dev;
+  KeyIndex index;
+};
+
+struct AutoCommittee {
+  std::mutex mu;  // everything below; `view` is also read lock-free (atomic_load)
+  std::shared_ptr<const AutoView> view;
+  std::unordered_map<Key32, uint32_t, KeyHash> seen;  // uncached key -> batches it appeared in
+  std::vector<Key32> pending;
+  std::unordered_set<Key32, KeyHash> pending_set;
+  bool building = false;
+  uint64_t generation = 0;  // bumped by a reset; a build of an older generation is discarded
+  uint32_t miss_streak = 0;
+  int failures = 0;
+  std::thread worker;
+  std::condition_variable idle;
+  std::atomic<int> enabled{-1};  // -1: read HSV_AUTO_COMMITTEE on first use
+  std::atomic<uint64_t> builds{0};
+  ~AutoCommittee() {
+    std::unique_lock<std::mutex> lk(mu);
+    idle.wait(lk, [&] { return !building; });
+    lk.unlock();
+    if (worker.joinable()) worker.join();
+  }
+};
+
+AutoCommittee &AC() {
+  static AutoCommittee a;
+  return a;
+}
+
+bool auto_enabled() {
+  AutoCommittee &a = AC();
+  int e = a.enabled.load();
+  if (e < 0) {
+    const char *v = std::getenv("HSV_AUTO_COMMITTEE");
+    e = (v && v[0] == '0') ? 0 : 1;
+    a.enabled.store(e);
+  }
+  return e == 1;
+}
+
+std::shared_ptr<const AutoView> current_view() { return std::atomic_load(&AC().view); }
+
+// Build tables for `keys` on top of `base` (nullptr: a fresh store on
+// `device`).  Runs without the cache lock.
+int build_view(const std::shared_ptr<const AutoView> &base, int device, const std::vector<Key32> &keys,
+               std::shared_ptr<const AutoView> &out) {
+  DeviceGuard guard(device);
+  if (guard.status() != hipSuccess) return hip_fail("hipSetDevice", guard.status());
+  std::shared_ptr<AutoStore> store = base ? base->store : std::make_shared<AutoStore>();
+  const uint32_t n0 = base ? base->dev.n : 0;
+  const uint32_t m = std::min<uint32_t>((uint32_t)keys.size(), kAutoMaxKeys - n0);
+  hipError_t e = hipSuccess;
+  if (!base) {
+    store->device = device;
+    e = hipMalloc(&store->d_pks, (size_t)kAutoMaxKeys * 32);
+    if (e == hipSuccess) e = hipMalloc(&store->d_kflags, kAutoMaxKeys);
+    if (e == hipSuccess) e = hipMalloc(&store->d_tabptr, (size_t)kAutoMaxKeys * sizeof(uint32_t *));
+    if (e == hipSuccess) e = hipMalloc(&store->d_tmp, hsv_comb_tmp_bytes(kBlockKeys));
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&store->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail("allocating the committee cache", e);
+  }
+  const uint64_t words = hsv_comb_table_bytes() / 4;
+  while ((uint64_t)store->blocks.size() * kBlockKeys < (uint64_t)n0 + m) {
+    uint32_t *blk = nullptr;
+    e = hipMalloc(&blk, (size_t)kBlockKeys * hsv_comb_table_bytes());
+    if (e != hipSuccess) return hip_fail("allocating committee tables", e);
+    store->blocks.push_back(blk);
+  }
+  std::vector<uint8_t> encs((size_t)m * 32);
+  std::vector<uint32_t *> ptrs(m);
+  for (uint32_t i = 0; i < m; ++i) {
+    std::memcpy(encs.data() + (size_t)i * 32, keys[i].data(), 32);
+    const uint32_t slot = n0 + i;
+    ptrs[i] = store->blocks[slot / kBlockKeys] + (uint64_t)(slot % kBlockKeys) * words;
+  }
+  e = hipMemcpyAsync(store->d_pks + (size_t)n0 * 32, encs.data(), encs.size(), hipMemcpyHostToDevice, store->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(store->d_tabptr + n0, ptrs.data(), m * sizeof(uint32_t *), hipMemcpyHostToDevice, store->stream);
+  if (e == hipSuccess)
+    e = build_tables(store->d_pks + (size_t)n0 * 32, m, ptrs.data(), store->d_kflags + n0, store->d_tmp, kBlockKeys,
+                     store->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(store->stream);
+  if (e != hipSuccess) return hip_fail("building committee tables", e);
+  auto v = std::make_shared<AutoView>();
+  v->store = store;
+  v->dev.device = store->device;
+  v->dev.n = n0 + m;
+  v->dev.d_pks = store->d_pks;
+  v->dev.d_kflags = store->d_kflags;
+  v->dev.d_tabptr = store->d_tabptr;
+  if (base) v->index = base->index;
+  for (uint32_t i = 0; i < m; ++i) v->index.emplace(keys[i], n0 + i);
+  out = v;
+  return HSV_OK;
+}
+
+void worker_main() {
+  AutoCommittee &a = AC();
+  std::unique_lock<std::mutex> lk(a.mu);
+  for (;;) {
+    if (a.pending.empty() || a.enabled.load() != 1) {
+      a.pending.clear();
+      a.pending_set.clear();
+      a.building = false;
+      a.idle.notify_all();
+      return;
+    }
+    std::vector<Key32> keys;
+    keys.swap(a.pending);
+    const uint64_t gen = a.generation;
+    std::shared_ptr<const AutoView> base = a.view;
+    const int device = base ? base->dev.device : home_device();
+    lk.unlock();
+    std::shared_ptr<const AutoView> built;
+    const int rc = build_view(base, device, keys, built);
+    lk.lock();
+    for (const Key32 &k : keys) {
+      a.pending_set.erase(k);
+      a.seen.erase(k);
+    }
+    if (rc == HSV_OK && gen == a.generation) {
+      std::atomic_store(&a.view, built);
+      a.builds.fetch_add(1);
+    } else if (rc != HSV_OK && ++a.failures >= kMaxBuildFailures) {
+      a.enabled.store(0);  // verification goes on through the generic kernels
+    }
+  }
+}
+
+// The view to verify this batch with (every key in it; idx receives the
+// member indices), or nullptr: the generic path.  Records misses.
+std::shared_ptr<const AutoView> auto_lookup(const uint8_t *pk, size_t pk_stride, size_t n, uint32_t *idx,
+                                            bool count_misses) {
+  std::shared_ptr<const AutoView> v = current_view();
+  std::vector<Key32> missing;
+  for (size_t i = 0; i < n; ++i) {
+    const Key32 k = key_of(pk + i * pk_stride);
+    if (v) {
+      auto it = v->index.find(k);
+      if (it != v->index.end()) {
+        idx[i] = it->second;
+        continue;
+      }
+    }
+    if (!count_misses) return nullptr;
+    missing.push_back(k);
+  }
+  AutoCommittee &a = AC();
+  if (missing.empty()) {
+    if (v && v->dev.device != home_device()) return nullptr;  // cache lives on another device
+    std::lock_guard<std::mutex> lk(a.mu);
+    a.miss_streak = 0;
+    return v;
+  }
+  if (n > kAutoMaxKeys) return nullptr;  // not a committee-sized batch
+  std::sort(missing.begin(), missing.end());
+  missing.erase(std::unique(missing.begin(), missing.end()), missing.end());  // once per batch
+  std::unique_lock<std::mutex> lk(a.mu);
+  const uint32_t cached = v ? v->dev.n : 0;
+  if (cached + a.pending_set.size() >= kAutoMaxKeys && ++a.miss_streak >= kResetAfterMisses) {
+    // a full cache that keeps missing: a new epoch, relearn from scratch
+    std::atomic_store(&a.view, std::shared_ptr<const AutoView>());
+    a.seen.clear();
+    a.pending.clear();
+    a.pending_set.clear();
+    a.miss_streak = 0;
+    ++a.generation;
+    return nullptr;
+  }
+  for (const Key32 &k : missing) {
+    if (a.pending_set.count(k)) continue;
+    if (++a.seen[k] >= 2 && cached + a.pending_set.size() < kAutoMaxKeys) {
+      a.pending.push_back(k);
+      a.pending_set.insert(k);
+    }
+  }
+  if (a.seen.size() > 4 * (size_t)kAutoMaxKeys) a.seen.clear();
+  if (!a.pending.empty() && !a.building && a.enabled.load() == 1) {
+    a.building = true;
+    if (a.worker.joinable()) a.worker.join();  // the previous build thread has finished
+    a.worker = std::thread(worker_main);
+  }
+  return nullptr;
+}
+
+void auto_reset(bool enable) {
+  AutoCommittee &a = AC();
+  std::unique_lock<std::mutex> lk(a.mu);
+  a.enabled.store(enable ? 1 : 0);
+  if (!enable) {
+    a.pending.clear();
+    a.idle.wait(lk, [&] { return !a.building; });
+    std::atomic_store(&a.view, std::shared_ptr<const AutoView>());
+    a.seen.clear();
+    a.pending_set.clear();
+    a.miss_streak = 0;
+    a.failures = 0;
+    ++a.generation;
+  } else {
+    a.failures = 0;
+  }
+}
+
+}  // namespace
+
+int auto_committee_try(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, size_t msg_stride, size_t n,
+                       uint8_t *flags_out) {
+  // only the latency range (a vote, a TC); large batches of fresh keys would
+  // pay a hash lookup per item for nothing
+  if (n > kCommitteeTryMax || !auto_enabled()) return 1;
+  std::vector<uint32_t> idx(n);
+  std::shared_ptr<const AutoView> v = auto_lookup(pk, 32, n, idx.data(), false);
+  if (!v || v->dev.device != home_device()) return 1;
+  return committee_run(v->dev, idx.data(), sig, msg, msg_stride, n, flags_out);
+}
+
+void auto_committee_shutdown() {
+  auto_reset(false);
+  AutoCommittee &a = AC();
+  std::lock_guard<std::mutex> lk(a.mu);
+  a.enabled.store(-1);  // re-read the environment on next use
+}
+
+}  // namespace hsvh
+
+extern "C" {
+
+int hsv_verify_batch_packed(const uint8_t digest[32], const uint8_t *votes, size_t n) {
+  if (n == 0) return 1;
+  if (!digest || !votes) return fail(HSV_ERR_INVALID_ARG, "null argument");
+  int rc = ensure_init();
+  if (rc != HSV_OK) return rc;
+  std::vector<uint8_t> flags(n);
+  if (n >= 2 && auto_enabled()) {
+    std::vector<uint32_t> idx(n);
+    std::shared_ptr<const AutoView> v = auto_lookup(votes, 96, n, idx.data(), true);
+    if (v) {
+      std::vector<uint8_t> sigs(n * 64);
+      for (size_t i = 0; i < n; ++i) std::memcpy(sigs.data() + 64 * i, votes + 96 * i + 32, 64);
+      rc = committee_run(v->dev, idx.data(), sigs.data(), digest, 0, n, flags.data());
+      if (rc == HSV_OK) return batch_verdict(flags.data(), n);
+      // an infrastructure error on the cached path: the generic path answers
+    }
+  }
+  rc = run_host(votes, 96, votes + 32, 96, digest, 0, n, flags.data());
+  return rc != HSV_OK ? rc : batch_verdict(flags.data(), n);
+}
+
+int hsv_set_auto_committee(int enable) {
+  auto_reset(enable != 0);
+  return HSV_OK;
+}
+
+size_t hsv_auto_committee_size(void) {
+  std::shared_ptr<const AutoView> v = current_view();
+  return v ? v->dev.n : 0;
+}
+
+int hsv_auto_committee_wait(int timeout_ms) {
+  AutoCommittee &a = AC();
+  std::unique_lock<std::mutex> lk(a.mu);
+  const bool done = a.idle.wait_for(lk, std::chrono::milliseconds(timeout_ms < 0 ? 0 : timeout_ms),
+                                    [&] { return !a.building; });
+  return done ? 1 : 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,131 @@
+// Host-side state shared by the C-ABI translation units (hsv_capi.cpp,
+// hsv_committee_api.cpp, hsv_tx.cpp).  Not part of the public ABI.
+//
+// Device model (include/hsv.h, hsv_init):
+//   * one DevCtx per visible GPU, created lazily;
+//   * each DevCtx owns a small pool of Slots (stream + pinned staging +
+//     device buffer + mutex), so concurrent host-buffer calls -- several
+//     tokio workers verifying QCs and votes at once -- run side by side
+//     instead of queueing on one staging buffer;
+//   * the fixed-base B tables (narrow comb for the committee kernels, wide
+//     comb for the generic kernels) are per device and shared by its slots.
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <atomic>
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "hsv.h"
+#include "hsv_internal.h"
+
+namespace hsvh {
+
+// ---- errors ----------------------------------------------------------------
+int fail(int code, const std::string &msg);
+int hip_fail(const char *where, hipError_t e);
+const std::string &last_error();
+
+// ---- sizes -------------------------------------------------------------------
+constexpr size_t kAlign = 256;
+constexpr size_t kChunk = size_t(1) << 22;        // items per verification launch
+constexpr size_t kShardMin = size_t(1) << 16;     // shard host batches across devices at or above this
+constexpr size_t kZeroCopyMax = size_t(1) << 12;  // small batches read straight from pinned memory
+inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// ---- device contexts ---------------------------------------------------------
+struct Slot {
+  std::mutex mu;
+  hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // second pipeline stage of large host batches
+  uint8_t *d_buf = nullptr;
+  size_t d_cap = 0;
+  uint8_t *h_buf = nullptr;
+  size_t h_cap = 0;
+};
+
+struct DevCtx {
+  int device = 0;
+  int cus = 0;
+  std::mutex table_mu;             // guards the two B tables below
+  uint32_t *d_btable = nullptr;    // narrow comb of B (committee kernels)
+  uint32_t *d_btable16 = nullptr;  // wide comb of B (generic kernels)
+  std::vector<std::unique_ptr<Slot>> slots;
+  std::atomic<unsigned> rr{0};
+};
+
+// Makes `device` current for the calling thread and restores the previous
+// current device on destruction (the library never leaves the caller's
+// thread on another device).
+class DeviceGuard {
+ public:
+  explicit DeviceGuard(int device);
+  ~DeviceGuard();
+  hipError_t status() const { return status_; }
+
+ private:
+  int prev_ = -1;
+  hipError_t status_ = hipSuccess;
+};
+
+int ensure_init();  // HSV_OK or HSV_ERR_NO_DEVICE
+int device_count_inited();
+DevCtx &ctx(int device);
+int variant();
+
+// Device a host-buffer call of n items that is not sharded runs on: the
+// bound device (hsv_init(d) / HSV_DEVICE), else the calling thread's
+// current HIP device.
+int home_device();
+// Number of shards a host batch of n items is split into (1 = no sharding)
+// and the device shard s runs on.
+int shard_count(size_t n);
+int shard_device(int shard, int nshards);
+
+// Lock a free slot of `c` (try every slot, then wait on one).
+class SlotLease {
+ public:
+  explicit SlotLease(DevCtx &c);
+  Slot &slot() { return *s_; }
+
+ private:
+  Slot *s_;
+  std::unique_lock<std::mutex> lk_;
+};
+
+// Stream and buffers of a slot (current device must be c.device).
+int slot_prepare(Slot &s, size_t dev_bytes, size_t host_bytes);
+int slot_stream2(Slot &s);
+
+// B tables of device c (current device must be c.device).
+int ensure_btable(DevCtx &c);
+int ensure_btable16(DevCtx &c);
+int comb_table_for(DevCtx &c, int variant, const uint32_t **out);
+
+// memcpy into pinned staging; large copies split over a few host threads
+void stage_copy(uint8_t *dst, const uint8_t *src, size_t bytes);
+
+// Device owning a device pointer (hipPointerGetAttributes); -1 if unknown.
+int pointer_device(const void *p);
+// Resolve the device a device-API call runs on: the device of its input
+// pointers, checked against the stream's device.  Returns HSV_OK and sets
+// *dev, or an error.
+int device_for_call(const void *d_ptr, void *stream, int *dev);
+
+// ---- the automatic committee cache (hsv_committee_api.cpp) --------------------
+// Strict verification of small batches whose keys are all cached: HSV_OK
+// when done, 1 when the caller should take the generic path, < 0 on error.
+int auto_committee_try(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, size_t msg_stride, size_t n,
+                       uint8_t *flags_out);
+void auto_committee_shutdown();
+
+// The generic host-buffer path (hsv_capi.cpp): records at the given strides.
+int run_host(const uint8_t *pk, size_t pk_stride, const uint8_t *sig, size_t sig_stride, const uint8_t *msg,
+             size_t msg_stride, size_t n, uint8_t *flags_out);
+int batch_verdict(const uint8_t *flags, size_t n);
+
+}  // namespace hsvh

@@ -8,7 +8,9 @@ extern "C" {
 #endif
 
 // Enqueue one verification launch on `stream` (no synchronisation).
-int hsv_num_variants(void);
+int hsv_num_variants(void);            // id space
+int hsv_variant_list(int *out, int cap);  // ids built into this library; returns their count
+int hsv_variant_available(int variant);
 hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig,
                              uint64_t sig_stride, const uint8_t *msg, uint64_t msg_stride,
                              uint32_t n, uint8_t *flags_out, uint32_t *strict_bits,
@@ -31,9 +33,10 @@ extern "C" {
 #endif
 hipError_t hsv_launch_comb_build(const uint8_t *encs, uint32_t nkeys, uint32_t negate, uint32_t *tables,
                                  uint32_t *tmp, uint8_t *key_flags, hipStream_t stream);
+// key_tables[i]: device pointer to key i's comb table (hsv_comb_table_bytes)
 hipError_t hsv_launch_comb_verify(const uint32_t *key_idx, const uint8_t *sig, uint64_t sig_stride,
                                   const uint8_t *msg, uint64_t msg_stride, uint32_t m, const uint8_t *pks,
-                                  const uint8_t *key_flags, uint32_t nkeys, const uint32_t *tables,
+                                  const uint8_t *key_flags, uint32_t nkeys, const uint32_t *const *key_tables,
                                   const uint32_t *btable, uint8_t *flags_out, hipStream_t stream);
 uint64_t hsv_comb_table_bytes(void);
 uint64_t hsv_comb_tmp_bytes(uint32_t nkeys);

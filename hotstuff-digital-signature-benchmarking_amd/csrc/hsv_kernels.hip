@@ -18,6 +18,9 @@
 
 namespace hsv {
 
+constexpr int kBlock = 256;
+
+#if HSV_ALL_VARIANTS
 __device__ const uint32_t g_btable[256 * 24] = {
 #include "hsv_btable.inc"
 };
@@ -47,8 +50,6 @@ struct LdsBTab {
     return n;
   }
 };
-
-constexpr int kBlock = 256;
 
 // One verification per lane.  WA/WB: window widths (hsv_verify_core.hpp);
 // WAVES: waves per SIMD requested from the register allocator (256 regs at 2,
@@ -119,6 +120,8 @@ hsv_verify_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
   }
 }
 
+#endif  // HSV_ALL_VARIANTS
+
 // Per-lane variable-base tables in global memory (hsv_verify_core.hpp, VT):
 // lane region = 2 tables x ENT entries x 128 B, entry = 8 x uint4.
 template <int ENT>
@@ -142,6 +145,7 @@ struct GlobalVarTab {
 template <int WA>
 constexpr int vt_lane_uint4() { return 2 * ((1 << (WA - 1)) + 1) * 8; }
 
+#if HSV_ALL_VARIANTS
 // Half-size scalars with memory-resident variable-base tables.  Persistent
 // grid: block b owns lane slots [b*kBlock, (b+1)*kBlock) of `vt_ws` and walks
 // the batch with stride gridDim.x * kBlock.
@@ -204,6 +208,8 @@ hsv_verify_mt_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
   }
 }
 
+#endif  // HSV_ALL_VARIANTS
+
 // one (pk, sig, msg) record into words
 __device__ __forceinline__ void load_triple(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig,
                                             uint64_t sig_stride, const uint8_t *msg, uint64_t msg_stride,
@@ -232,6 +238,7 @@ struct HcCounters {
   uint32_t pad;
 };
 
+#if HSV_ALL_VARIANTS
 // Half-size scalars + comb table for B (hsv_verify_hc.hpp).  No LDS; the
 // per-lane tables live in `vt_ws` (lane slot = blockIdx * kBlock + threadIdx),
 // the B comb table `comb_b` is read through L2 / MALL.  Work is handed out
@@ -316,6 +323,8 @@ hsv_verify_fb_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
     }
   }
 }
+
+#endif  // HSV_ALL_VARIANTS
 
 // Two-pass form (hsv_verify_hc.hpp, prep_scalars / verify_one_prepped).
 // Pass 1: one lane per item, scalar work only; records to `rec` (SoA, row
@@ -512,6 +521,7 @@ hsv_verify_pair_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const
   }
 }
 
+#if HSV_ALL_VARIANTS
 // Point pass with a pair-lane tail (variant 22): as hsv_verify_hp_kernel, but
 // the last n_tail items (a multiple-of-64 boundary, about one round of the
 // persistent grid) are dealt out as 32-item batches run two lanes per item
@@ -587,6 +597,8 @@ hsv_verify_hpt_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const 
   }
 }
 
+#endif  // HSV_ALL_VARIANTS
+
 // ---- v_mad_u64_u32 issue-rate probe -------------------------------------
 // 8 independent accumulation chains, 16 mads per asm statement (the compiler
 // puts an s_nop after every asm statement that writes an SGPR, so one mad per
@@ -638,10 +650,12 @@ __global__ void __launch_bounds__(256) hsv_mad_peak_kernel(uint32_t *sink, uint3
 //  21: as 19 for batches above 2^13 items; at or below, the latency form:
 //      prepass, then two lanes per item (hsv_verify_pair_kernel)
 //  22: as 21 with a pair-lane tail in the large-batch point pass (hsv_verify_hpt_kernel)
+// id space of the variants (hsv_variant_list gives the ids built into this library)
 extern "C" int hsv_num_variants(void) { return 23; }
 
 namespace {
 
+#if HSV_ALL_VARIANTS
 // Persistent-grid launch of hsv_verify_mt_kernel with a stream-ordered
 // workspace for the per-lane tables (freed on the same stream).
 template <int WA, int WB, int WAVES, bool COMB, bool PREFETCH = true, int CB = 8, bool DEFER = false>
@@ -709,6 +723,8 @@ hipError_t launch_mt(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
   return e != hipSuccess ? e : ef;
 }
 
+#endif  // HSV_ALL_VARIANTS
+
 // Two-pass launch (variants 19/20): prepass over all items, then the
 // persistent point pass.  Workspace: per-lane tables | counters (256 B) |
 // fallback list (4 B per item) | prep records (kPrepWords x 4 B per item).
@@ -716,9 +732,12 @@ template <int WA, int WAVES, int CB, bool TAIL = false>
 hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
                      const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
                      uint32_t *strict_bits, const uint32_t *comb_b, hipStream_t stream) {
-  const void *kern;
+  const void *kern = reinterpret_cast<const void *>(hsv::hsv_verify_hp_kernel<WA, WAVES, CB>);
+#if HSV_ALL_VARIANTS
   if constexpr (TAIL) kern = reinterpret_cast<const void *>(hsv::hsv_verify_hpt_kernel<WA, WAVES, CB>);
-  else kern = reinterpret_cast<const void *>(hsv::hsv_verify_hp_kernel<WA, WAVES, CB>);
+#else
+  static_assert(!TAIL, "the pair-tail point pass is built with HSV_ALL_VARIANTS only");
+#endif
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
@@ -764,6 +783,7 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
     e = hipGetLastError();
   }
   if (e == hipSuccess) {
+#if HSV_ALL_VARIANTS
     if constexpr (TAIL) {
       // about one round of the grid as pair batches; the regular range stays a multiple of 64
       const uint32_t target = grid * (hsv::kBlock / 64u) * 32u;
@@ -771,7 +791,9 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
       hipLaunchKernelGGL((hsv::hsv_verify_hpt_kernel<WA, WAVES, CB>), dim3(grid), dim3(hsv::kBlock), 0, stream,
                          pk, pk_stride, sig, sig_stride, msg, msg_stride, n, n_tail, flags_out, strict_bits, vt_ws,
                          comb_b, rec, ctr, fb_list);
-    } else {
+    } else
+#endif
+    {
       hipLaunchKernelGGL((hsv::hsv_verify_hp_kernel<WA, WAVES, CB>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
                          pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, vt_ws, comb_b, rec,
                          ctr, fb_list);
@@ -831,11 +853,27 @@ extern "C" hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t
                                         uint8_t *flags_out, uint32_t *strict_bits,
                                         const uint32_t *comb_b, hipStream_t stream) {
   if (n == 0) return hipSuccess;
+  if (hsv_variant_needs_comb(variant) && !comb_b) return hipErrorInvalidValue;
+  switch (variant) {
+    case 19:
+      return launch_hp<4, 3, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
+    case 21:
+      if (n <= kPairMax)
+        return launch_pair<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
+      return launch_hp<4, 3, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
+#if HSV_ALL_VARIANTS
+    default: break;
+#else
+    default: return hipErrorInvalidValue;
+#endif
+  }
+#if HSV_ALL_VARIANTS
   const uint32_t grid = (n + hsv::kBlock - 1) / hsv::kBlock;
 #define HSV_LAUNCH(WA, WB, WV, HALF)                                                           \
   hipLaunchKernelGGL((hsv::hsv_verify_kernel<WA, WB, WV, HALF>), dim3(grid), dim3(hsv::kBlock), 0, \
                      stream, pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out,   \
                      strict_bits)
+#define HSV_ARGS pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream
   switch (variant) {
     case 0: HSV_LAUNCH(2, 8, 2, false); break;
     case 1: HSV_LAUNCH(3, 9, 1, false); break;
@@ -844,43 +882,50 @@ extern "C" hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t
     case 4: HSV_LAUNCH(3, 9, 2, true); break;
     case 5: HSV_LAUNCH(3, 9, 1, true); break;
     case 6: HSV_LAUNCH(2, 8, 2, true); break;
-#define HSV_LAUNCH_MT(WA, WB, WV, COMB) \
-  return launch_mt<WA, WB, WV, COMB>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream)
-    case 7: HSV_LAUNCH_MT(3, 9, 2, false);
-    case 8: HSV_LAUNCH_MT(2, 8, 2, false);
-    case 9: HSV_LAUNCH_MT(4, 8, 2, false);
-    case 10: if (!comb_b) return hipErrorInvalidValue; HSV_LAUNCH_MT(3, 3, 2, true);
-    case 11: if (!comb_b) return hipErrorInvalidValue; HSV_LAUNCH_MT(4, 4, 2, true);
-    case 12: if (!comb_b) return hipErrorInvalidValue; HSV_LAUNCH_MT(5, 5, 2, true);
-    case 13: if (!comb_b) return hipErrorInvalidValue;
-      return launch_mt<4, 4, 3, true, false>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
-    case 14: if (!comb_b) return hipErrorInvalidValue;
-      return launch_mt<4, 4, 2, true, false>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
-    case 15: if (!comb_b) return hipErrorInvalidValue;
-      return launch_mt<4, 4, 3, true, false, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
-    case 16: if (!comb_b) return hipErrorInvalidValue;
-      return launch_mt<4, 4, 2, true, false, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
-    case 17: if (!comb_b) return hipErrorInvalidValue;
-      return launch_mt<4, 4, 3, true, false, 16, true>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
-    case 18: if (!comb_b) return hipErrorInvalidValue;
-      return launch_mt<4, 4, 2, true, false, 16, true>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
-    case 19: if (!comb_b) return hipErrorInvalidValue;
-      return launch_hp<4, 3, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
-    case 20: if (!comb_b) return hipErrorInvalidValue;
-      return launch_hp<4, 2, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
-    case 21: if (!comb_b) return hipErrorInvalidValue;
-      if (n <= kPairMax)
-        return launch_pair<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
-      return launch_hp<4, 3, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
-    case 22: if (!comb_b) return hipErrorInvalidValue;
-      if (n <= kPairMax)
-        return launch_pair<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
-      return launch_hp<4, 3, 16, true>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
-#undef HSV_LAUNCH_MT
+    case 7: return launch_mt<3, 9, 2, false>(HSV_ARGS);
+    case 8: return launch_mt<2, 8, 2, false>(HSV_ARGS);
+    case 9: return launch_mt<4, 8, 2, false>(HSV_ARGS);
+    case 10: return launch_mt<3, 3, 2, true>(HSV_ARGS);
+    case 11: return launch_mt<4, 4, 2, true>(HSV_ARGS);
+    case 12: return launch_mt<5, 5, 2, true>(HSV_ARGS);
+    case 13: return launch_mt<4, 4, 3, true, false>(HSV_ARGS);
+    case 14: return launch_mt<4, 4, 2, true, false>(HSV_ARGS);
+    case 15: return launch_mt<4, 4, 3, true, false, 16>(HSV_ARGS);
+    case 16: return launch_mt<4, 4, 2, true, false, 16>(HSV_ARGS);
+    case 17: return launch_mt<4, 4, 3, true, false, 16, true>(HSV_ARGS);
+    case 18: return launch_mt<4, 4, 2, true, false, 16, true>(HSV_ARGS);
+    case 20: return launch_hp<4, 2, 16>(HSV_ARGS);
+    case 22:
+      if (n <= kPairMax) return launch_pair<4, 16>(HSV_ARGS);
+      return launch_hp<4, 3, 16, true>(HSV_ARGS);
     default: return hipErrorInvalidValue;
   }
+#undef HSV_ARGS
 #undef HSV_LAUNCH
   return hipGetLastError();
+#endif
+}
+
+// Variant ids compiled into this library.  The product build carries the
+// default (21: variant 19's two-pass kernels above 2^13 items, the pair-lane
+// latency form at or below) and 19 itself; the other ids are measurement
+// history, built only with HSV_ALL_VARIANTS=1 (make ALL_VARIANTS=1).
+#if HSV_ALL_VARIANTS
+static const int kVariantIds[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22};
+#else
+static const int kVariantIds[] = {19, 21};
+#endif
+
+extern "C" int hsv_variant_list(int *out, int cap) {
+  const int n = (int)(sizeof(kVariantIds) / sizeof(kVariantIds[0]));
+  for (int i = 0; out && i < n && i < cap; ++i) out[i] = kVariantIds[i];
+  return n;
+}
+
+extern "C" int hsv_variant_available(int variant) {
+  for (int v : kVariantIds)
+    if (v == variant) return 1;
+  return 0;
 }
 
 extern "C" double hsv_launch_mad_peak(int device_cus) {

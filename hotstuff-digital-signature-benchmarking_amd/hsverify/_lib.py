@@ -17,7 +17,9 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhsv.so")
+# HSV_LIB=libhsv_all.so selects the measurement build with every kernel
+# variant (make ALL_VARIANTS=1); it must live in this directory as well.
+LIB_PATH = os.path.join(_HERE, os.path.basename(os.environ.get("HSV_LIB", "libhsv.so")))
 
 # flag bits (include/hsv.h)
 STRICT_OK = 0x01
@@ -53,6 +55,11 @@ def _declare(lib):
     sz = ctypes.c_size_t
     sig = {
         "hsv_init": (ctypes.c_int, [ctypes.c_int]),
+        "hsv_bound_device": (ctypes.c_int, []),
+        "hsv_set_virtual_shards": (ctypes.c_int, [ctypes.c_int]),
+        "hsv_auto_committee_wait": (ctypes.c_int, [ctypes.c_int]),
+        "hsv_variant_list": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+        "hsv_variant_available": (ctypes.c_int, [ctypes.c_int]),
         "hsv_shutdown": (None, []),
         "hsv_device_count": (ctypes.c_int, []),
         "hsv_last_error": (ctypes.c_char_p, []),

@@ -54,16 +54,20 @@ def verify_device(pk, sig, msg, flags=None, strict_bits=None, stream=None) -> No
     import torch
 
     n = pk.shape[0]
-    if stream is None:
-        stream = torch.cuda.current_stream(pk.device).cuda_stream
-    msg_stride = 0 if msg.dim() == 1 else msg.stride(0)
-    lib = _lib.load()
-    rc = lib.hsv_verify_device_bits(
-        ctypes.c_void_p(pk.data_ptr()), pk.stride(0), ctypes.c_void_p(sig.data_ptr()), sig.stride(0),
-        ctypes.c_void_p(msg.data_ptr()), msg_stride, n,
-        ctypes.c_void_p(flags.data_ptr()) if flags is not None else None,
-        ctypes.c_void_p(strict_bits.data_ptr()) if strict_bits is not None else None,
-        ctypes.c_void_p(stream))
+    for t in (sig, msg, flags, strict_bits):
+        if t is not None and t.device != pk.device:
+            raise ValueError(f"all tensors must live on {pk.device}, got {t.device}")
+    with torch.cuda.device(pk.device):  # the library launches on the inputs' device
+        if stream is None:
+            stream = torch.cuda.current_stream(pk.device).cuda_stream
+        msg_stride = 0 if msg.dim() == 1 else msg.stride(0)
+        lib = _lib.load()
+        rc = lib.hsv_verify_device_bits(
+            ctypes.c_void_p(pk.data_ptr()), pk.stride(0), ctypes.c_void_p(sig.data_ptr()), sig.stride(0),
+            ctypes.c_void_p(msg.data_ptr()), msg_stride, n,
+            ctypes.c_void_p(flags.data_ptr()) if flags is not None else None,
+            ctypes.c_void_p(strict_bits.data_ptr()) if strict_bits is not None else None,
+            ctypes.c_void_p(stream))
     _lib.check(rc, "hsv_verify_device_bits")
 
 
@@ -95,4 +99,24 @@ def get_variant() -> int:
 
 
 def num_variants() -> int:
+    """Size of the variant id space (not all ids are built: see variants())."""
     return _lib.load().hsv_num_variants()
+
+
+def variants() -> list:
+    """Kernel variant ids built into the loaded library (product build: 19, 21)."""
+    lib = _lib.load()
+    n = lib.hsv_variant_list(None, 0)
+    buf = (ctypes.c_int * n)()
+    lib.hsv_variant_list(buf, n)
+    return list(buf)
+
+
+def bind_device(device: int) -> int:
+    """hsv_init: -1 = every visible GPU (large host batches sharded), d >= 0 = GPU d only."""
+    return _lib.check(_lib.load().hsv_init(device), "hsv_init")
+
+
+def set_virtual_shards(k: int) -> None:
+    """Test hook: split host batches of >= 2^16 items into k shards (0 = default)."""
+    _lib.check(_lib.load().hsv_set_virtual_shards(k), "hsv_set_virtual_shards")

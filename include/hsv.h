@@ -56,11 +56,27 @@ extern "C" {
 #define HSV_ERR_ALIGN (-5)
 #define HSV_ERR_PARSE (-6) /* malformed wire bytes (hsv_*_bincode) */
 
-/* ---- lifecycle ---------------------------------------------------------- */
-/* Optional: contexts are created lazily on first use.  device = -1 selects
- * every visible GPU (large host-buffer batches are then sharded across them
- * by contiguous range).  Returns the number of devices initialised or < 0. */
+/* ---- lifecycle and device binding -------------------------------------- */
+/* Optional: contexts are created lazily on first use.
+ *   device >= 0  binds the process to that GPU: every host-buffer call
+ *                (hsv_verify*, hsv_verify_batch*, transactions, certificates,
+ *                committee creation) runs on it.  This is the one-process-
+ *                per-GPU deployment (the reference runs one node per process,
+ *                node/src/main.rs:16); returns 1.
+ *   device == -1 every visible GPU: host batches of >= 2^16 items are
+ *                sharded across them by contiguous range (one host thread
+ *                each, flags gathered into the caller's buffer); smaller
+ *                batches run on the calling thread's current HIP device.
+ *                Returns the number of devices.
+ * Without a call, the environment variable HSV_DEVICE (same values) applies,
+ * else -1.  Each device keeps a pool of HSV_SLOTS (default 4) staging slots,
+ * so concurrent calls (several tokio workers) do not queue behind one buffer.
+ * Device-resident calls (hsv_*_device*) always run on the device that owns
+ * their input pointers; a stream of another device is an error.
+ * Returns < 0 for a device index out of range. */
 int hsv_init(int device);
+/* The binding in effect: a device index, or -1 for "every device". */
+int hsv_bound_device(void);
 /* Release all device buffers, streams and pinned staging memory. */
 void hsv_shutdown(void);
 /* Number of visible HIP devices (0 when none). */
@@ -92,17 +108,25 @@ int hsv_verify_batch_packed(const uint8_t digest[32], const uint8_t *votes, size
 
 /* Automatic committee cache behind hsv_verify_batch[_packed] (on by default;
  * env HSV_AUTO_COMMITTEE=0 turns it off).  Consensus keys repeat every round
- * (consensus/src/config.rs Committee), so once a batch carries keys seen in an
- * earlier batch, comb tables are built for them (one-time cost, ~4 ms per 1000
- * keys, at most 8192 keys) and later batches of cached keys take the
- * committee kernels.  Verdicts are identical either way.  enable = 0 also
- * drops the cache. */
+ * (consensus/src/config.rs Committee): a key seen in two batches is queued,
+ * and a background thread builds its comb table on a stream of its own and
+ * appends it to the cache (at most 8192 keys, 384 KiB each; batches of more
+ * than 8192 votes are never cached).  A verify call never waits for a build:
+ * batches whose keys are all cached take the committee kernels, all others
+ * the generic kernels, with identical flags either way.  A failed build is a
+ * cache miss, never an error; when a full cache keeps missing (a new epoch)
+ * it is dropped and relearnt.  Strict batches of <= 4096 cached keys
+ * (hsv_verify, hsv_verify_strict) use it too.  enable = 0 also drops it. */
 int hsv_set_auto_committee(int enable);
 /* Number of keys in the automatic cache (0 when none). */
 size_t hsv_auto_committee_size(void);
+/* Wait up to timeout_ms for a pending cache build to be published:
+ * 1 = no build in flight, 0 = timed out.  (Warm-up and tests.) */
+int hsv_auto_committee_wait(int timeout_ms);
 
 /* ---- verification, device-resident buffers (stream-ordered, async) ------ */
-/* Inputs already in HBM of the current device.  Record i reads
+/* Inputs already in HBM (of any device: the call runs on the device owning
+ * d_pk, and `stream` must belong to it).  Record i reads
  * pk + i*pk_stride (32 B), sig + i*sig_stride (64 B), msg + i*msg_stride
  * (32 B; msg_stride may be 0).  Pointers and strides must be multiples of 16.
  * Writes n flag bytes to d_flags.  stream: a hipStream_t (NULL = default).
@@ -120,7 +144,7 @@ int hsv_verify_device_bits(const uint8_t *d_pk, size_t pk_stride, const uint8_t 
 
 /* ---- committee key cache --------------------------- */
 /* Consensus keys are fixed per epoch (consensus/src/config.rs Committee).  A
- * committee holds, in HBM of the device current at creation, a 384 KiB
+ * committee holds, in HBM of the device bound at creation (hsv_init), a 384 KiB
  * fixed-base comb table of -A per key; verifying a vote by a member then costs
  * 64 mixed additions and no doublings.  Flags are identical to hsv_verify's
  * (undecodable or small-order keys are accepted as members and reported

@@ -18,6 +18,9 @@
  *                       R' = vartime_double_scalar_mul_basepoint(k, -A, s)
  *                       (width-5 NAF for A, width-8 NAF table for B), R' == R
  *                       as projective points.
+ *   verify_batch        (oracle_verify_batch_dalek) random linear combination,
+ *                       one multiscalar multiplication (Straus / Pippenger),
+ *                       the reference's QC path; timed as the QC CPU baseline.
  * Flag bits match include/hsv.h.
  */
 #include <pthread.h>
@@ -512,6 +515,8 @@ static void double_scalar_mul(ge *r, const uint8_t a[32], const ge *A, const uin
   *r = q;
 }
 
+void oracle_sc_reduce64_fast(uint8_t out[32], const uint8_t x[64]);
+
 /* flag bits (include/hsv.h) */
 enum { STRICT_OK = 1, EQ_OK = 2, PARSE_OK = 4, SMALL_A = 8, SMALL_R = 16, S_OK = 32, A_OK = 64, R_OK = 128 };
 
@@ -541,7 +546,7 @@ uint8_t oracle_verify_flags(const uint8_t pk[32], const uint8_t sig[64], const u
   memcpy(buf + 64, msg, msg_len);
   sha512(hbuf, buf, 64 + msg_len);
   free(buf);
-  sc_reduce64(k, hbuf);
+  oracle_sc_reduce64_fast(k, hbuf); /* Barrett; equal to the bit-serial sc_reduce64 (tests/test_oracle.py) */
   ge negA = A;
   fe_neg(&negA.X, &A.X);
   fe_neg(&negA.T, &A.T);
@@ -635,4 +640,305 @@ int oracle_verify_tx_many(const uint8_t *txs, const uint64_t *offsets, size_t tx
   }
   for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
   return 0;
+}
+
+/* ===================================================================== */
+/* Fast mod-l arithmetic (Barrett, HAC 14.42 with b = 2^64, k = 4).       */
+/* Cross-checked against the bit-serial sc_reduce64 in tests/test_oracle.  */
+static const uint64_t L64[4] = {0x5812631a5cf5d3edull, 0x14def9dea2f79cd6ull, 0ull, 0x1000000000000000ull};
+static const uint64_t MU64[5] = {0xed9ce5a30a2c131bull, 0x2106215d086329a7ull, 0xffffffffffffffebull,
+                                 0xffffffffffffffffull, 0xfull};  /* floor(2^512 / l) */
+
+static int geq_l(const uint64_t r[5]) {
+  if (r[4]) return 1;
+  for (int i = 3; i >= 0; --i) {
+    if (r[i] > L64[i]) return 1;
+    if (r[i] < L64[i]) return 0;
+  }
+  return 1;
+}
+
+/* x: 8 little-endian u64 limbs (< 2^512) -> x mod l in 4 limbs */
+static void sc_barrett(uint64_t out[4], const uint64_t x[8]) {
+  uint64_t q2[10] = {0};
+  /* q2 = (x >> 192) * mu, only limbs >= 5 are needed but compute all */
+  for (int i = 0; i < 5; ++i) {
+    u128 c = 0;
+    const uint64_t xi = x[3 + i];
+    for (int j = 0; j < 5; ++j) {
+      c += (u128)xi * MU64[j] + q2[i + j];
+      q2[i + j] = (uint64_t)c;
+      c >>= 64;
+    }
+    q2[i + 5] = (uint64_t)c;
+  }
+  const uint64_t *q3 = q2 + 5; /* q2 >> 320 */
+  /* r2 = (q3 * l) mod 2^320 */
+  uint64_t r2[5] = {0};
+  for (int i = 0; i < 5; ++i) {
+    u128 c = 0;
+    for (int j = 0; i + j < 5 && j < 4; ++j) {
+      c += (u128)q3[i] * L64[j] + r2[i + j];
+      r2[i + j] = (uint64_t)c;
+      c >>= 64;
+    }
+    if (i + 4 < 5) r2[i + 4] += (uint64_t)c;
+  }
+  /* r = (x mod 2^320) - r2 mod 2^320 */
+  uint64_t r[5];
+  u128 borrow = 0;
+  for (int i = 0; i < 5; ++i) {
+    const u128 t = (u128)x[i] - r2[i] - borrow;
+    r[i] = (uint64_t)t;
+    borrow = (t >> 64) ? 1 : 0;
+  }
+  while (geq_l(r)) {
+    u128 b = 0;
+    for (int i = 0; i < 5; ++i) {
+      const u128 t = (u128)r[i] - (i < 4 ? L64[i] : 0) - b;
+      r[i] = (uint64_t)t;
+      b = (t >> 64) ? 1 : 0;
+    }
+  }
+  memcpy(out, r, 32);
+}
+
+static void sc_from_bytes64(uint64_t out[8], const uint8_t x[64]) {
+  for (int i = 0; i < 8; ++i) out[i] = load64(x + 8 * i);
+}
+
+static void sc_to_bytes(uint8_t out[32], const uint64_t s[4]) {
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 8; ++j) out[8 * i + j] = (uint8_t)(s[i] >> (8 * j));
+}
+
+static void sc_load(uint64_t s[4], const uint8_t b[32]) {
+  for (int i = 0; i < 4; ++i) s[i] = load64(b + 8 * i);
+}
+
+/* (a * b) mod l for a, b < 2^256 */
+static void sc_mul(uint64_t out[4], const uint64_t a[4], const uint64_t b[4]) {
+  uint64_t p[8] = {0};
+  for (int i = 0; i < 4; ++i) {
+    u128 c = 0;
+    for (int j = 0; j < 4; ++j) {
+      c += (u128)a[i] * b[j] + p[i + j];
+      p[i + j] = (uint64_t)c;
+      c >>= 64;
+    }
+    p[i + 4] = (uint64_t)c;
+  }
+  sc_barrett(out, p);
+}
+
+/* (a + b) mod l for a, b < l */
+static void sc_add(uint64_t out[4], const uint64_t a[4], const uint64_t b[4]) {
+  uint64_t x[8] = {0};
+  u128 c = 0;
+  for (int i = 0; i < 4; ++i) {
+    c += (u128)a[i] + b[i];
+    x[i] = (uint64_t)c;
+    c >>= 64;
+  }
+  x[4] = (uint64_t)c;
+  sc_barrett(out, x);
+}
+
+/* exported for the cross-check test: both reductions of 64 bytes */
+void oracle_sc_reduce64_fast(uint8_t out[32], const uint8_t x[64]) {
+  uint64_t w[8], r[4];
+  sc_from_bytes64(w, x);
+  sc_barrett(r, w);
+  sc_to_bytes(out, r);
+}
+
+void oracle_sc_reduce64_slow(uint8_t out[32], const uint8_t x[64]) { sc_reduce64(out, x); }
+
+/* ===================================================================== */
+/* ed25519-dalek 1.0.1 verify_batch (feature "batch"), the QC path of the  */
+/* reference (crypto/src/lib.rs:210-223 -> dalek::verify_batch):           */
+/*   parse every s (check_scalar) and A (PublicKey::from_bytes),           */
+/*   k_i = SHA-512(R_i || A_i || M) mod l, random 128-bit z_i,             */
+/*   [-sum z_i s_i]B + sum [z_i]R_i + sum [z_i k_i]A_i == O  (one MSM of   */
+/*   2n+1 points; R_i decompressed inside the MSM's point list),           */
+/*   curve25519-dalek 3.x VartimeMultiscalarMul: Straus with width-5 NAF   */
+/*   tables below 190 points, Pippenger (w = 6/7/8 by size) above.         */
+/* dalek draws z_i from a merlin transcript finalised with thread_rng; the */
+/* port draws them from a seeded splitmix64 (same cost class, the verdict  */
+/* differs only for pure-torsion failures).           */
+
+static uint64_t splitmix64(uint64_t *s) {
+  uint64_t z = (*s += 0x9e3779b97f4a7c15ull);
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+/* Scalar::to_radix_2w (w in 5..8): signed digits in [-2^(w-1), 2^(w-1)) */
+static int to_radix_2w(int16_t *digits, const uint64_t s[4], int w) {
+  const uint64_t radix = 1ull << w, mask = radix - 1;
+  const int count = (256 + w - 1) / w;
+  uint64_t carry = 0;
+  for (int i = 0; i < count; ++i) {
+    const int bit_offset = i * w, u = bit_offset / 64, b = bit_offset % 64;
+    uint64_t buf;
+    if (b < 64 - w || u == 3) buf = s[u] >> b;
+    else buf = (s[u] >> b) | (s[u + 1] << (64 - b));
+    const uint64_t coef = carry + (buf & mask);
+    carry = (coef + radix / 2) >> w;
+    digits[i] = (int16_t)((int64_t)coef - (int64_t)(carry << w));
+  }
+  if (w == 8) {
+    digits[count] = (int16_t)carry;
+    return count + 1;
+  }
+  digits[count - 1] = (int16_t)(digits[count - 1] + (int16_t)(carry << w));
+  return count;
+}
+
+static void ge_add_ext(ge *r, const ge *p, const ge *q) {
+  ge_cached c;
+  ge_to_cached(&c, q);
+  ge_add(r, p, &c);
+}
+
+/* Straus: NAF width 5, tables [1,3,...,15]P per point */
+static void msm_straus(ge *out, const uint64_t (*sc)[4], const ge *pts, size_t m) {
+  int8_t(*nafs)[256] = malloc(m * sizeof *nafs);
+  ge_cached(*tabs)[8] = malloc(m * sizeof *tabs);
+  for (size_t i = 0; i < m; ++i) {
+    uint8_t b[32];
+    sc_to_bytes(b, sc[i]);
+    naf(nafs[i], b, 5);
+    ge p2, acc = pts[i];
+    ge_cached c2;
+    ge_dbl(&p2, &pts[i]);
+    ge_to_cached(&c2, &p2);
+    for (int k = 0; k < 8; ++k) {
+      ge_to_cached(&tabs[i][k], &acc);
+      ge_add(&acc, &acc, &c2);
+    }
+  }
+  ge r;
+  ge_identity(&r);
+  for (int bit = 255; bit >= 0; --bit) {
+    ge_dbl(&r, &r);
+    for (size_t i = 0; i < m; ++i) {
+      const int d = nafs[i][bit];
+      if (d > 0) ge_add(&r, &r, &tabs[i][d / 2]);
+      else if (d < 0) ge_sub(&r, &r, &tabs[i][-d / 2]);
+    }
+  }
+  *out = r;
+  free(nafs);
+  free(tabs);
+}
+
+/* Pippenger: signed radix-2^w digits, 2^(w-1) buckets per column */
+static void msm_pippenger(ge *out, const uint64_t (*sc)[4], const ge *pts, size_t m) {
+  const int w = m < 500 ? 6 : (m < 800 ? 7 : 8);
+  const int nb = 1 << (w - 1);
+  int16_t(*digits)[64] = malloc(m * sizeof *digits);
+  ge_cached *pc = malloc(m * sizeof *pc);
+  int count = 0;
+  for (size_t i = 0; i < m; ++i) {
+    count = to_radix_2w(digits[i], sc[i], w);
+    ge_to_cached(&pc[i], &pts[i]);
+  }
+  ge *buckets = malloc((size_t)nb * sizeof *buckets);
+  ge total;
+  ge_identity(&total);
+  for (int col = count - 1; col >= 0; --col) {
+    for (int b = 0; b < nb; ++b) ge_identity(&buckets[b]);
+    for (size_t i = 0; i < m; ++i) {
+      const int d = digits[i][col];
+      if (d > 0) ge_add(&buckets[d - 1], &buckets[d - 1], &pc[i]);
+      else if (d < 0) ge_sub(&buckets[-d - 1], &buckets[-d - 1], &pc[i]);
+    }
+    ge inter = buckets[nb - 1], sum = buckets[nb - 1];
+    for (int b = nb - 2; b >= 0; --b) {
+      ge_add_ext(&inter, &inter, &buckets[b]);
+      ge_add_ext(&sum, &sum, &inter);
+    }
+    if (col == count - 1) {
+      total = sum;
+    } else {
+      for (int k = 0; k < w; ++k) ge_dbl(&total, &total);
+      ge_add_ext(&total, &total, &sum);
+    }
+  }
+  *out = total;
+  free(buckets);
+  free(digits);
+  free(pc);
+}
+
+/* 1 = Ok, 0 = Err, for crypto::Signature::verify_batch(digest, votes) */
+int oracle_verify_batch_dalek(const uint8_t digest[32], const uint8_t *pk, const uint8_t *sig, size_t n,
+                              uint64_t seed) {
+  pthread_once(&g_once, init_consts);
+  if (n == 0) return 1;
+  const size_t m = 2 * n + 1;
+  uint64_t(*sc)[4] = malloc(m * sizeof *sc);
+  ge *pts = malloc(m * sizeof *pts);
+  int ok = 1;
+  uint64_t bcoef[4] = {0, 0, 0, 0};
+  uint64_t rng = seed;
+  for (size_t i = 0; i < n && ok; ++i) {
+    const uint8_t *p = pk + 32 * i, *s = sig + 64 * i;
+    if (!sc_canonical(s + 32)) { ok = 0; break; }          /* InternalSignature::try_from */
+    if (!ge_decompress(&pts[1 + n + i], p)) { ok = 0; break; } /* PublicKey::from_bytes (glue) */
+    if (!ge_decompress(&pts[1 + i], s)) { ok = 0; break; }     /* R inside the MSM point list */
+    uint8_t buf[96], h[64];
+    memcpy(buf, s, 32);
+    memcpy(buf + 32, p, 32);
+    memcpy(buf + 64, digest, 32);
+    sha512(h, buf, 96);
+    uint64_t hw[8], k[4], sv[4], z[4] = {0, 0, 0, 0}, t[4];
+    sc_from_bytes64(hw, h);
+    sc_barrett(k, hw);                                       /* Scalar::from_hash */
+    sc_load(sv, s + 32);
+    z[0] = splitmix64(&rng);
+    z[1] = splitmix64(&rng);
+    memcpy(sc[1 + i], z, 32);                                /* z_i R_i */
+    sc_mul(sc[1 + n + i], z, k);                             /* z_i k_i A_i */
+    sc_mul(t, z, sv);
+    sc_add(bcoef, bcoef, t);                                 /* sum z_i s_i */
+  }
+  if (ok) {
+    /* -B_coefficient */
+    uint64_t zero[4] = {0, 0, 0, 0}, negb[4];
+    if (memcmp(bcoef, zero, 32) == 0) {
+      memset(negb, 0, 32);
+    } else {
+      u128 b = 0;
+      for (int i = 0; i < 4; ++i) {
+        const u128 t = (u128)L64[i] - bcoef[i] - b;
+        negb[i] = (uint64_t)t;
+        b = (t >> 64) ? 1 : 0;
+      }
+    }
+    memcpy(sc[0], negb, 32);
+    uint8_t by[32];
+    memset(by, 0x66, 32);
+    by[0] = 0x58;
+    ge_decompress(&pts[0], by);
+    ge r;
+    if (m < 190) msm_straus(&r, (const uint64_t(*)[4])sc, pts, m);
+    else msm_pippenger(&r, (const uint64_t(*)[4])sc, pts, m);
+    ok = ge_is_identity(&r);
+  }
+  free(sc);
+  free(pts);
+  return ok;
+}
+
+/* consensus TC::verify's signature loop (consensus/src/messages.rs:307-313):
+ * Signature::verify per vote over its own digest, in order, stopping at the
+ * first failure.  1 = all Ok. */
+int oracle_tc_verify(const uint8_t *pk, const uint8_t *sig, const uint8_t *digests, size_t n) {
+  pthread_once(&g_once, init_consts);
+  for (size_t i = 0; i < n; ++i)
+    if (!(oracle_verify_flags(pk + 32 * i, sig + 64 * i, digests + 32 * i, 32) & STRICT_OK)) return 0;
+  return 1;
 }

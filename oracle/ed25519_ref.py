@@ -397,9 +397,10 @@ def chacha20_block(key: bytes, counter: int, nonce8: bytes = b"\x00" * 8) -> byt
 def reference_key_seeds(seed: bytes = b"\x00" * 32, count: int = 4) -> List[bytes]:
     """Secret seeds of the reference ``keys()`` fixture (crypto/src/tests/crypto_tests.rs:26-29).
 
-    ``StdRng::from_seed(seed)`` in rand 0.7 is ChaCha20; dalek ``SecretKey::generate``
-    fills 32 bytes from it, so seed i is keystream bytes [32i, 32i+32).  This recipe is
-    unpinned (no Rust toolchain to confirm), and nothing depends on it matching exactly.
+    ``StdRng::from_seed(seed)`` in rand 0.7.3 (crypto/Cargo.toml:12) is rand_chacha 0.2's
+    ChaCha20Rng (key = seed, counter and nonce zero); dalek ``SecretKey::generate`` fills
+    32 bytes from it, so seed i is keystream bytes [32i, 32i+32).  The block function is
+    pinned by the RFC 7539 test vectors (tests/test_oracle.py::test_chacha20_block_rfc7539).
     """
     need = 32 * count
     stream = b""

@@ -244,7 +244,7 @@ def main():
         assert got == v["expect_ok"], name
     with open(os.path.join(HERE, "reference_fixtures.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py",
-                   "key_recipe": "StdRng::from_seed([0;32]) = ChaCha20 keystream, 32 B per key (unpinned)",
+                   "key_recipe": "StdRng::from_seed([0;32]) (rand 0.7.3 = rand_chacha 0.2 ChaCha20Rng) keystream, 32 B per key; ChaCha20 block pinned by RFC 7539 A.1/2.3.2 (tests/test_oracle.py)",
                    "qc_digest": qd.hex(), "fixtures": fx}, f, indent=1)
     print("reference fixtures:", len(fx), "qc digest", qd.hex())
 

@@ -125,8 +125,9 @@ def test_auto_committee_behind_verify_batch(mods):
         d = bytes(w.msg)
         assert lib.hsv_verify_batch_packed(d, packed, w.n) == 1
         assert lib.hsv_auto_committee_size() == 0          # seen once: no cache yet
-        assert lib.hsv_verify_batch_packed(d, packed, w.n) == 1
-        assert lib.hsv_auto_committee_size() == w.n        # recurring keys: cache built
+        assert lib.hsv_verify_batch_packed(d, packed, w.n) == 1   # recurring keys: build queued
+        assert lib.hsv_auto_committee_wait(30000) == 1     # built in the background, never on the call
+        assert lib.hsv_auto_committee_size() == w.n
         for pos in (40, 70):                               # corrupted s / R through the cache
             bad = bytearray(packed)
             bad[96 * 5 + pos] ^= 1
@@ -146,12 +147,14 @@ def test_auto_committee_behind_verify_batch(mods):
         for _ in range(3):
             assert crypto.Signature.verify_batch(digest, votes).is_ok()
             assert crypto.Signature.verify_batch(digest, votes[:2] + [(keys[2][0], crypto.Signature.default())]).is_err()
+        assert lib.hsv_auto_committee_wait(30000) == 1
         assert lib.hsv_auto_committee_size() >= 3
         # strict verification of cached keys (Vote::verify, TC-style per-vote digests) takes the
         # committee kernels: flags equal the generic path's on every corruption kind
         from hsverify import verifier
         for _ in range(2):   # make sure all 67 committee keys are cached
             assert lib.hsv_verify_batch_packed(d, packed, w.n) == 1
+        assert lib.hsv_auto_committee_wait(30000) == 1
         t = synth.tc_votes(100, seed=41, corrupt_frac=0.3)     # the same 67 committee keys
         keep = t.kind != synth.CORRUPTIONS.index("small_order_A")  # that kind swaps the key out
         pk, sg, mg = t.pk[keep], t.sig[keep], t.msg[keep]
@@ -163,6 +166,7 @@ def test_auto_committee_behind_verify_batch(mods):
         assert (cached == generic).all() and not (generic[~t.honest[keep]] & o.STRICT_OK).any()
         for _ in range(2):   # repopulate the cache with the QC keys, then single strict verifies
             assert lib.hsv_verify_batch_packed(d, packed, w.n) == 1
+        assert lib.hsv_auto_committee_wait(30000) == 1
         assert lib.hsv_auto_committee_size() >= w.n
         assert lib.hsv_verify_strict(d, bytes(w.pk[3]), bytes(w.sig[3])) == 1
         s_bad = bytearray(w.sig[3]); s_bad[10] ^= 4

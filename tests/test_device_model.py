@@ -1,0 +1,163 @@
+"""The boundary's device model (include/hsv.h, hsv_init) on the GPU.
+
+* hsv_init(d) binds host-buffer calls to device d; hsv_init(-1) selects every
+  device (large host batches sharded by contiguous range).
+* The multi-device shard / thread / gather path of run_host runs with
+  virtual shards mapped onto the one GPU of the box (hsv_set_virtual_shards),
+  compared with the unsharded result and the C oracle.
+* Slot pools: concurrent host calls from many threads stay exact.
+* Committees survive hsv_shutdown (the B table is rebuilt on use); the
+  automatic cache ignores batches above its 8192-key capacity.
+The reference runs several nodes per process on a multi-thread runtime
+(node/src/main.rs:16, consensus/src/tests/consensus_tests.rs:10-56), which is
+what the binding and the slot pools serve.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+import ed25519_ref as o
+from conftest import oracle_flags
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mods(hsv):
+    from hsverify import _lib, committee, synth, verifier
+    return _lib, committee, synth, verifier
+
+
+def test_init_binds_and_reports_device(mods, hsv):
+    _lib, _, synth, verifier = mods
+    ndev = hsv.hsv_device_count()
+    try:
+        assert verifier.bind_device(0) == 1
+        assert hsv.hsv_bound_device() == 0
+        w = synth.qc_votes(100, seed=12)
+        assert (verifier.verify_flags(w.pk, w.sig, w.msg) & o.STRICT_OK).all()
+        assert hsv.hsv_init(ndev) < 0                      # out of range: an error, binding unchanged
+        assert hsv.hsv_bound_device() == 0
+        assert hsv.hsv_init(-2) < 0
+        assert verifier.bind_device(-1) == ndev
+        assert hsv.hsv_bound_device() == -1
+        assert (verifier.verify_flags(w.pk, w.sig, w.msg) & o.STRICT_OK).all()
+    finally:
+        hsv.hsv_init(-1)
+
+
+@pytest.mark.parametrize("shards", [2, 3, 5])
+def test_virtual_shards_gather_matches_unsharded_and_oracle(mods, oracle_lib, shards):
+    """run_host's multi-device path: contiguous shards, one host thread and
+    slot each, flags written into the caller's buffer at the shard offsets."""
+    _, _, synth, verifier = mods
+    n = (1 << 16) + 12345
+    w = synth.independent_triples(n, seed=500 + shards, corrupt_frac=0.05)
+    verifier.set_virtual_shards(0)
+    whole = verifier.verify_flags(w.pk, w.sig, w.msg)
+    try:
+        verifier.set_virtual_shards(shards)
+        sharded = verifier.verify_flags(w.pk, w.sig, w.msg)
+    finally:
+        verifier.set_virtual_shards(0)
+    assert (sharded == whole).all()
+    assert (whole[w.honest] & o.STRICT_OK).all() and not (whole[~w.honest] & o.STRICT_OK).any()
+    # oracle sample around every shard boundary
+    cuts = [n * d // shards for d in range(1, shards)]
+    idx = np.unique(np.concatenate([np.arange(max(0, c - 40), min(n, c + 40)) for c in cuts] + [np.arange(64)]))
+    assert (sharded[idx] == oracle_flags(oracle_lib, w.pk[idx], w.sig[idx], w.msg[idx])).all()
+
+
+def test_virtual_shards_transactions(mods, oracle_lib):
+    from hsverify import mempool
+    _, _, synth, verifier = mods
+    n = (1 << 16) + 77
+    w = synth.transactions(n, tx_size=200, seed=31)
+    whole = mempool.verify_transactions_fixed(w.txs)
+    try:
+        verifier.set_virtual_shards(4)
+        sharded = mempool.verify_transactions_fixed(w.txs)
+    finally:
+        verifier.set_virtual_shards(0)
+    assert (sharded == whole).all()
+    assert (whole[w.honest] & o.STRICT_OK).all() and not (whole[~w.honest] & o.STRICT_OK).any()
+
+
+def test_many_concurrent_small_calls(mods, golden):
+    """More threads than slots: QC-sized and single-vote calls interleave."""
+    _, _, _, verifier = mods
+    errors = []
+
+    def work(k):
+        try:
+            rng = np.random.default_rng(k)
+            for _ in range(6):
+                m = int(rng.integers(1, 700))
+                sl = rng.integers(0, len(golden["flags"]), m)
+                got = verifier.verify_flags(golden["pk"][sl], golden["sig"][sl], golden["msg"][sl])
+                if not (got == golden["flags"][sl]).all():
+                    errors.append(k)
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(12)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors
+
+
+def test_committee_survives_shutdown(mods, hsv, golden):
+    _, committee, _, _ = mods
+    keys = golden["pk"][:8]
+    with committee.Committee(keys) as c:
+        hsv.hsv_shutdown()                       # frees the B tables and staging slots
+        got = c.verify_flags(np.arange(8, dtype=np.uint32), golden["sig"][:8], golden["msg"][:8])
+        assert (got == golden["flags"][:8]).all()
+
+
+def test_auto_cache_ignores_batches_above_capacity(mods, hsv):
+    """A recurring 8193-vote batch is never cached (the cache holds 8192 keys at
+    most) and its verdict is the generic one."""
+    _, _, synth, verifier = mods
+    hsv.hsv_set_auto_committee(0)
+    hsv.hsv_set_auto_committee(1)
+    try:
+        n = 8193
+        seeds = synth.committee_seeds(n, 3)
+        digest = np.frombuffer(bytes(range(32)), np.uint8)
+        pk, sig = verifier.sign_many(seeds, np.repeat(digest[None], n, 0))
+        packed = np.concatenate([pk, sig], 1).tobytes()
+        for _ in range(3):
+            assert hsv.hsv_verify_batch_packed(bytes(digest), packed, n) == 1
+        assert hsv.hsv_auto_committee_wait(30000) == 1
+        assert hsv.hsv_auto_committee_size() == 0
+        bad = bytearray(packed)
+        bad[96 * 4000 + 40] ^= 1
+        assert hsv.hsv_verify_batch_packed(bytes(digest), bytes(bad), n) == 0
+    finally:
+        hsv.hsv_set_auto_committee(0)
+        hsv.hsv_set_auto_committee(1)
+
+
+def test_auto_cache_counts_a_key_once_per_batch(mods, hsv):
+    """A key repeated inside one batch (a duplicated vote) is not 'recurring'."""
+    _, _, synth, _ = mods
+    hsv.hsv_set_auto_committee(0)
+    hsv.hsv_set_auto_committee(1)
+    try:
+        w = synth.qc_votes(4, seed=77)
+        votes = np.concatenate([w.pk, w.sig], 1)
+        dup = np.concatenate([votes, votes], 0).tobytes()   # every key twice in one batch
+        assert hsv.hsv_verify_batch_packed(bytes(w.msg), dup, 2 * w.n) == 1
+        assert hsv.hsv_auto_committee_wait(30000) == 1
+        assert hsv.hsv_auto_committee_size() == 0
+        assert hsv.hsv_verify_batch_packed(bytes(w.msg), dup, 2 * w.n) == 1   # second batch: now recurring
+        assert hsv.hsv_auto_committee_wait(30000) == 1
+        assert hsv.hsv_auto_committee_size() == w.n
+        assert hsv.hsv_verify_batch_packed(bytes(w.msg), dup, 2 * w.n) == 1   # through the cache
+    finally:
+        hsv.hsv_set_auto_committee(0)
+        hsv.hsv_set_auto_committee(1)

@@ -28,7 +28,7 @@ def test_golden_every_variant(api, golden):
     _, verifier, _ = api
     default = verifier.get_variant()
     try:
-        for v in range(verifier.num_variants()):
+        for v in verifier.variants():
             verifier.set_variant(v)
             got = verifier.verify_flags(golden["pk"], golden["sig"], golden["msg"])
             bad = np.nonzero(got != golden["flags"])[0]
@@ -44,7 +44,7 @@ def test_lattice_fallback_records_every_variant(api, fallback_records):
     fb = fallback_records
     default = verifier.get_variant()
     try:
-        for v in range(verifier.num_variants()):
+        for v in verifier.variants():
             verifier.set_variant(v)
             got = verifier.verify_flags(fb["pk"], fb["sig"], fb["msg"])
             assert (got == fb["flags"]).all(), (v, np.nonzero(got != fb["flags"])[0][:8])
@@ -307,33 +307,3 @@ def test_host_api_pipelined_chunks_match_device_api(api, oracle_lib):
     assert (got[w.honest] & o.STRICT_OK).all() and not (got[~w.honest] & o.STRICT_OK).any()
     sample = np.sort(np.random.default_rng(3).choice(n, 4096, replace=False))
     assert (got[sample] == oracle_flags(oracle_lib, w.pk[sample], w.sig[sample], w.msg[sample])).all()
-
-
-def test_pair_tail_variant_matches_default_at_scale(api, oracle_lib):
-    """Variant 22 runs the last ~one round of a large batch as pair-lane batches
-    (hsv_verify_hpt_kernel); it only engages above ~2 x 98k items, so compare it
-    with the default kernel at 3 x 10^5 items: flags and STRICT_OK bits equal."""
-    import torch
-    _, verifier, synth = api
-    n = 300_007
-    w = synth.independent_triples(n, seed=88, corrupt_frac=0.05)
-    dev = torch.device("cuda:0")
-    pk, sig, msg = (torch.from_numpy(a).to(dev) for a in (w.pk, w.sig, w.msg))
-    out = {}
-    default = verifier.get_variant()
-    try:
-        for v in (default, 22):
-            verifier.set_variant(v)
-            flags = torch.zeros(n, dtype=torch.uint8, device=dev)
-            bits = torch.zeros((n + 31) // 32, dtype=torch.int32, device=dev)
-            verifier.verify_device(pk, sig, msg, flags, bits)
-            torch.cuda.synchronize()
-            out[v] = (flags.cpu().numpy(), bits.cpu().numpy())
-    finally:
-        verifier.set_variant(default)
-    assert (out[default][0] == out[22][0]).all() and (out[default][1] == out[22][1]).all()
-    f = out[22][0]
-    assert (f[w.honest] & o.STRICT_OK).all() and not (f[~w.honest] & o.STRICT_OK).any()
-    tail = np.arange(n - 100_000, n)
-    sample = np.sort(np.random.default_rng(4).choice(tail, 2048, replace=False))
-    assert (f[sample] == oracle_flags(oracle_lib, w.pk[sample], w.sig[sample], w.msg[sample])).all()

@@ -86,7 +86,7 @@ def test_tx_golden_every_variant(hsv, tx_golden):
     from hsverify import mempool, verifier
     default = verifier.get_variant()
     try:
-        for v in range(verifier.num_variants()):
+        for v in verifier.variants():
             verifier.set_variant(v)
             got = mempool.verify_transactions(tx_golden["txs"])
             assert (got == tx_golden["flags"]).all(), (v, np.nonzero(got != tx_golden["flags"])[0][:8])

@@ -151,3 +151,95 @@ def test_c_oracle_reproduces_fallback_records(fallback_records, oracle_lib):
     got = oracle_flags(oracle_lib, fb["pk"], fb["sig"], fb["msg"])
     assert (got == fb["flags"]).all()
     assert (fb["flags"][0::4] & o.STRICT_OK).all()
+
+
+# ---- the reference's keys() fixture recipe (crypto/src/tests/crypto_tests.rs:26-29) ----
+# rand 0.7.3 (crypto/Cargo.toml:12) StdRng = rand_chacha 0.2 ChaCha20Rng: key =
+# the 32-byte seed, 64-bit counter and nonce starting at zero, keystream consumed
+# in order by dalek's SecretKey::generate (fill_bytes).  The block function is
+# pinned by the published RFC 7539 vectors (A.1 #1/#2: zero key, counters 0/1;
+# 2.3.2: key 00..1f, nonce 000000090000004a00000000, counter 1 in the
+# 32-bit-counter layout = the djb layout with the first nonce word in the high
+# counter half).
+@pytest.mark.parametrize("key,counter,nonce8,block", [
+    (bytes(32), 0, bytes(8),
+     "76b8e0ada0f13d90405d6ae55386bd28bdd219b8a08ded1aa836efcc8b770dc7"
+     "da41597c5157488d7724e03fb8d84a376a43b8f41518a11cc387b669b2ee6586"),
+    (bytes(32), 1, bytes(8),
+     "9f07e7be5551387a98ba977c732d080dcb0f29a048e3656912c6533e32ee7aed"
+     "29b721769ce64e43d57133b074d839d531ed1f28510afb45ace10a1f4b794d6f"),
+    (bytes(range(32)), 1 + (0x09000000 << 32), bytes.fromhex("0000004a00000000"),
+     "10f1e7e4d13b5915500fdd1fa32071c4c7d1f4c733c068030422aa9ac3d46c4e"
+     "d2826446079faa0914c2d705d98b02a2b5129cd1de164eb9cbd083e8a2503c4e"),
+])
+def test_chacha20_block_rfc7539(key, counter, nonce8, block):
+    assert o.chacha20_block(key, counter, nonce8).hex() == block
+
+
+def test_reference_key_seeds_are_the_zero_key_keystream():
+    seeds = o.reference_key_seeds()
+    assert seeds[0].hex() == "76b8e0ada0f13d90405d6ae55386bd28bdd219b8a08ded1aa836efcc8b770dc7"
+    assert b"".join(seeds) == o.chacha20_block(bytes(32), 0) + o.chacha20_block(bytes(32), 1)
+
+
+def test_reference_fixture_recipe_is_pinned(reference_fixtures):
+    assert "unpinned" not in reference_fixtures["key_recipe"]
+    pks = {bytes.fromhex(v["pk"]) for v in reference_fixtures["fixtures"].values() if v.get("pk")}
+    want = {o.public_key(s) for s in o.reference_key_seeds()}
+    assert pks and pks <= want
+
+
+# ---- fast mod-l reduction used by the C port (Barrett) vs the bit-serial one ----
+def test_fast_scalar_reduction_matches_bit_serial(oracle_lib):
+    fast, slow = oracle_lib.oracle_sc_reduce64_fast, oracle_lib.oracle_sc_reduce64_slow
+    rng = random.Random(7)
+    cases = [bytes(64), b"\xff" * 64, o.L.to_bytes(64, "little"), (o.L - 1).to_bytes(64, "little"),
+             (o.L * o.L).to_bytes(64, "little"), ((1 << 512) - o.L).to_bytes(64, "little")]
+    cases += [rng.getrandbits(512).to_bytes(64, "little") for _ in range(3000)]
+    a, b = ctypes.create_string_buffer(32), ctypes.create_string_buffer(32)
+    for i, x in enumerate(cases):
+        fast(a, x)
+        assert int.from_bytes(a.raw, "little") == int.from_bytes(x, "little") % o.L
+        if i < 300:
+            slow(b, x)
+            assert a.raw == b.raw
+
+
+# ---- C port of ed25519-dalek verify_batch (the QC CPU baseline) ------------------
+def _batch_port(oracle_lib):
+    f = oracle_lib.oracle_verify_batch_dalek
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64]
+    return f
+
+
+@pytest.mark.parametrize("committee", [4, 100, 400])   # 3 / 67 / 267 votes: Straus and Pippenger w=6
+def test_dalek_batch_port_verdicts(oracle_lib, committee):
+    from hsverify import synth
+    f = _batch_port(oracle_lib)
+    w = synth.qc_votes(committee, seed=committee)
+    pk, sig = np.ascontiguousarray(w.pk), np.ascontiguousarray(w.sig)
+    for seed in (1, 2):
+        assert f(bytes(w.msg), pk.ctypes.data, sig.ctypes.data, w.n, seed) == 1
+    for pos in (0, 40, 63):          # R, s and the top byte of s
+        bad = sig.copy()
+        bad[w.n // 2, pos] ^= 2
+        assert f(bytes(w.msg), pk.ctypes.data, bad.ctypes.data, w.n, 3) == 0
+    other = bytearray(w.msg)
+    other[0] ^= 1
+    assert f(bytes(other), pk.ctypes.data, sig.ctypes.data, w.n, 4) == 0
+    assert f(bytes(w.msg), pk.ctypes.data, sig.ctypes.data, 0, 5) == 1
+
+
+def test_dalek_batch_port_agrees_with_deterministic_rule(oracle_lib):
+    """Corrupted QCs over every corruption kind (C3 shape at n = 1000, 667
+    votes: Pippenger w = 8): the port's verdict equals the build's rule
+    (all PARSE_OK and EQ_OK) whenever no failure is pure torsion."""
+    from hsverify import synth
+    f = _batch_port(oracle_lib)
+    for frac, seed in ((0.0, 11), (0.005, 12), (0.05, 13)):
+        w = synth.qc_votes(1000, seed=seed, corrupt_frac=frac)
+        pk, sig = np.ascontiguousarray(w.pk), np.ascontiguousarray(w.sig)
+        flags = oracle_flags(oracle_lib, pk, sig, w.msg)
+        rule = int(((flags & (o.PARSE_OK | o.EQ_OK)) == (o.PARSE_OK | o.EQ_OK)).all())
+        assert f(bytes(w.msg), pk.ctypes.data, sig.ctypes.data, w.n, seed) == rule
