@@ -1,35 +1,47 @@
 #!/usr/bin/env python3
 """Benchmark: Ed25519 verifications/s at batch 2^20 per GPU (BASELINE.json metric).
 
-python bench.py [--gpus N] [--steps K] [--warmup W] [--n ITEMS_PER_GPU]
-For N > 1 the driver launches one process per GPU with torch.distributed.run;
-RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* come from the environment.
+python bench.py [--gpus N] [--steps K] [--warmup W] [--n ITEMS_PER_GPU] [--global-n ITEMS]
+
+One process per GPU.  Launched under torch.distributed.run (RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_* in the environment), every rank runs its shard.  Run
+directly with --gpus N > 1 and no WORLD_SIZE, this script starts
+`python -m torch.distributed.run --nproc-per-node N` itself (the parent never
+touches a GPU) and exits with its status; WORLD_SIZE != N is an error.
 
 Workload (config C4 / C5 shards): each rank holds n = 2^20 independent
 (public key, 32-byte digest, signature) triples in HBM, 5 % corrupted across
 the SURVEY 8(d) corruption kinds.  A step is one verification launch over the
 rank's whole batch (per-item flag bytes + packed STRICT_OK bits).  Shards are
 contiguous and independent: no collective touches the data path; the gloo
-group only carries the timing barrier and the max-over-ranks reduction.
+group only carries the timing barrier, the max-over-ranks reduction and the
+final bitmask gather.  --global-n 16777216 runs C5 (2^24 split over the ranks,
+strong scaling).  --dry-run exercises the launcher, sharding, timing and
+gather on CPU (gloo, no GPU, no verification) for tests/test_bench_launcher.py.
 
 Reported beside it:
-  roofline      int32-VALU bound; achieved = 192,000 u32 MACs per verification
-                (SURVEY 8(d) convention) x items per launch / mean launch time
-                from HIP events on the launch stream; peak = live
-                v_mad_u64_u32 probe on this GPU.
-  cpu_baseline  rank 0, N = 1 only: the C restatement of ed25519-dalek's
-                verify_strict (oracle/ed25519_oracle.c, "port") on host cores
-                over a bounded sample of the same workload.
-  qc_latency    p50/p99 of the host-buffer QC call (hsv_verify_batch_packed:
-                H2D + kernel + D2H) for 67 (n=100) and 667 (n=1000) votes.
-  mempool_tx    2^20 client transactions of 512 B (message || pk || sig,
-                mempool/src/batch_maker.rs:79-85) in HBM: tx/s of digest +
-                verification, with the C port beside it.
+  roofline         int32-VALU bound; achieved = 192,000 u32 MACs per verification
+                   (SURVEY 8(d) convention) x items per launch / mean launch time
+                   from HIP events on the launch stream; per rank with --global-n.
+  cpu_baseline     rank 0, N = 1 only: the C restatement of ed25519-dalek's
+                   verify_strict (oracle/ed25519_oracle.c, "port") on every host
+                   core this job may use, over the full C4 batch, flag-for-flag
+                   against the GPU; plus the batch way (verify_batch over chunks
+                   of 64, verify_strict for failing chunks).
+  qc_latency*      p50/p99 of the host-buffer QC call (C1/C2/C3), of one
+                   verify_strict, of the C3 QC from bincode, and of C3 with 5 %
+                   corrupted votes.
+  tc_latency       C3 TC (667 timeouts, per-vote digests) through the batched
+                   strict API and from bincode, 0 % and 5 % corrupted.
+  qc_cpu_baseline  one host core: the C port of dalek verify_batch (Straus /
+                   Pippenger MSM) for C1-C3 QCs and the sequential TC::verify loop.
+  mempool_tx       2^20 client transactions of 512 B in HBM.
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -45,7 +57,12 @@ IO_BYTES = 129               # algorithmic HBM bytes per verification (128 in + 
 # half the f32 rate on gfx950, profiles/r01e_ubench) x 2.4 GHz max clock
 # (MI355X_MICROARCH.md chip table) = 39.3 T MAC/s
 PEAK_MACS = 256 * 4 * 16 * 2.4e9
-PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "latest_pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "latest_pmc_traffic.json")
+ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "libhsv_oracle.so")
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
 
 
 def pmc_traffic(variant, n):
@@ -65,34 +82,22 @@ def pmc_traffic(variant, n):
     return 2 * t["fetch_bytes_per_launch"] + t["write_bytes_per_launch"], t.get("source")
 
 
-def log(*a):
-    print(*a, file=sys.stderr, flush=True)
+def host_cores():
+    """CPU threads this job may use: the affinity mask, capped by a cgroup v2
+    CPU quota (a GPU box grants each job a share of a larger machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(p)
+            n = min(n, max(1, int(quota)))
+    except (OSError, ValueError):
+        pass
+    return n, quota
 
 
-def cpu_baseline(w, gpu_flags, sample, threads):
-    """Time the C port of dalek's verify_strict on host cores (rank 0, N = 1)."""
-    so = os.path.join(ROOT, "oracle", "_build", "libhsv_oracle.so")
-    if not os.path.exists(so):
-        subprocess.run(["make", "-s"], cwd=os.path.join(ROOT, "oracle"), check=True)
-    lib = ctypes.CDLL(so)
-    lib.oracle_verify_many.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_size_t] * 2 + [ctypes.c_void_p, ctypes.c_int]
-    m = min(sample, w.n)
-    pk, sig, msg = (np.ascontiguousarray(a[:m]) for a in (w.pk, w.sig, w.msg))
-    out = np.zeros(m, np.uint8)
-    t0 = time.perf_counter()
-    lib.oracle_verify_many(pk.ctypes.data, sig.ctypes.data, msg.ctypes.data, 32, m, out.ctypes.data, threads)
-    dt = time.perf_counter() - t0
-    return {
-        "value": m / dt, "unit": "verif/s", "cores": threads, "kind": "port",
-        "sample": f"first {m} triples of the same C4 workload; oracle/ed25519_oracle.c "
-                  f"(C restatement of ed25519-dalek 1.0.1 verify_strict, radix-2^51, w-NAF), "
-                  f"{threads} threads, {dt:.2f} s wall",
-        "sample_parity_vs_gpu": bool((out == gpu_flags[:m]).all()),
-        "cpu_model": _cpu_model(),
-    }
-
-
-def _cpu_model():
+def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
@@ -102,62 +107,172 @@ def _cpu_model():
     return "unknown"
 
 
+def _oracle():
+    if not os.path.exists(ORACLE_SO):
+        subprocess.run(["make", "-s"], cwd=os.path.join(ROOT, "oracle"), check=True)
+    lib = ctypes.CDLL(ORACLE_SO)
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    lib.oracle_verify_many.argtypes = [vp, vp, vp, sz, sz, vp, ctypes.c_int]
+    lib.oracle_verify_many_batch64.restype = ctypes.c_uint64
+    lib.oracle_verify_many_batch64.argtypes = [vp, vp, vp, sz, vp, ctypes.c_int]
+    lib.oracle_verify_batch_dalek.argtypes = [ctypes.c_char_p, vp, vp, sz, ctypes.c_uint64]
+    lib.oracle_verify_batch.argtypes = [ctypes.c_char_p, vp, vp, sz]
+    lib.oracle_tc_verify.argtypes = [vp, vp, vp, sz]
+    lib.oracle_verify_flags.restype = ctypes.c_uint8
+    lib.oracle_verify_flags.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, sz]
+    lib.oracle_verify_tx_many.argtypes = [vp, vp, sz, sz, vp, ctypes.c_int]
+    return lib
+
+
+def cpu_baseline(w, gpu_flags, sample):
+    """C4 on the host cores: the C port of dalek's verify_strict per item (the
+    reference's Signature::verify, which gives the per-signature vector), and
+    the batch way (verify_batch over chunks of 64 + verify_strict for chunks
+    that fail).  Rank 0, N = 1 only, outside the timed region."""
+    lib = _oracle()
+    threads, quota = host_cores()
+    m = min(sample, w.n)
+    pk, sig, msg = (np.ascontiguousarray(a[:m]) for a in (w.pk, w.sig, w.msg))
+    out = np.zeros(m, np.uint8)
+    t0 = time.perf_counter()
+    lib.oracle_verify_many(pk.ctypes.data, sig.ctypes.data, msg.ctypes.data, 32, m, out.ctypes.data, threads)
+    dt = time.perf_counter() - t0
+    out64 = np.zeros(m, np.uint8)
+    t0 = time.perf_counter()
+    fb = lib.oracle_verify_many_batch64(pk.ctypes.data, sig.ctypes.data, msg.ctypes.data, m, out64.ctypes.data,
+                                        threads)
+    dt64 = time.perf_counter() - t0
+    return {
+        "value": m / dt, "unit": "verif/s", "cores": threads, "kind": "port",
+        "sample": f"first {m} triples of the same C4 workload (5 % corrupted); oracle/ed25519_oracle.c "
+                  f"(C restatement of ed25519-dalek 1.0.1 verify_strict: radix-2^51 field, width-5/8 NAF "
+                  f"double-scalar multiplication), {threads} threads, {dt:.2f} s wall",
+        "sample_parity_vs_gpu": bool((out == gpu_flags[:m]).all()),
+        "nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": quota,
+        "cpu_model": cpu_model(),
+        "batch64": {"value": m / dt64, "unit": "verif/s", "cores": threads,
+                    "algorithm": "dalek verify_batch (random linear combination, Straus MSM) over chunks of 64, "
+                                 "verify_strict per item for the chunks that fail",
+                    "failed_chunks": int(fb), "chunks": (m + 63) // 64,
+                    "strict_ok_parity_vs_gpu": bool(((out64 & 1) == (gpu_flags[:m] & 1)).all())},
+    }
+
+
+def _p(ts):
+    ts = np.array(ts) * 1e3
+    return {"p50_ms": float(np.percentile(ts, 50)), "p99_ms": float(np.percentile(ts, 99)), "reps": len(ts)}
+
+
+def _timed(fn, reps, warm=10):
+    for _ in range(warm):
+        fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return ts
+
+
+def member_corrupted(make, committee, seed, frac=0.05):
+    """A C3 certificate with `frac` corrupted votes whose keys all stay committee
+    members: the reference rejects a vote by a non-member before any signature
+    check (QC::verify / TC::verify stake lookups, consensus/src/messages.rs:186,296),
+    so the small_order_A kind (which swaps the key) is reverted to an honest vote."""
+    from hsverify import synth
+    w = make(committee, seed=seed, corrupt_frac=frac)
+    clean = make(committee, seed=seed)
+    swap = w.kind == synth.CORRUPTIONS.index("small_order_A")
+    w.pk[swap], w.sig[swap] = clean.pk[swap], clean.sig[swap]
+    w.honest[swap] = True
+    return w
+
+
+def tc_hqc(committee, seed, round_=1000):
+    quorum = 2 * committee // 3 + 1
+    return np.random.default_rng(seed + 29).integers(round_ - 10, round_, size=quorum)
+
+
 def qc_latency(reps, auto=True):
     """auto: the drop-in default, hsv_verify_batch_packed with its automatic
     committee cache in steady state (the same keys every round, as consensus
     has); auto=False: the generic kernels only."""
-    from hsverify import _lib, synth
+    from hsverify import _lib, synth, wire
+    import hashlib
     lib = _lib.load()
     lib.hsv_set_auto_committee(1 if auto else 0)
     res = {"automatic_committee_cache": bool(auto)}
+
+    def settle(fn):  # two sightings queue the keys; wait for the background build
+        for _ in range(3):
+            fn()
+        lib.hsv_auto_committee_wait(60000)
+
     for committee in (4, 100, 1000):
         w = synth.qc_votes(committee, seed=committee)
         packed = np.concatenate([w.pk, w.sig], axis=1).tobytes()
         digest = bytes(w.msg)
-        for _ in range(10):
-            assert lib.hsv_verify_batch_packed(digest, packed, w.n) == 1
-        ts = []
-        for _ in range(reps):
-            t0 = time.perf_counter()
-            rc = lib.hsv_verify_batch_packed(digest, packed, w.n)
-            ts.append(time.perf_counter() - t0)
-            assert rc == 1
-        ts = np.array(ts) * 1e3
-        res[f"n{committee}_votes{w.n}"] = {"p50_ms": float(np.percentile(ts, 50)),
-                                            "p99_ms": float(np.percentile(ts, 99)), "reps": reps}
+        call = lambda: lib.hsv_verify_batch_packed(digest, packed, w.n)
+        settle(call)
+        assert call() == 1
+        res[f"n{committee}_votes{w.n}"] = _p(_timed(call, reps))
+    # C3 with 5 % corrupted votes (member keys): Err, every flag computed
+    w = member_corrupted(synth.qc_votes, 1000, seed=1000)
+    packed = np.concatenate([w.pk, w.sig], axis=1).tobytes()
+    digest = bytes(w.msg)
+    call = lambda: lib.hsv_verify_batch_packed(digest, packed, w.n)
+    settle(call)
+    assert call() == 0
+    res["n1000_votes667_corrupt5pct"] = dict(_p(_timed(call, reps)), corrupted=int((~w.honest).sum()))
     # one strict verification (Vote::verify / Block::verify, consensus/src/messages.rs:136-146)
     w = synth.qc_votes(4, seed=4)
     pk0, sig0, d0 = bytes(w.pk[0]), bytes(w.sig[0]), bytes(w.msg)
-    for _ in range(10):
-        assert lib.hsv_verify_strict(d0, pk0, sig0) == 1
-    ts = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        rc = lib.hsv_verify_strict(d0, pk0, sig0)
-        ts.append(time.perf_counter() - t0)
-        assert rc == 1
-    ts = np.array(ts) * 1e3
-    res["single_verify_strict"] = {"p50_ms": float(np.percentile(ts, 50)), "p99_ms": float(np.percentile(ts, 99)),
-                                   "reps": reps}
-    # the same C3 QC handed over as its bincode wire bytes (hsv_qc_verify_bincode:
+    settle(lambda: lib.hsv_verify_batch_packed(d0, np.concatenate([w.pk, w.sig], 1).tobytes(), w.n))
+    call = lambda: lib.hsv_verify_strict(d0, pk0, sig0)
+    assert call() == 1
+    res["single_verify_strict"] = _p(_timed(call, reps))
+    # the C3 QC handed over as its bincode wire bytes (hsv_qc_verify_bincode:
     # parse + base64 keys + qc.digest() on the host, verification on the GPU)
-    from hsverify import wire
-    import hashlib
     w = synth.qc_votes(1000, seed=1000)
     block_hash = hashlib.sha512(b"block" + (1000).to_bytes(4, "little")).digest()[:32]
     buf = wire.encode_qc(block_hash, 1, [(bytes(p), bytes(q)) for p, q in zip(w.pk, w.sig)])
     nv = ctypes.c_size_t(0)
-    for _ in range(10):
-        assert lib.hsv_qc_verify_bincode(buf, len(buf), ctypes.byref(nv), None) == 1
-    ts = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        rc = lib.hsv_qc_verify_bincode(buf, len(buf), ctypes.byref(nv), None)
-        ts.append(time.perf_counter() - t0)
-        assert rc == 1
-    ts = np.array(ts) * 1e3
-    res["n1000_votes667_bincode"] = {"p50_ms": float(np.percentile(ts, 50)), "p99_ms": float(np.percentile(ts, 99)),
-                                     "reps": reps, "bytes": len(buf)}
+    call = lambda: lib.hsv_qc_verify_bincode(buf, len(buf), ctypes.byref(nv), None)
+    settle(call)
+    assert call() == 1
+    res["n1000_votes667_bincode"] = dict(_p(_timed(call, reps)), bytes=len(buf))
+    return res
+
+
+def tc_latency(reps, auto=True):
+    """C3 TC: 667 timeouts with per-vote digests SHA-512(round || hqc)[..32].
+    TC::verify (consensus/src/messages.rs:307-313) calls Signature::verify per
+    vote; the GPU form is the batched strict API (hsv_verify with per-item
+    digests) and the certificate from its bincode bytes."""
+    from hsverify import _lib, synth, wire
+    lib = _lib.load()
+    lib.hsv_set_auto_committee(1 if auto else 0)
+    res = {"automatic_committee_cache": bool(auto)}
+    for frac, tag in ((0.0, "clean"), (0.05, "corrupt5pct")):
+        w = member_corrupted(synth.tc_votes, 1000, seed=1000, frac=frac) if frac else synth.tc_votes(1000, seed=1000)
+        pk, sig, msg = (np.ascontiguousarray(a) for a in (w.pk, w.sig, w.msg))
+        flags = np.zeros(w.n, np.uint8)
+        if auto:  # the committee's keys were learnt from its QCs
+            q = synth.qc_votes(1000, seed=1000)
+            pq = np.concatenate([q.pk, q.sig], 1).tobytes()
+            for _ in range(3):
+                lib.hsv_verify_batch_packed(bytes(q.msg), pq, q.n)
+            lib.hsv_auto_committee_wait(60000)
+        call = lambda: lib.hsv_verify(pk.ctypes.data, sig.ctypes.data, msg.ctypes.data, 32, w.n, flags.ctypes.data)
+        res[f"n1000_votes667_{tag}_batched_strict"] = _p(_timed(call, reps))
+        assert bool((flags & 1).all()) == (frac == 0)
+        hqc = tc_hqc(1000, 1000)
+        buf = wire.encode_tc(1000, [(bytes(p), bytes(s), int(h)) for p, s, h in zip(w.pk, w.sig, hqc)])
+        nv = ctypes.c_size_t(0)
+        call = lambda: lib.hsv_tc_verify_bincode(buf, len(buf), ctypes.byref(nv), None)
+        rc = call()
+        assert rc == (1 if frac == 0 else 0)
+        res[f"n1000_votes667_{tag}_bincode"] = dict(_p(_timed(call, reps)), bytes=len(buf))
     return res
 
 
@@ -177,17 +292,9 @@ def committee_bench(reps, dev, n_votes=1 << 20):
         c = committee.Committee(synth.qc_votes(size, seed=size).pk)
         build_ms = (time.perf_counter() - t0) * 1e3
         h = c._h
-        for _ in range(10):
-            assert lib.hsv_committee_verify_batch_packed(h, digest, packed, w.n) == 1
-        ts = []
-        for _ in range(reps):
-            t0 = time.perf_counter()
-            rc = lib.hsv_committee_verify_batch_packed(h, digest, packed, w.n)
-            ts.append(time.perf_counter() - t0)
-            assert rc == 1
-        ts = np.array(ts) * 1e3
-        res[f"qc_n{size}_votes{w.n}"] = {"p50_ms": float(np.percentile(ts, 50)), "p99_ms": float(np.percentile(ts, 99)),
-                                         "reps": reps, "table_build_ms": build_ms}
+        call = lambda: lib.hsv_committee_verify_batch_packed(h, digest, packed, w.n)
+        assert call() == 1
+        res[f"qc_n{size}_votes{w.n}"] = dict(_p(_timed(call, reps)), table_build_ms=build_ms)
         c.close()
     # throughput: n_votes votes, each by one of 1000 members over its own digest
     seeds = synth.committee_seeds(1000, 7)
@@ -200,14 +307,15 @@ def committee_bench(reps, dev, n_votes=1 << 20):
     sig = torch.from_numpy(sigs).to(dev)
     msg = torch.from_numpy(msgs).to(dev)
     flags = torch.zeros(n_votes, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
     c.verify_device(idx, sig, msg, flags)
     torch.cuda.synchronize(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     steps = 5
-    e0.record()
+    e0.record(stream)
     for _ in range(steps):
         c.verify_device(idx, sig, msg, flags)
-    e1.record()
+    e1.record(stream)
     torch.cuda.synchronize(dev)
     ms = e0.elapsed_time(e1) / steps
     res["throughput"] = {"votes": n_votes, "committee": 1000, "kernel_ms": ms, "verif_per_s": n_votes / (ms * 1e-3),
@@ -217,32 +325,37 @@ def committee_bench(reps, dev, n_votes=1 << 20):
 
 
 def qc_cpu(reps=5):
-    """Single-core C port verify_batch rule for the C1 / C2 / C3 QCs (3, 67 and
-    667 votes): the reference's QC::verify path timed on one host core."""
+    """One host core: the reference's QC::verify crypto (dalek verify_batch:
+    random linear combination, one Straus / Pippenger MSM of 2n+1 points,
+    ported in oracle/ed25519_oracle.c) for C1 / C2 / C3, the strict-loop rule
+    beside it, the sequential TC::verify loop (early exit) and one verify_strict."""
     from hsverify import synth
-    so = os.path.join(ROOT, "oracle", "_build", "libhsv_oracle.so")
-    lib = ctypes.CDLL(so)
-    lib.oracle_verify_batch.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
-    res = {"cores": 1, "kind": "port"}
+    lib = _oracle()
+    res = {"cores": 1, "kind": "port", "cpu_model": cpu_model(),
+           "algorithm": "C port of ed25519-dalek 1.0.1 verify_batch (curve25519-dalek 3.x: Straus below 190 "
+                        "points, Pippenger w=6/7/8 above), radix-2^51 field"}
     for committee in (4, 100, 1000):
         w = synth.qc_votes(committee, seed=committee)
         pk, sig = np.ascontiguousarray(w.pk), np.ascontiguousarray(w.sig)
-        ts = []
-        for _ in range(reps):
-            t0 = time.perf_counter()
-            ok = lib.oracle_verify_batch(bytes(w.msg), pk.ctypes.data, sig.ctypes.data, w.n)
-            ts.append(time.perf_counter() - t0)
-            assert ok == 1
+        ts = _timed(lambda: lib.oracle_verify_batch_dalek(bytes(w.msg), pk.ctypes.data, sig.ctypes.data, w.n, 1),
+                    reps, warm=1)
+        assert lib.oracle_verify_batch_dalek(bytes(w.msg), pk.ctypes.data, sig.ctypes.data, w.n, 2) == 1
         res[f"n{committee}_votes{w.n}_p50_ms"] = float(np.median(ts) * 1e3)
-    lib.oracle_verify_flags.restype = ctypes.c_uint8
-    lib.oracle_verify_flags.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
+        ts = _timed(lambda: lib.oracle_verify_batch(bytes(w.msg), pk.ctypes.data, sig.ctypes.data, w.n), reps, warm=1)
+        res[f"n{committee}_votes{w.n}_strict_loop_p50_ms"] = float(np.median(ts) * 1e3)
+    w = member_corrupted(synth.qc_votes, 1000, seed=1000)
+    pk, sig = np.ascontiguousarray(w.pk), np.ascontiguousarray(w.sig)
+    ts = _timed(lambda: lib.oracle_verify_batch_dalek(bytes(w.msg), pk.ctypes.data, sig.ctypes.data, w.n, 3),
+                reps, warm=1)
+    assert lib.oracle_verify_batch_dalek(bytes(w.msg), pk.ctypes.data, sig.ctypes.data, w.n, 3) == 0
+    res["n1000_votes667_corrupt5pct_p50_ms"] = float(np.median(ts) * 1e3)
+    for frac, tag in ((0.0, "clean"), (0.05, "corrupt5pct")):
+        w = member_corrupted(synth.tc_votes, 1000, seed=1000, frac=frac) if frac else synth.tc_votes(1000, seed=1000)
+        pk, sig, msg = (np.ascontiguousarray(a) for a in (w.pk, w.sig, w.msg))
+        ts = _timed(lambda: lib.oracle_tc_verify(pk.ctypes.data, sig.ctypes.data, msg.ctypes.data, w.n), reps, warm=1)
+        res[f"tc_n1000_votes667_{tag}_p50_ms"] = float(np.median(ts) * 1e3)
     w = synth.qc_votes(4, seed=4)
-    ts = []
-    for _ in range(50):
-        t0 = time.perf_counter()
-        f = lib.oracle_verify_flags(bytes(w.pk[0]), bytes(w.sig[0]), bytes(w.msg), 32)
-        ts.append(time.perf_counter() - t0)
-        assert f & 1
+    ts = _timed(lambda: lib.oracle_verify_flags(bytes(w.pk[0]), bytes(w.sig[0]), bytes(w.msg), 32), 50, warm=2)
     res["single_verify_strict_p50_ms"] = float(np.median(ts) * 1e3)
     return res
 
@@ -273,20 +386,16 @@ def mempool_bench(dev, n=1 << 20, tx_size=512, cpu_sample=1 << 17):
     res = {"txs": n, "tx_size": tx_size, "ms_per_step": ms, "tx_per_s": n / (ms * 1e-3),
            "honest_all_accepted": bool((f[w.honest] & 1).all()),
            "corrupted_all_rejected": bool(not (f[~w.honest] & 1).any())}
-    so = os.path.join(ROOT, "oracle", "_build", "libhsv_oracle.so")
-    if os.path.exists(so):
-        lib = ctypes.CDLL(so)
-        lib.oracle_verify_tx_many.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
-                                              ctypes.c_void_p, ctypes.c_int]
-        m = min(cpu_sample, n)
-        threads = max(1, min(16, os.cpu_count() or 1))
-        buf = np.ascontiguousarray(w.txs[:m])
-        out = np.zeros(m, np.uint8)
-        t0 = time.perf_counter()
-        lib.oracle_verify_tx_many(buf.ctypes.data, None, tx_size, m, out.ctypes.data, threads)
-        dt = time.perf_counter() - t0
-        res["cpu_baseline"] = {"value": m / dt, "unit": "tx/s", "cores": threads, "kind": "port",
-                               "sample": f"first {m} transactions", "sample_parity_vs_gpu": bool((out == f[:m]).all())}
+    lib = _oracle()
+    m = min(cpu_sample, n)
+    threads, _ = host_cores()
+    buf = np.ascontiguousarray(w.txs[:m])
+    out = np.zeros(m, np.uint8)
+    t0 = time.perf_counter()
+    lib.oracle_verify_tx_many(buf.ctypes.data, None, tx_size, m, out.ctypes.data, threads)
+    dt = time.perf_counter() - t0
+    res["cpu_baseline"] = {"value": m / dt, "unit": "tx/s", "cores": threads, "kind": "port",
+                           "sample": f"first {m} transactions", "sample_parity_vs_gpu": bool((out == f[:m]).all())}
     return res
 
 
@@ -305,24 +414,89 @@ def host_api_bench(w, reps=3):
             "honest_all_accepted": bool((f[w.honest] & 1).all())}
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (one per GPU); default WORLD_SIZE or 1")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=1 << 20, help="triples per GPU")
+    ap.add_argument("--n", "--per-gpu", dest="n", type=int, default=1 << 20, help="triples per GPU")
     ap.add_argument("--variant", type=int, default=None)
     ap.add_argument("--cpu-sample", type=int, default=1 << 20,
-                    help="triples the CPU port verifies (default: the whole C4 batch, about 3 s on 16 cores)")
+                    help="triples the CPU port verifies (default: the whole C4 batch)")
     ap.add_argument("--qc-reps", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-qc", action="store_true")
     ap.add_argument("--global-n", type=int, default=None,
                     help="C5 strong scaling: total triples split over the ranks (e.g. 16777216 = 2^24); "
                          "default: weak scaling with --n per GPU")
-    a = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU only: launcher, shards, timing and gather without a GPU or verification")
+    return ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+
+def launch_ranks(a):
+    """Start one rank per GPU under torch.distributed.run; this process stays
+    off the GPU and exits with the launcher's status."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    # torch.distributed.run's own parser rejects "--n" as an ambiguous prefix of
+    # its options even after the script path: hand it on as --per-gpu
+    args = ["--per-gpu" + x[3:] if x == "--n" or x.startswith("--n=") else x for x in sys.argv[1:]]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + args
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    log(f"[launcher] {' '.join(cmd)}")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dry_run(a, world, rank, dist):
+    """Launcher / sharding / timing / gather path without a GPU: each rank owns
+    its contiguous shard and runs a byte checksum over it as the 'step'."""
+    strong = a.global_n is not None
+    n = a.global_n // world if strong else a.n
+    lo, hi = rank * n, (rank + 1) * n
+    rng = np.random.default_rng(rank)
+    data = rng.integers(0, 256, (n, 128), dtype=np.uint8)
+    for _ in range(a.warmup):
+        np.bitwise_xor.reduce(data, axis=1)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        flags = np.bitwise_xor.reduce(data, axis=1)
+    elapsed = time.perf_counter() - t0
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    shards = [None] * world
+    dist.all_gather_object(shards, (rank, lo, hi, int(flags.size)))
+    from hsverify import dist as hd
+    gathered = hd.gather_strict(flags & 1, n * world)
+    if rank == 0:
+        el = float(t.item())
+        print(json.dumps({
+            "metric": "dry run (no GPU, no verification): launcher / shard / gather check",
+            "value": n * world * a.steps / el, "unit": "items/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": el / a.steps * 1e3, "higher_is_better": True,
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "dry_run": True, "config": {"workload": "dry run", "batch_per_gpu": n, "global_batch": n * world,
+                                        "parallelism": f"dp{world}"},
+            "shards": [[r, l, h, m] for r, l, h, m in sorted(shards)], "gathered_items": int(gathered.size),
+        }), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def main():
+    a = parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus is not None and a.gpus > 1:
+        sys.exit(launch_ranks(a))
+    world = int(env_world or "1")
+    if a.gpus is not None and a.gpus != world:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     strong = a.global_n is not None
     if strong:
         if a.global_n % world:
@@ -331,8 +505,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
-    import torch
     import torch.distributed as dist
+    if a.dry_run:
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                init_method=None if world > 1 else "tcp://127.0.0.1:%d" % _free_port())
+        return dry_run(a, world, rank, dist)
+
+    import torch
     from hsverify import _lib, synth, verifier
 
     if world > 1:
@@ -340,10 +519,11 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     _lib.load()
+    verifier.bind_device(local_rank)  # this rank's host-buffer calls stay on its GPU
     if a.variant is not None:
         verifier.set_variant(a.variant)
 
-    host_threads = max(1, min(16, (os.cpu_count() or 1) // max(1, world)))
+    host_threads = max(1, host_cores()[0] // max(1, world))
     t0 = time.perf_counter()
     # contiguous shard of the global batch: rank r owns items [r*n, (r+1)*n)
     w = synth.independent_triples(a.n, seed=0xC4 * 1000 + rank, corrupt_frac=0.05, nthreads=host_threads)
@@ -369,12 +549,18 @@ def main():
     e1.record(stream)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
+    kernel_ms = e0.elapsed_time(e1) / a.steps
+    mine = {"rank": rank, "kernel_ms": kernel_ms, "elapsed_s": elapsed}
+    per_rank = [mine]
     if world > 1:
         dist.barrier()
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kernel_ms = e0.elapsed_time(e1) / a.steps
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
+    for r in per_rank:
+        r["frac"] = a.n * WORK_MACS / (r["kernel_ms"] * 1e-3) / PEAK_MACS
 
     f = flags.cpu().numpy()
     honest_ok = bool((f[w.honest] & 1).all())
@@ -435,18 +621,18 @@ def main():
             "peak_probe": probe / 1e12,
             "work_per_verify": f"{WORK_MACS} u32 MACs (SURVEY 8(d)); {IO_BYTES} HBM bytes algorithmic",
             "kernel_ms": kernel_ms,
-            "kernels": ("hsv_prep_kernel + hsv_verify_hp_kernel (one verify launch: scalar prepass, point pass)"
-                        if verifier.get_variant() in (19, 20, 21) else "hsv_verify_hc_kernel"),
+            "kernels": "hsv_prep_kernel + hsv_verify_hp_kernel (one verify launch: scalar prepass, point pass)",
+            "per_rank": per_rank,
         },
         "checks": {"honest_all_accepted": honest_ok, "corrupted_all_rejected": corrupt_rejected,
                    "strict_accepted_global": global_accepted},
     }
     if world == 1 and not a.no_cpu_baseline:
-        threads = max(1, min(16, os.cpu_count() or 1))
-        out["cpu_baseline"] = cpu_baseline(w, f, a.cpu_sample, threads)
+        out["cpu_baseline"] = cpu_baseline(w, f, a.cpu_sample)
     if not a.no_qc:
         out["qc_latency"] = qc_latency(a.qc_reps, auto=True)
         out["qc_latency_generic"] = qc_latency(a.qc_reps, auto=False)
+        out["tc_latency"] = tc_latency(a.qc_reps, auto=True)
         _lib.load().hsv_set_auto_committee(1)
         out["committee_cache"] = committee_bench(a.qc_reps, dev)
         out["mempool_tx"] = mempool_bench(dev)
@@ -457,6 +643,14 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
 
 if __name__ == "__main__":

@@ -873,9 +873,11 @@ static void msm_pippenger(ge *out, const uint64_t (*sc)[4], const ge *pts, size_
   free(pc);
 }
 
-/* 1 = Ok, 0 = Err, for crypto::Signature::verify_batch(digest, votes) */
-int oracle_verify_batch_dalek(const uint8_t digest[32], const uint8_t *pk, const uint8_t *sig, size_t n,
-                              uint64_t seed) {
+/* 1 = Ok, 0 = Err, for dalek verify_batch over n (pk, sig, msg) triples with
+ * 32-byte messages at msg + i * msg_stride (msg_stride 0: one shared digest,
+ * crypto::Signature::verify_batch(digest, votes)) */
+int oracle_verify_batch_dalek_msgs(const uint8_t *msg, size_t msg_stride, const uint8_t *pk, const uint8_t *sig,
+                                   size_t n, uint64_t seed) {
   pthread_once(&g_once, init_consts);
   if (n == 0) return 1;
   const size_t m = 2 * n + 1;
@@ -892,7 +894,7 @@ int oracle_verify_batch_dalek(const uint8_t digest[32], const uint8_t *pk, const
     uint8_t buf[96], h[64];
     memcpy(buf, s, 32);
     memcpy(buf + 32, p, 32);
-    memcpy(buf + 64, digest, 32);
+    memcpy(buf + 64, msg + msg_stride * i, 32);
     sha512(h, buf, 96);
     uint64_t hw[8], k[4], sv[4], z[4] = {0, 0, 0, 0}, t[4];
     sc_from_bytes64(hw, h);
@@ -931,6 +933,61 @@ int oracle_verify_batch_dalek(const uint8_t digest[32], const uint8_t *pk, const
   free(sc);
   free(pts);
   return ok;
+}
+
+int oracle_verify_batch_dalek(const uint8_t digest[32], const uint8_t *pk, const uint8_t *sig, size_t n,
+                              uint64_t seed) {
+  return oracle_verify_batch_dalek_msgs(digest, 0, pk, sig, n, seed);
+}
+
+/* Per-item accept vector the batch way (BASELINE.md CPU plan for C4/C5):
+ * chunks of 64 through verify_batch; a chunk that fails is re-verified item
+ * by item with verify_strict.  Fills flags with STRICT_OK bits only (1 / 0)
+ * for the chunk-accepted items and the full flag byte for re-verified ones;
+ * nthreads host threads over contiguous chunk ranges. */
+typedef struct {
+  const uint8_t *pk, *sig, *msg;
+  size_t lo, hi;
+  uint8_t *flags;
+  uint64_t fallback_chunks;
+} b64job_t;
+
+static void *b64_worker(void *arg) {
+  b64job_t *j = (b64job_t *)arg;
+  for (size_t c = j->lo; c < j->hi; c += 64) {
+    const size_t m = (j->hi - c) < 64 ? (j->hi - c) : 64;
+    if (oracle_verify_batch_dalek_msgs(j->msg + 32 * c, 32, j->pk + 32 * c, j->sig + 64 * c, m, 0x5eed + c)) {
+      memset(j->flags + c, STRICT_OK, m);
+    } else {
+      ++j->fallback_chunks;
+      for (size_t i = c; i < c + m; ++i)
+        j->flags[i] = oracle_verify_flags(j->pk + 32 * i, j->sig + 64 * i, j->msg + 32 * i, 32);
+    }
+  }
+  return NULL;
+}
+
+uint64_t oracle_verify_many_batch64(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, size_t n,
+                                    uint8_t *flags, int nthreads) {
+  pthread_once(&g_once, init_consts);
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  b64job_t jobs[256];
+  const size_t chunks = (n + 63) / 64;
+  for (int t = 0; t < nthreads; ++t) {
+    size_t lo = chunks * t / nthreads * 64, hi = chunks * (t + 1) / nthreads * 64;
+    if (hi > n) hi = n;
+    if (lo > n) lo = n;
+    jobs[t] = (b64job_t){pk, sig, msg, lo, hi, flags, 0};
+    pthread_create(&th[t], NULL, b64_worker, &jobs[t]);
+  }
+  uint64_t fb = 0;
+  for (int t = 0; t < nthreads; ++t) {
+    pthread_join(th[t], NULL);
+    fb += jobs[t].fallback_chunks;
+  }
+  return fb;
 }
 
 /* consensus TC::verify's signature loop (consensus/src/messages.rs:307-313):
