@@ -138,10 +138,11 @@ DeviceGuard::~DeviceGuard() {
 }
 
 SlotLease::SlotLease(DevCtx &c) {
+  // lowest free slot first: a lone caller keeps reusing slot 0 and its warm
+  // staging buffers; concurrent callers spill over to the next slots
   const size_t k = c.slots.size();
-  const unsigned start = c.rr.fetch_add(1);
   for (size_t i = 0; i < k; ++i) {
-    Slot &s = *c.slots[(start + i) % k];
+    Slot &s = *c.slots[i];
     std::unique_lock<std::mutex> l(s.mu, std::try_to_lock);
     if (l.owns_lock()) {
       s_ = &s;
@@ -149,7 +150,7 @@ SlotLease::SlotLease(DevCtx &c) {
       return;
     }
   }
-  s_ = c.slots[start % k].get();
+  s_ = c.slots[c.rr.fetch_add(1) % k].get();  // all busy: queue on one, round-robin
   lk_ = std::unique_lock<std::mutex>(s_->mu);
 }
 

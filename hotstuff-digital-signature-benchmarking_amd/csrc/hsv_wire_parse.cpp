@@ -1,0 +1,192 @@
+// Bincode parsers of QC / TC certificates (see hsv_wire_parse.h).
+//
+// Layouts (bincode 1.3 default options: little-endian, fixed-width integers,
+// u64 length prefixes; the serde derives of the reference):
+//   Digest            32 raw bytes            crypto/src/lib.rs:20-22
+//   PublicKey         str: u64 len + base64   crypto/src/lib.rs:94-101
+//   Signature         part1 (32) || part2 (32) crypto/src/lib.rs:176-182
+//   QC  = hash: Digest | round: u64 | votes: Vec<(PublicKey, Signature)>
+//   TC  = round: u64 | votes: Vec<(PublicKey, Signature, Round)>
+// PublicKey::decode_base64 (crypto/src/lib.rs:73-79) runs base64 0.13's
+// standard decoder and keeps the first 32 bytes; shorter decodings are an
+// error.  This decoder follows the same rules: standard alphabet, optional
+// '=' padding only at the end, no non-zero trailing bits.
+#include "hsv_wire_parse.h"
+
+#include <array>
+#include <cstring>
+#include <unordered_map>
+
+#include "hsv_sha512.hpp"
+
+namespace hsvw {
+namespace {
+
+struct Reader {
+  const uint8_t *p;
+  size_t left;
+  bool u64(uint64_t &v) {
+    if (left < 8) return false;
+    v = 0;
+    for (int i = 7; i >= 0; --i) v = (v << 8) | p[i];
+    p += 8;
+    left -= 8;
+    return true;
+  }
+  bool bytes(const uint8_t *&out, size_t n) {
+    if (left < n) return false;
+    out = p;
+    p += n;
+    left -= n;
+    return true;
+  }
+};
+
+int b64_value(uint8_t c) {
+  if (c >= 'A' && c <= 'Z') return c - 'A';
+  if (c >= 'a' && c <= 'z') return c - 'a' + 26;
+  if (c >= '0' && c <= '9') return c - '0' + 52;
+  if (c == '+') return 62;
+  if (c == '/') return 63;
+  return -1;
+}
+
+// PublicKey from its bincode str
+bool read_public_key(Reader &r, uint8_t pk[32]) {
+  uint64_t len = 0;
+  const uint8_t *s = nullptr;
+  if (!r.u64(len) || len > r.left || !r.bytes(s, (size_t)len)) return false;
+  std::vector<uint8_t> dec;
+  if (!b64_decode(s, (size_t)len, dec) || dec.size() < 32) return false;
+  std::memcpy(pk, dec.data(), 32);
+  return true;
+}
+
+void put_le64(uint8_t *p, uint64_t v) {
+  for (int b = 0; b < 8; ++b) p[b] = (uint8_t)(v >> (8 * b));
+}
+
+}  // namespace
+
+bool b64_decode(const uint8_t *s, size_t n, std::vector<uint8_t> &out) {
+  size_t end = n;
+  while (end > 0 && s[end - 1] == '=') --end;
+  if (n - end > 2) return false;
+  if (n != end && n % 4 != 0) return false;  // padded input comes in whole quads
+  const size_t rem = end % 4;
+  if (rem == 1) return false;
+  out.clear();
+  out.reserve(end * 3 / 4);
+  uint32_t acc = 0;
+  int bits = 0;
+  for (size_t i = 0; i < end; ++i) {
+    const int v = b64_value(s[i]);
+    if (v < 0) return false;
+    acc = (acc << 6) | (uint32_t)v;
+    bits += 6;
+    if (bits >= 8) {
+      bits -= 8;
+      out.push_back((uint8_t)(acc >> bits));
+      acc &= (1u << bits) - 1u;
+    }
+  }
+  return acc == 0;  // the leftover (trailing) bits must be zero
+}
+
+bool parse_qc(const uint8_t *buf, size_t len, QcParsed &out, std::string &err) {
+  if (!buf && len) {
+    err = "null buffer";
+    return false;
+  }
+  Reader r{buf, len};
+  const uint8_t *hash = nullptr;
+  uint64_t nv = 0;
+  if (!r.bytes(hash, 32) || !r.u64(out.round) || !r.u64(nv)) {
+    err = "truncated QC header";
+    return false;
+  }
+  if (nv > r.left / 72) {  // a vote is at least 8 + 0 + 64 bytes
+    err = "vote count exceeds the buffer";
+    return false;
+  }
+  out.n = (size_t)nv;
+  out.votes.assign(out.n * 96, 0);
+  for (size_t i = 0; i < out.n; ++i) {
+    uint8_t *v = out.votes.data() + i * 96;
+    const uint8_t *sig = nullptr;
+    if (!read_public_key(r, v)) {
+      err = "vote " + std::to_string(i) + ": bad public key";
+      return false;
+    }
+    if (!r.bytes(sig, 64)) {
+      err = "vote " + std::to_string(i) + ": truncated signature";
+      return false;
+    }
+    std::memcpy(v + 32, sig, 64);
+  }
+  if (r.left != 0) {
+    err = "trailing bytes after the QC";
+    return false;
+  }
+  uint8_t pre[40], h[64];
+  std::memcpy(pre, hash, 32);
+  put_le64(pre + 32, out.round);
+  hsv::sha512_bytes(pre, sizeof(pre), h);
+  std::memcpy(out.digest, h, 32);
+  return true;
+}
+
+bool parse_tc(const uint8_t *buf, size_t len, TcParsed &out, std::string &err) {
+  if (!buf && len) {
+    err = "null buffer";
+    return false;
+  }
+  Reader r{buf, len};
+  uint64_t nv = 0;
+  if (!r.u64(out.round) || !r.u64(nv)) {
+    err = "truncated TC header";
+    return false;
+  }
+  if (nv > r.left / 80) {  // 8 + 0 + 64 + 8 bytes at least
+    err = "vote count exceeds the buffer";
+    return false;
+  }
+  out.n = (size_t)nv;
+  out.pks.assign(out.n * 32, 0);
+  out.sigs.assign(out.n * 64, 0);
+  out.digests.assign(out.n * 32, 0);
+  // the per-vote digest depends only on (round, high_qc_round), and a TC's
+  // high_qc_rounds take few distinct values: hash each once
+  std::unordered_map<uint64_t, std::array<uint8_t, 32>> memo;
+  for (size_t i = 0; i < out.n; ++i) {
+    const uint8_t *sig = nullptr;
+    uint64_t hqc = 0;
+    if (!read_public_key(r, out.pks.data() + i * 32)) {
+      err = "vote " + std::to_string(i) + ": bad public key";
+      return false;
+    }
+    if (!r.bytes(sig, 64) || !r.u64(hqc)) {
+      err = "vote " + std::to_string(i) + ": truncated";
+      return false;
+    }
+    std::memcpy(out.sigs.data() + i * 64, sig, 64);
+    auto it = memo.find(hqc);
+    if (it == memo.end()) {
+      uint8_t pre[16], h[64];
+      put_le64(pre, out.round);
+      put_le64(pre + 8, hqc);
+      hsv::sha512_bytes(pre, sizeof(pre), h);
+      std::array<uint8_t, 32> d;
+      std::memcpy(d.data(), h, 32);
+      it = memo.emplace(hqc, d).first;
+    }
+    std::memcpy(out.digests.data() + i * 32, it->second.data(), 32);
+  }
+  if (r.left != 0) {
+    err = "trailing bytes after the TC";
+    return false;
+  }
+  return true;
+}
+
+}  // namespace hsvw
