@@ -57,6 +57,19 @@ HSV_INL constexpr uint32_t fe26_2p(int i) { return i == 0 ? 0x7ffffdau : ((i & 1
 // largest limb value g may hold in fe_mul (so that 19 * g fits 32 bits)
 HSV_INL constexpr uint32_t fe26_gmax(int i) { return (i & 1) ? 113025455u : 226050910u; }
 
+// 2x as v_add_u32 (x + x): the compiler's canonical form is a left shift,
+// and v_lshlrev_b32 issues at the VOP3 rate on gfx950 while v_add_u32 is a
+// full-rate op (tools/ubench_isa.hip, profiles/r02_ubench_isa.txt)
+HSV_INL uint32_t fe26_x2(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_add_u32_e32 %0, %1, %1" : "=v"(r) : "v"(x));
+  return r;
+#else
+  return x * 2u;
+#endif
+}
+
 HSV_INL fe fe_small(uint32_t x) {
   fe r;
   r.v[0] = x;
@@ -194,43 +207,51 @@ HSV_INL void fe26_check_columns(const fe &f, const fe &g) {
 // otherwise split a column into parallel partial sums (and move the carry-in
 // to the end), paying a 64-bit add per split; a dependent chain issues as
 // fast as independent ones on gfx950 (tools/ubench_chain.hip).  The carry-out
-// SGPR pair of the instruction is a dead early-clobber output.
-#define HSV_MAD1(i) "v_mad_u64_u32 %0, %1, %" #i ", %" #i "+1, %0\n\t"
-template <int N>
+// carry-out SGPR pair of the instruction is dead (see below).
+template <int N, bool ZERO = false>
 HSV_INL uint64_t fe26_chain(const uint32_t *a, const uint32_t *b, uint64_t acc) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  uint64_t cc;
+  static_assert(N == 5 || N == 6 || N == 10, "chain length");
+  // Operand i of the chain is (a[i], b[i]) = (%(2i+1), %(2i+2)).  The
+  // instruction's carry-out SGPR pair is dead: it goes to VCC, declared
+  // clobbered (an SGPR output operand makes the compiler pad every chain
+  // with an s_nop).  A ZERO chain starts from the inline constant 0 instead
+  // of a cleared register pair (early-clobber output: the inputs are read
+  // after the first instruction writes it).
+#define HSV_MC(x, y, c) "v_mad_u64_u32 %0, vcc, %" #x ", %" #y ", " c "\n\t"
+#define HSV_C0 (ZERO ? "0" : "%0")
 #define HSV_P(i) "v"(a[i]), "v"(b[i])
-#define HSV_M(k) "v_mad_u64_u32 %0, %1, %" #k
-  static_assert(N >= 1 && N <= 10, "chain length");
-  if constexpr (N == 5)
-    asm(HSV_M(2) ", %3, %0\n\t" HSV_M(4) ", %5, %0\n\t" HSV_M(6) ", %7, %0\n\t" HSV_M(8) ", %9, %0\n\t"
-        HSV_M(10) ", %11, %0"
-        : "+v"(acc), "=&s"(cc) : HSV_P(0), HSV_P(1), HSV_P(2), HSV_P(3), HSV_P(4));
-  else if constexpr (N == 6)
-    asm(HSV_M(2) ", %3, %0\n\t" HSV_M(4) ", %5, %0\n\t" HSV_M(6) ", %7, %0\n\t" HSV_M(8) ", %9, %0\n\t"
-        HSV_M(10) ", %11, %0\n\t" HSV_M(12) ", %13, %0"
-        : "+v"(acc), "=&s"(cc) : HSV_P(0), HSV_P(1), HSV_P(2), HSV_P(3), HSV_P(4), HSV_P(5));
-  else if constexpr (N == 10)
-    asm(HSV_M(2) ", %3, %0\n\t" HSV_M(4) ", %5, %0\n\t" HSV_M(6) ", %7, %0\n\t" HSV_M(8) ", %9, %0\n\t"
-        HSV_M(10) ", %11, %0\n\t" HSV_M(12) ", %13, %0\n\t" HSV_M(14) ", %15, %0\n\t" HSV_M(16) ", %17, %0\n\t"
-        HSV_M(18) ", %19, %0\n\t" HSV_M(20) ", %21, %0"
-        : "+v"(acc), "=&s"(cc)
-        : HSV_P(0), HSV_P(1), HSV_P(2), HSV_P(3), HSV_P(4), HSV_P(5), HSV_P(6), HSV_P(7), HSV_P(8), HSV_P(9));
-  else {
-    HSV_UNROLL
-    for (int i = 0; i < N; ++i) acc += (uint64_t)a[i] * b[i];
+#define HSV_BODY5 HSV_MC(3, 4, "%0") HSV_MC(5, 6, "%0") HSV_MC(7, 8, "%0") HSV_MC(9, 10, "%0")
+#define HSV_BODY6 HSV_BODY5 HSV_MC(11, 12, "%0")
+#define HSV_BODY10 HSV_BODY6 HSV_MC(13, 14, "%0") HSV_MC(15, 16, "%0") HSV_MC(17, 18, "%0") HSV_MC(19, 20, "%0")
+#define HSV_IN5 HSV_P(0), HSV_P(1), HSV_P(2), HSV_P(3), HSV_P(4)
+#define HSV_IN6 HSV_IN5, HSV_P(5)
+#define HSV_IN10 HSV_IN6, HSV_P(6), HSV_P(7), HSV_P(8), HSV_P(9)
+  if constexpr (ZERO) {
+    static_assert(N != 5, "zero-start chains are columns 0 (6 or 10 products)");
+    if constexpr (N == 6) asm(HSV_MC(1, 2, "0") HSV_BODY6 : "=&v"(acc) : HSV_IN6 : "vcc");
+    else asm(HSV_MC(1, 2, "0") HSV_BODY10 : "=&v"(acc) : HSV_IN10 : "vcc");
+  } else {
+    if constexpr (N == 5) asm(HSV_MC(1, 2, "%0") HSV_BODY5 : "+v"(acc) : HSV_IN5 : "vcc");
+    else if constexpr (N == 6) asm(HSV_MC(1, 2, "%0") HSV_BODY6 : "+v"(acc) : HSV_IN6 : "vcc");
+    else asm(HSV_MC(1, 2, "%0") HSV_BODY10 : "+v"(acc) : HSV_IN10 : "vcc");
   }
+#undef HSV_MC
+#undef HSV_C0
 #undef HSV_P
-#undef HSV_M
-  (void)cc;
+#undef HSV_BODY5
+#undef HSV_BODY6
+#undef HSV_BODY10
+#undef HSV_IN5
+#undef HSV_IN6
+#undef HSV_IN10
   return acc;
 #else
+  if (ZERO) acc = 0;
   for (int i = 0; i < N; ++i) acc += (uint64_t)a[i] * b[i];
   return acc;
 #endif
 }
-#undef HSV_MAD1
 
 // Columns are produced in order 0..9; the carry out of column k is the
 // initial accumulator of column k+1 (v_mad_u64_u32 adds it for free), so the
@@ -254,7 +275,7 @@ HSV_INL fe fe_mul(const fe &f, const fe &g) {
   HSV_UNROLL
   for (int i = 0; i < 10; ++i) {
     g19[i] = g.v[i] * 19u;
-    f2[i] = (i & 1) ? f.v[i] * 2u : f.v[i];
+    f2[i] = (i & 1) ? fe26_x2(f.v[i]) : f.v[i];
   }
 #ifdef HSV_FE26_PARALLEL_CARRY
   uint64_t h[10];
@@ -287,7 +308,7 @@ HSV_INL fe fe_mul(const fe &f, const fe &g) {
       ca[i] = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
       cb[i] = wrap ? g19[j] : g.v[j];
     }
-    acc = fe26_chain<10>(ca, cb, acc);
+    acc = k == 0 ? fe26_chain<10, true>(ca, cb, 0) : fe26_chain<10>(ca, cb, acc);
     r.v[k] = (uint32_t)acc & fe26_mask(k);
     acc >>= fe26_bits(k);
   }
@@ -318,6 +339,7 @@ HSV_INL void fe26_sq_operands(int i, int j, const uint32_t *f, const uint32_t *f
 template <int K>
 HSV_INL uint64_t fe26_sq_column(const uint32_t *f, const uint32_t *f2, const uint32_t *f19, const uint32_t *f38,
                                 uint64_t acc) {
+  constexpr bool ZERO = K == 0;
   constexpr int N = (K % 2 == 0) ? 6 : 5;
   uint32_t ca[N], cb[N];
   int n = 0;
@@ -330,7 +352,7 @@ HSV_INL uint64_t fe26_sq_column(const uint32_t *f, const uint32_t *f2, const uin
       ++n;
     }
   }
-  return fe26_chain<N>(ca, cb, acc);
+  return fe26_chain<N, ZERO>(ca, cb, acc);
 }
 
 HSV_INL fe fe_sq(const fe &f) {
@@ -342,9 +364,11 @@ HSV_INL fe fe_sq(const fe &f) {
   uint32_t f2[10], f19[10], f38[10];
   HSV_UNROLL
   for (int i = 0; i < 10; ++i) {
-    f2[i] = f.v[i] * 2u;
-    f19[i] = f.v[i] * 19u;
-    f38[i] = (i & 1) ? f19[i] * 2u : 0u;  // only odd limbs are scaled by 38
+    f2[i] = fe26_x2(f.v[i]);
+    // 19x only where a product wraps past limb 9 (j >= 5 in f_i f_j, i <= j);
+    // 38x only for odd j >= 5, as 19x + 19x (one VOP3 multiply per limb)
+    f19[i] = i >= 5 ? f.v[i] * 19u : 0u;
+    f38[i] = (i >= 5 && (i & 1)) ? fe26_x2(f19[i]) : 0u;
   }
 #ifdef HSV_FE26_PARALLEL_CARRY
   uint64_t h[10];
@@ -451,10 +475,20 @@ HSV_INL uint32_t fe_eq(const fe &a, const fe &b) {
   return acc == 0;
 }
 
+// Per-lane select.  On the device the lane mask is an explicit SGPR pair
+// (ballot) read by v_cndmask_b32_e64: the compiler's VCC form
+// (v_cndmask_b32_e32) issues ~5x slower on gfx950 when several read VCC in a
+// row (tools/ubench_isa.hip, profiles/r02_ubench_isa.txt).
 HSV_INL fe fe_select(const fe &a, const fe &b, uint32_t take_b) {
   fe r;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint64_t m = __ballot(take_b != 0u);
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r.v[i]) : "v"(a.v[i]), "v"(b.v[i]), "s"(m));
+#else
   HSV_UNROLL
   for (int i = 0; i < 10; ++i) r.v[i] = take_b ? b.v[i] : a.v[i];
+#endif
   return r;
 }
 
