@@ -265,18 +265,40 @@ HSV_INL void fe26_wrap_carry(fe &r, uint64_t acc) {
   r.v[1] += (uint32_t)(t >> 26);
 }
 
-HSV_INL fe fe_mul(const fe &f, const fe &g) {
-  HSV_SCHED_FENCE();
+// column K of f*g (10 products, with the 19x / 2x folds) added to acc; column
+// 0 starts from zero
+template <int K>
+HSV_INL uint64_t fe26_mul_column(const uint32_t *f, const uint32_t *f2, const uint32_t *g, const uint32_t *g19,
+                                 uint64_t acc) {
+  uint32_t ca[10], cb[10];
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) {
+    int j = K - i;
+    const bool wrap = j < 0;
+    if (wrap) j += 10;
+    ca[i] = ((i & 1) && (j & 1)) ? f2[i] : f[i];
+    cb[i] = wrap ? g19[j] : g[j];
+  }
+  return K == 0 ? fe26_chain<10, true>(ca, cb, 0) : fe26_chain<10>(ca, cb, acc);
+}
+
+// operand prescaling of fe_mul: 19 g (every limb), 2 f (odd limbs)
+HSV_INL void fe26_mul_prescale(const fe &f, const fe &g, uint32_t f2[10], uint32_t g19[10]) {
 #if defined(HSV_CHECK_BOUNDS) && !defined(__HIP_DEVICE_COMPILE__)
   for (int i = 0; i < 10; ++i) HSV_BOUND(g.v[i] <= fe26_gmax(i), "fe_mul g operand too large");
   fe26_check_columns(f, g);
 #endif
-  uint32_t g19[10], f2[10];
   HSV_UNROLL
   for (int i = 0; i < 10; ++i) {
     g19[i] = g.v[i] * 19u;
     f2[i] = (i & 1) ? fe26_x2(f.v[i]) : f.v[i];
   }
+}
+
+HSV_INL fe fe_mul(const fe &f, const fe &g) {
+  HSV_SCHED_FENCE();
+  uint32_t g19[10], f2[10];
+  fe26_mul_prescale(f, g, f2, g19);
 #ifdef HSV_FE26_PARALLEL_CARRY
   uint64_t h[10];
   HSV_UNROLL
@@ -297,25 +319,117 @@ HSV_INL fe fe_mul(const fe &f, const fe &g) {
 #else
   fe r;
   uint64_t acc = 0;
-  HSV_UNROLL
-  for (int k = 0; k < 10; ++k) {
-    uint32_t ca[10], cb[10];
-    HSV_UNROLL
-    for (int i = 0; i < 10; ++i) {
-      int j = k - i;
-      const bool wrap = j < 0;
-      if (wrap) j += 10;
-      ca[i] = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
-      cb[i] = wrap ? g19[j] : g.v[j];
-    }
-    acc = k == 0 ? fe26_chain<10, true>(ca, cb, 0) : fe26_chain<10>(ca, cb, acc);
-    r.v[k] = (uint32_t)acc & fe26_mask(k);
-    acc >>= fe26_bits(k);
-  }
+#define HSV_MULC(K)                                         \
+  acc = fe26_mul_column<K>(f.v, f2, g.v, g19, acc);         \
+  r.v[K] = (uint32_t)acc & fe26_mask(K);                    \
+  acc >>= fe26_bits(K);
+  HSV_MULC(0) HSV_MULC(1) HSV_MULC(2) HSV_MULC(3) HSV_MULC(4)
+  HSV_MULC(5) HSV_MULC(6) HSV_MULC(7) HSV_MULC(8) HSV_MULC(9)
+#undef HSV_MULC
   fe26_wrap_carry(r, acc);
 #endif
   HSV_SCHED_FENCE();
   return r;
+}
+
+// Two independent products r = f g, s = h k, interleaved column by column:
+// two dependency chains per wave instead of one.  A lone chain leaves the
+// SIMD's v_mad_u64_u32 issue short of its rate at the point pass's 3 waves per
+// SIMD (tools/ubench_fe.hip), and the instruction after each chain no longer
+// reads that chain's result (no s_nop pad behind the inline asm).
+HSV_INL void fe_mul2(const fe &f, const fe &g, const fe &h, const fe &k, fe &r, fe &s) {
+  HSV_SCHED_FENCE();
+  uint32_t g19[10], f2[10], k19[10], h2[10];
+  fe26_mul_prescale(f, g, f2, g19);
+  fe26_mul_prescale(h, k, h2, k19);
+  uint64_t a0 = 0, a1 = 0;
+#define HSV_MULC2(K)                                        \
+  a0 = fe26_mul_column<K>(f.v, f2, g.v, g19, a0);           \
+  a1 = fe26_mul_column<K>(h.v, h2, k.v, k19, a1);           \
+  r.v[K] = (uint32_t)a0 & fe26_mask(K);                     \
+  a0 >>= fe26_bits(K);                                      \
+  s.v[K] = (uint32_t)a1 & fe26_mask(K);                     \
+  a1 >>= fe26_bits(K);
+  HSV_MULC2(0) HSV_MULC2(1) HSV_MULC2(2) HSV_MULC2(3) HSV_MULC2(4)
+  HSV_MULC2(5) HSV_MULC2(6) HSV_MULC2(7) HSV_MULC2(8) HSV_MULC2(9)
+#undef HSV_MULC2
+  fe26_wrap_carry(r, a0);
+  fe26_wrap_carry(s, a1);
+  HSV_SCHED_FENCE();
+}
+
+// Prepared operands: the prescaling of fe_mul done once for an operand that
+// several products share (the point formulas' E, F, G, H).
+//   fe_f: f with odd limbs doubled;  fe_g: g with every limb times 19.
+struct fe_f {
+  fe v;
+  uint32_t x2[10];
+};
+struct fe_g {
+  fe v;
+  uint32_t x19[10];
+};
+
+HSV_INL fe_f fe_prep_f(const fe &f) {
+  fe_f r;
+  r.v = f;
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) r.x2[i] = (i & 1) ? fe26_x2(f.v[i]) : f.v[i];
+  return r;
+}
+
+HSV_INL fe_g fe_prep_g(const fe &g) {
+#if defined(HSV_CHECK_BOUNDS) && !defined(__HIP_DEVICE_COMPILE__)
+  for (int i = 0; i < 10; ++i) HSV_BOUND(g.v[i] <= fe26_gmax(i), "fe_mul g operand too large");
+#endif
+  fe_g r;
+  r.v = g;
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) r.x19[i] = g.v[i] * 19u;
+  return r;
+}
+
+// f g from prepared operands (sequential carry, as fe_mul)
+HSV_INL fe fe_mul_p(const fe_f &f, const fe_g &g) {
+  HSV_SCHED_FENCE();
+#if defined(HSV_CHECK_BOUNDS) && !defined(__HIP_DEVICE_COMPILE__)
+  fe26_check_columns(f.v, g.v);
+#endif
+  fe r;
+  uint64_t acc = 0;
+#define HSV_MULC(K)                                         \
+  acc = fe26_mul_column<K>(f.v.v, f.x2, g.v.v, g.x19, acc); \
+  r.v[K] = (uint32_t)acc & fe26_mask(K);                    \
+  acc >>= fe26_bits(K);
+  HSV_MULC(0) HSV_MULC(1) HSV_MULC(2) HSV_MULC(3) HSV_MULC(4)
+  HSV_MULC(5) HSV_MULC(6) HSV_MULC(7) HSV_MULC(8) HSV_MULC(9)
+#undef HSV_MULC
+  fe26_wrap_carry(r, acc);
+  HSV_SCHED_FENCE();
+  return r;
+}
+
+// r = f g and s = h k from prepared operands, interleaved (fe_mul2)
+HSV_INL void fe_mul2_p(const fe_f &f, const fe_g &g, const fe_f &h, const fe_g &k, fe &r, fe &s) {
+  HSV_SCHED_FENCE();
+#if defined(HSV_CHECK_BOUNDS) && !defined(__HIP_DEVICE_COMPILE__)
+  fe26_check_columns(f.v, g.v);
+  fe26_check_columns(h.v, k.v);
+#endif
+  uint64_t a0 = 0, a1 = 0;
+#define HSV_MULC2(K)                                        \
+  a0 = fe26_mul_column<K>(f.v.v, f.x2, g.v.v, g.x19, a0);   \
+  a1 = fe26_mul_column<K>(h.v.v, h.x2, k.v.v, k.x19, a1);   \
+  r.v[K] = (uint32_t)a0 & fe26_mask(K);                     \
+  a0 >>= fe26_bits(K);                                      \
+  s.v[K] = (uint32_t)a1 & fe26_mask(K);                     \
+  a1 >>= fe26_bits(K);
+  HSV_MULC2(0) HSV_MULC2(1) HSV_MULC2(2) HSV_MULC2(3) HSV_MULC2(4)
+  HSV_MULC2(5) HSV_MULC2(6) HSV_MULC2(7) HSV_MULC2(8) HSV_MULC2(9)
+#undef HSV_MULC2
+  fe26_wrap_carry(r, a0);
+  fe26_wrap_carry(s, a1);
+  HSV_SCHED_FENCE();
 }
 
 // operands of the product f_i f_j (i <= j) in a squaring, with its factor
@@ -355,13 +469,11 @@ HSV_INL uint64_t fe26_sq_column(const uint32_t *f, const uint32_t *f2, const uin
   return fe26_chain<N, ZERO>(ca, cb, acc);
 }
 
-HSV_INL fe fe_sq(const fe &f) {
-  HSV_SCHED_FENCE();
+HSV_INL void fe26_sq_prescale(const fe &f, uint32_t f2[10], uint32_t f19[10], uint32_t f38[10]) {
 #if defined(HSV_CHECK_BOUNDS) && !defined(__HIP_DEVICE_COMPILE__)
   for (int i = 0; i < 10; ++i) HSV_BOUND(f.v[i] <= fe26_gmax(i), "fe_sq operand too large");
   fe26_check_columns(f, f);
 #endif
-  uint32_t f2[10], f19[10], f38[10];
   HSV_UNROLL
   for (int i = 0; i < 10; ++i) {
     f2[i] = fe26_x2(f.v[i]);
@@ -370,6 +482,12 @@ HSV_INL fe fe_sq(const fe &f) {
     f19[i] = i >= 5 ? f.v[i] * 19u : 0u;
     f38[i] = (i >= 5 && (i & 1)) ? fe26_x2(f19[i]) : 0u;
   }
+}
+
+HSV_INL fe fe_sq(const fe &f) {
+  HSV_SCHED_FENCE();
+  uint32_t f2[10], f19[10], f38[10];
+  fe26_sq_prescale(f, f2, f19, f38);
 #ifdef HSV_FE26_PARALLEL_CARRY
   uint64_t h[10];
   HSV_UNROLL
@@ -402,6 +520,28 @@ HSV_INL fe fe_sq(const fe &f) {
 #endif
   HSV_SCHED_FENCE();
   return r;
+}
+
+// Two independent squarings ra = a^2, rb = b^2 interleaved (see fe_mul2).
+HSV_INL void fe_sq2(const fe &a, const fe &b, fe &ra, fe &rb) {
+  HSV_SCHED_FENCE();
+  uint32_t a2[10], a19[10], a38[10], b2[10], b19[10], b38[10];
+  fe26_sq_prescale(a, a2, a19, a38);
+  fe26_sq_prescale(b, b2, b19, b38);
+  uint64_t x0 = 0, x1 = 0;
+#define HSV_SQC2(K)                                  \
+  x0 = fe26_sq_column<K>(a.v, a2, a19, a38, x0);     \
+  x1 = fe26_sq_column<K>(b.v, b2, b19, b38, x1);     \
+  ra.v[K] = (uint32_t)x0 & fe26_mask(K);             \
+  x0 >>= fe26_bits(K);                               \
+  rb.v[K] = (uint32_t)x1 & fe26_mask(K);             \
+  x1 >>= fe26_bits(K);
+  HSV_SQC2(0) HSV_SQC2(1) HSV_SQC2(2) HSV_SQC2(3) HSV_SQC2(4)
+  HSV_SQC2(5) HSV_SQC2(6) HSV_SQC2(7) HSV_SQC2(8) HSV_SQC2(9)
+#undef HSV_SQC2
+  fe26_wrap_carry(ra, x0);
+  fe26_wrap_carry(rb, x1);
+  HSV_SCHED_FENCE();
 }
 
 // Unique representative in [0, p), limbs exact.

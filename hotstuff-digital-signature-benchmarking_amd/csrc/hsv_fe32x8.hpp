@@ -169,6 +169,30 @@ HSV_INL fe fe_sq(const fe &a) {
   return r;
 }
 
+// prepared operands and paired forms (the radix-26 field prescales operands
+// once and interleaves the two products; here they are plain products)
+struct fe_f {
+  fe v;
+};
+struct fe_g {
+  fe v;
+};
+HSV_INL fe_f fe_prep_f(const fe &f) { return fe_f{f}; }
+HSV_INL fe_g fe_prep_g(const fe &g) { return fe_g{g}; }
+HSV_INL fe fe_mul_p(const fe_f &f, const fe_g &g) { return fe_mul(f.v, g.v); }
+HSV_INL void fe_mul2_p(const fe_f &f, const fe_g &g, const fe_f &h, const fe_g &k, fe &r, fe &s) {
+  r = fe_mul(f.v, g.v);
+  s = fe_mul(h.v, k.v);
+}
+HSV_INL void fe_mul2(const fe &f, const fe &g, const fe &h, const fe &k, fe &r, fe &s) {
+  r = fe_mul(f, g);
+  s = fe_mul(h, k);
+}
+HSV_INL void fe_sq2(const fe &a, const fe &b, fe &ra, fe &rb) {
+  ra = fe_sq(a);
+  rb = fe_sq(b);
+}
+
 // Unique representative in [0, p).
 HSV_INL fe fe_canon(const fe &a) {
   fe r = a;

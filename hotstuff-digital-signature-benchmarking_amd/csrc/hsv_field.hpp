@@ -127,6 +127,75 @@ HSV_INL fe fe_pow22523(const fe &z) {
   return fe_mul(t0, z);                // 2^252 - 3
 }
 
+// Paired forms for two independent inputs (two root chains per lane run as
+// interleaved pairs of squarings / products: fe_sq2, fe_mul2).
+HSV_INL void fe_sqn2(fe &a, fe &b, int n) {
+  if (n & 1) {
+    fe x, y;
+    fe_sq2(a, b, x, y);
+    a = x;
+    b = y;
+  }
+  // two steps per trip: the values return to (a, b) without register copies
+  HSV_NOUNROLL
+  for (int i = 0; i < n / 2; ++i) {
+    fe x, y;
+    fe_sq2(a, b, x, y);
+    fe_sq2(x, y, a, b);
+  }
+}
+
+HSV_INL void fe_mul2_inplace(fe &a, const fe &ga, fe &b, const fe &gb) {
+  fe x, y;
+  fe_mul2(a, ga, b, gb, x, y);
+  a = x;
+  b = y;
+}
+
+// (z^((p-5)/8), w^((p-5)/8)), the chain of fe_pow22523 on both inputs
+HSV_INL void fe_pow22523_2(const fe &z, const fe &w, fe &rz, fe &rw) {
+#ifdef HSV_TIMING_STUB_SQRT
+  rz = z;
+  rw = w;
+  return;
+#endif
+  fe t0z, t0w, t1z, t1w, t2z, t2w;
+  fe_sq2(z, w, t0z, t0w);                                    // 2
+  t1z = t0z;
+  t1w = t0w;
+  fe_sqn2(t1z, t1w, 2);                                      // 8
+  fe_mul2_inplace(t1z, z, t1w, w);                           // 9
+  fe_mul2_inplace(t0z, t1z, t0w, t1w);                       // 11
+  fe_sqn2(t0z, t0w, 1);                                      // 22
+  fe_mul2_inplace(t0z, t1z, t0w, t1w);                       // 31 = 2^5 - 1
+  t1z = t0z;
+  t1w = t0w;
+  fe_sqn2(t1z, t1w, 5);
+  fe_mul2_inplace(t0z, t1z, t0w, t1w);                       // 2^10 - 1
+  t1z = t0z;
+  t1w = t0w;
+  fe_sqn2(t1z, t1w, 10);
+  fe_mul2_inplace(t1z, t0z, t1w, t0w);                       // 2^20 - 1
+  t2z = t1z;
+  t2w = t1w;
+  fe_sqn2(t2z, t2w, 20);
+  fe_mul2_inplace(t1z, t2z, t1w, t2w);                       // 2^40 - 1
+  fe_sqn2(t1z, t1w, 10);
+  fe_mul2_inplace(t0z, t1z, t0w, t1w);                       // 2^50 - 1
+  t1z = t0z;
+  t1w = t0w;
+  fe_sqn2(t1z, t1w, 50);
+  fe_mul2_inplace(t1z, t0z, t1w, t0w);                       // 2^100 - 1
+  t2z = t1z;
+  t2w = t1w;
+  fe_sqn2(t2z, t2w, 100);
+  fe_mul2_inplace(t1z, t2z, t1w, t2w);                       // 2^200 - 1
+  fe_sqn2(t1z, t1w, 50);
+  fe_mul2_inplace(t0z, t1z, t0w, t1w);                       // 2^250 - 1
+  fe_sqn2(t0z, t0w, 2);                                      // 2^252 - 4
+  fe_mul2(t0z, z, t0w, w, rz, rw);                           // 2^252 - 3
+}
+
 // z^(p-2) = z^(2^255 - 21): inversion (host-side signing / encoding only)
 HSV_INL fe fe_invert(const fe &z) {
   fe t0 = fe_sq(z);                    // 2

@@ -56,108 +56,72 @@ HSV_INL ge_cached ge_to_cached(const ge_ext &p) {
   return r;
 }
 
+// The four output products of every formula below, from E, F, G, H:
+//   X3 = E F,  Y3 = G H,  Z3 = G F,  T3 = E H,
+// each operand prescaled once (E, G as f; F, H as g) and the products taken
+// in interleaved pairs (fe_mul2_p).  Without T, r.T is left holding Z3.
+HSV_INL ge_ext ge_finish_rt(const fe &E, const fe &F, const fe &G, const fe &H, bool with_t) {
+  const fe_f Ef = fe_prep_f(E), Gf = fe_prep_f(G);
+  const fe_g Fg = fe_prep_g(F), Hg = fe_prep_g(H);
+  ge_ext r;
+  fe_mul2_p(Ef, Fg, Gf, Hg, r.X, r.Y);
+  if (with_t) {
+    fe_mul2_p(Gf, Fg, Ef, Hg, r.Z, r.T);
+  } else {
+    r.Z = fe_mul_p(Gf, Fg);
+    r.T = r.Z;
+  }
+  return r;
+}
+
 // 2P.  with_t = false skips T3 (saves one multiply when the next op is a doubling).
 // Operand classes (hsv_fe26x10.hpp): X, Y, Z in R.  H, C in S2, G in D,
 // E = H - S in 4R (used only as the unscaled f operand), F carried to R.
+// The four squarings run as two interleaved pairs.
+HSV_INL ge_ext ge_dbl_rt(const ge_ext &p, bool with_t) {
+  fe A, B, C, S;
+  fe_sq2(p.X, p.Y, A, B);
+  fe_sq2(p.Z, fe_add(p.X, p.Y), C, S);
+  C = fe_add(C, C);
+  const fe H = fe_add(A, B);
+  const fe E = fe_sub(H, S);
+  const fe G = fe_sub(A, B);
+  const fe F = fe_carry(fe_add(C, G));
+  return ge_finish_rt(E, F, G, H, with_t);
+}
+
 template <bool with_t>
 HSV_INL ge_ext ge_dbl(const ge_ext &p) {
-  fe A = fe_sq(p.X);
-  fe B = fe_sq(p.Y);
-  fe C = fe_sq(p.Z);
-  C = fe_add(C, C);
-  fe H = fe_add(A, B);
-  fe xy = fe_add(p.X, p.Y);
-  fe E = fe_sub(H, fe_sq(xy));
-  fe G = fe_sub(A, B);
-  fe F = fe_carry(fe_add(C, G));
-  ge_ext r;
-  r.X = fe_mul(E, F);
-  r.Y = fe_mul(G, H);
-  r.Z = fe_mul(F, G);
-  if (with_t) r.T = fe_mul(E, H);
-  else r.T = fe_small(0);
+  ge_ext r = ge_dbl_rt(p, with_t);
+  if (!with_t) r.T = fe_small(0);
   return r;
 }
 
 // P + Q with Q cached.  P in R; Q.YpX / Q.YmX in S2 / D (swapped when
 // negated), Q.Z2 in S2, Q.T2d in R (2R when negated).  E, F in D; G, H in S2.
+HSV_INL ge_ext ge_add_cached_rt(const ge_ext &p, const ge_cached &q, bool with_t) {
+  fe A, B, C, D;
+  fe_mul2(fe_sub(p.Y, p.X), q.YmX, fe_add(p.Y, p.X), q.YpX, A, B);
+  fe_mul2(p.T, q.T2d, p.Z, q.Z2, C, D);
+  return ge_finish_rt(fe_sub(B, A), fe_sub(D, C), fe_add(D, C), fe_add(B, A), with_t);
+}
+
 template <bool with_t>
 HSV_INL ge_ext ge_add_cached(const ge_ext &p, const ge_cached &q) {
-  fe A = fe_mul(fe_sub(p.Y, p.X), q.YmX);
-  fe B = fe_mul(fe_add(p.Y, p.X), q.YpX);
-  fe C = fe_mul(p.T, q.T2d);
-  fe D = fe_mul(p.Z, q.Z2);
-  fe E = fe_sub(B, A);
-  fe F = fe_sub(D, C);
-  fe G = fe_add(D, C);
-  fe H = fe_add(B, A);
-  ge_ext r;
-  r.X = fe_mul(E, F);
-  r.Y = fe_mul(G, H);
-  r.Z = fe_mul(F, G);
-  if (with_t) r.T = fe_mul(E, H);
-  else r.T = fe_small(0);
+  ge_ext r = ge_add_cached_rt(p, q, with_t);
+  if (!with_t) r.T = fe_small(0);
   return r;
 }
 
 // P + Q with Q affine Niels (Z2 = 1).
 template <bool with_t>
 HSV_INL ge_ext ge_add_niels(const ge_ext &p, const ge_niels &q) {
-  fe A = fe_mul(fe_sub(p.Y, p.X), q.ymx);
-  fe B = fe_mul(fe_add(p.Y, p.X), q.ypx);
-  fe C = fe_mul(p.T, q.xy2d);
-  fe D = fe_carry(fe_add(p.Z, p.Z));  // minuend and subtrahend below: keep it in R
-  fe E = fe_sub(B, A);
-  fe F = fe_sub(D, C);
-  fe G = fe_add(D, C);
-  fe H = fe_add(B, A);
-  ge_ext r;
-  r.X = fe_mul(E, F);
-  r.Y = fe_mul(G, H);
-  r.Z = fe_mul(F, G);
-  if (with_t) r.T = fe_mul(E, H);
-  else r.T = fe_small(0);
-  return r;
-}
-
-// Runtime-flag forms of the two formulas above: one copy of the code serves
-// every doubling / addition of a loop (the T product sits behind a wave-
-// uniform branch), which keeps the main loop inside the instruction cache.
-// Without T, r.T is left holding an unrelated value that must not be read.
-HSV_INL ge_ext ge_dbl_rt(const ge_ext &p, bool with_t) {
-  fe A = fe_sq(p.X);
-  fe B = fe_sq(p.Y);
-  fe C = fe_sq(p.Z);
-  C = fe_add(C, C);
-  fe H = fe_add(A, B);
-  fe xy = fe_add(p.X, p.Y);
-  fe E = fe_sub(H, fe_sq(xy));
-  fe G = fe_sub(A, B);
-  fe F = fe_carry(fe_add(C, G));
-  ge_ext r;
-  r.X = fe_mul(E, F);
-  r.Y = fe_mul(G, H);
-  r.Z = fe_mul(F, G);
-  r.T = r.Z;
-  if (with_t) r.T = fe_mul(E, H);
-  return r;
-}
-
-HSV_INL ge_ext ge_add_cached_rt(const ge_ext &p, const ge_cached &q, bool with_t) {
-  fe A = fe_mul(fe_sub(p.Y, p.X), q.YmX);
-  fe B = fe_mul(fe_add(p.Y, p.X), q.YpX);
-  fe C = fe_mul(p.T, q.T2d);
-  fe D = fe_mul(p.Z, q.Z2);
-  fe E = fe_sub(B, A);
-  fe F = fe_sub(D, C);
-  fe G = fe_add(D, C);
-  fe H = fe_add(B, A);
-  ge_ext r;
-  r.X = fe_mul(E, F);
-  r.Y = fe_mul(G, H);
-  r.Z = fe_mul(F, G);
-  r.T = r.Z;
-  if (with_t) r.T = fe_mul(E, H);
+  fe A, B;
+  fe_mul2(fe_sub(p.Y, p.X), q.ymx, fe_add(p.Y, p.X), q.ypx, A, B);
+  const fe C = fe_mul(p.T, q.xy2d);
+  const fe D = fe_carry(fe_add(p.Z, p.Z));  // minuend and subtrahend below: keep it in R
+  ge_ext r = ge_finish_rt(fe_sub(B, A), fe_sub(D, C), fe_add(D, C), fe_add(B, A), with_t);
+  if (!with_t) r.T = fe_small(0);
   return r;
 }
 
@@ -179,12 +143,9 @@ HSV_INL ge_niels ge_niels_cneg(const ge_niels &q, uint32_t neg) {
   return r;
 }
 
-// curve25519-dalek FieldElement::sqrt_ratio_i: returns was_nonzero_square
-// (true also for u == 0) and the non-negative root r.
-HSV_INL uint32_t fe_sqrt_ratio_i(const fe &u, const fe &v, fe &r_out) {
-  fe v3 = fe_mul(fe_sq(v), v);
-  fe v7 = fe_mul(fe_sq(v3), v);
-  fe r = fe_mul(fe_mul(u, v3), fe_pow22523(fe_mul(u, v7)));
+// Tail of sqrt_ratio_i once the candidate root r = u v^3 (u v^7)^((p-5)/8)
+// is known: fix up by sqrt(-1), pick the non-negative root.
+HSV_INL uint32_t fe_sqrt_ratio_fix(const fe &u, const fe &v, fe r, fe &r_out) {
   fe check = fe_mul(v, fe_sq(r));
   fe neg_u = fe_neg(u);
   uint32_t correct = fe_eq(check, u);
@@ -195,6 +156,15 @@ HSV_INL uint32_t fe_sqrt_ratio_i(const fe &u, const fe &v, fe &r_out) {
   const uint32_t neg = fe_is_negative(r);
   r_out = fe_canon(fe_select(r, fe_neg(r), neg));
   return correct | flipped;
+}
+
+// curve25519-dalek FieldElement::sqrt_ratio_i: returns was_nonzero_square
+// (true also for u == 0) and the non-negative root r.
+HSV_INL uint32_t fe_sqrt_ratio_i(const fe &u, const fe &v, fe &r_out) {
+  fe v3 = fe_mul(fe_sq(v), v);
+  fe v7 = fe_mul(fe_sq(v3), v);
+  fe r = fe_mul(fe_mul(u, v3), fe_pow22523(fe_mul(u, v7)));
+  return fe_sqrt_ratio_fix(u, v, r, r_out);
 }
 
 // CompressedEdwardsY::decompress.  enc = 32 bytes as 8 little-endian words.
@@ -209,6 +179,38 @@ HSV_INL uint32_t ge_decompress(const uint32_t enc[8], fe &x, fe &y) {
   uint32_t sign = enc[7] >> 31;
   x = fe_canon(fe_select(x, fe_neg(x), sign));  // -0 == 0 is accepted (no rejection)
   return ok;
+}
+
+// Two decompressions (R and A of one signature) with their root chains run
+// as interleaved pairs (fe_pow22523_2); results as two ge_decompress calls.
+HSV_INL void ge_decompress2(const uint32_t ea[8], const uint32_t eb[8], fe &xa, fe &ya, fe &xb, fe &yb,
+                            uint32_t &oka, uint32_t &okb) {
+  ya = fe_from_words_masked(ea);
+  yb = fe_from_words_masked(eb);
+  fe yya, yyb;
+  fe_sq2(ya, yb, yya, yyb);
+  const fe ua = fe_carry(fe_sub(yya, fe_small(1))), ub = fe_carry(fe_sub(yyb, fe_small(1)));
+  fe va, vb;
+  fe_mul2(yya, fe_d(), yyb, fe_d(), va, vb);
+  va = fe_add(va, fe_small(1));
+  vb = fe_add(vb, fe_small(1));
+  fe sa, sb, v3a, v3b, v7a, v7b;
+  fe_sq2(va, vb, sa, sb);
+  fe_mul2(sa, va, sb, vb, v3a, v3b);  // v^3
+  fe_sq2(v3a, v3b, sa, sb);
+  fe_mul2(sa, va, sb, vb, v7a, v7b);  // v^7
+  fe wa, wb;
+  fe_mul2(ua, v7a, ub, v7b, wa, wb);
+  fe pa, pb;
+  fe_pow22523_2(wa, wb, pa, pb);
+  fe ta, tb;
+  fe_mul2(ua, v3a, ub, v3b, ta, tb);
+  fe ra, rb;
+  fe_mul2(ta, pa, tb, pb, ra, rb);
+  oka = fe_sqrt_ratio_fix(ua, va, ra, xa);
+  okb = fe_sqrt_ratio_fix(ub, vb, rb, xb);
+  xa = fe_canon(fe_select(xa, fe_neg(xa), ea[7] >> 31));
+  xb = fe_canon(fe_select(xb, fe_neg(xb), eb[7] >> 31));
 }
 
 // [8]P == O  <=>  canonical y in {0, 1, p-1, y8, p-y8}  (the y values of E[8])

@@ -228,16 +228,12 @@ HSV_INL uint32_t verify_one_prepped(const uint32_t pk[8], const uint32_t rb[8], 
   constexpr int TS = 1 << (WA - 1);
   uint32_t a_ok, small_a, r_ok, small_r;
   {
-    fe x, y;
-    r_ok = ge_decompress(rb, x, y);
-    small_r = r_ok & y_is_small_order(y);
-    vt_build<TS>(vt, 0, fe_carry(fe_neg(x)), y);
-  }
-  {
-    fe x, y;
-    a_ok = ge_decompress(pk, x, y);
-    small_a = a_ok & y_is_small_order(y);
-    vt_build<TS>(vt, 1, fe_carry(fe_neg(x)), y);
+    fe xr, yr, xa, ya;
+    ge_decompress2(rb, pk, xr, yr, xa, ya, r_ok, a_ok);  // both root chains at once
+    small_r = r_ok & y_is_small_order(yr);
+    small_a = a_ok & y_is_small_order(ya);
+    vt_build<TS>(vt, 0, fe_carry(fe_neg(xr)), yr);
+    vt_build<TS>(vt, 1, fe_carry(fe_neg(xa)), ya);
   }
   uint32_t d[2][5];
   HSV_UNROLL

@@ -87,7 +87,7 @@ def core_host32():
     return _build(BIN + "32", "-DHSV_FE_RADIX=32")
 
 
-@pytest.mark.parametrize("variant", [0, 1, 10, 11, 12, 14, 16, 18, 20])
+@pytest.mark.parametrize("variant", [0, 1, 10, 11, 12, 14, 16, 18, 20, 21])
 def test_operand_bounds_hold_on_edge_and_sample(core_host_checked, golden, variant):
     """Bound-checked build over every edge vector and a random sample: no field
     operand leaves its class and no 64-bit column sum overflows."""
@@ -153,7 +153,7 @@ def test_lattice_reduction_properties(core_host):
     assert n_ok >= len(ks) - 8
 
 
-@pytest.mark.parametrize("variant", [16, 17, 20])
+@pytest.mark.parametrize("variant", [16, 17, 20, 21])
 def test_lattice_fallback_records(core_host, fallback_records, variant):
     """Records built on challenges the lattice reduction rejects: the half-size
     path hands them to the full-length path (reported on stderr) and the flags
