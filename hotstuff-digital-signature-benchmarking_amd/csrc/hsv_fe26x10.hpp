@@ -597,6 +597,54 @@ HSV_INL void fe_pack(const fe &a, uint32_t w[8]) {
   }
 }
 
+// Loose 256-bit encoding for values kept in memory only to be read back into
+// arithmetic (the per-lane point tables): one sequential carry pass instead of
+// fe_canon, so the value is exact but not necessarily < p.  After the pass
+// limbs 0 and 2..9 fit their widths and limb 1 fits 26 bits (it takes the one
+// carry out of the wrapped limb 0), so the widths 26,26,26,25,26,25,26,25,26,25
+// fill exactly 256 bits.  Input: limbs < 2^31.
+HSV_INL constexpr int fe26_loose_bits(int i) { return i < 3 ? 26 : fe26_bits(i); }
+HSV_INL constexpr int fe26_loose_off(int i) { return i == 0 ? 0 : fe26_loose_off(i - 1) + fe26_loose_bits(i - 1); }
+
+HSV_INL void fe_pack_loose(const fe &a, uint32_t w[8]) {
+  uint32_t h[10];
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) h[i] = a.v[i];
+  fe26_carry_step<0>(h);
+  fe26_carry_step<1>(h);
+  fe26_carry_step<2>(h);
+  fe26_carry_step<3>(h);
+  fe26_carry_step<4>(h);
+  fe26_carry_step<5>(h);
+  fe26_carry_step<6>(h);
+  fe26_carry_step<7>(h);
+  fe26_carry_step<8>(h);
+  fe26_carry_wrap(h);
+  fe26_carry_step<0>(h);
+  HSV_BOUND(h[1] < (1u << 26), "fe_pack_loose limb 1");
+  HSV_UNROLL
+  for (int j = 0; j < 8; ++j) w[j] = 0;
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) {
+    const int off = fe26_loose_off(i), wi = off >> 5, sh = off & 31;
+    w[wi] |= h[i] << sh;
+    if (sh + fe26_loose_bits(i) > 32) w[wi + 1] |= h[i] >> (32 - sh);
+  }
+}
+
+HSV_INL fe fe_unpack_loose(const uint32_t w[8]) {
+  fe r;
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) {
+    const int off = fe26_loose_off(i), wi = off >> 5, sh = off & 31;
+    const uint32_t lo = w[wi];
+    const uint32_t hi = (wi + 1 < 8) ? w[wi + 1] : 0u;
+    const uint32_t x = sh ? ((lo >> sh) | (hi << ((32 - sh) & 31))) : lo;
+    r.v[i] = x & ((1u << fe26_loose_bits(i)) - 1u);
+  }
+  return r;
+}
+
 HSV_INL uint32_t fe_canon_low_bit(const fe &a) { return fe_canon(a).v[0] & 1u; }
 
 HSV_INL uint32_t fe_is_zero(const fe &a) {

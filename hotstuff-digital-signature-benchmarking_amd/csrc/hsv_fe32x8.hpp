@@ -266,4 +266,8 @@ HSV_INL void fe_pack(const fe &a, uint32_t w[8]) {
 
 HSV_INL uint32_t fe_canon_low_bit(const fe &a) { return fe_canon(a).v[0] & 1u; }
 
+// memory encoding of table entries (the radix-26 field has a cheaper loose form)
+HSV_INL void fe_pack_loose(const fe &a, uint32_t w[8]) { fe_pack(a, w); }
+HSV_INL fe fe_unpack_loose(const uint32_t w[8]) { return fe_from_words_masked(w); }
+
 }  // namespace hsv

@@ -123,17 +123,31 @@ hsv_verify_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
 #endif  // HSV_ALL_VARIANTS
 
 // Per-lane variable-base tables in global memory (hsv_verify_core.hpp, VT):
-// lane region = 2 tables x ENT entries x 128 B, entry = 8 x uint4.
+// lane region = 2 tables x (ENT - 1) entries x 128 B, entry = 8 x uint4.
+// Entry 0 of every table is the identity: it is not stored per lane; a zero
+// digit reads this one shared line (L2-resident) instead.  Loose encoding of
+// (Y+X, Y-X, 2Z, 2dT) = (1, 1, 2, 0).
+__device__ const uint4 kVtIdentity[8] = {{1u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {1u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u},
+                                         {2u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
+
 template <int ENT>
 struct GlobalVarTab {
+  static constexpr int kStored = ENT - 1;  // entries 1 .. ENT-1 per table
   uint4 *base;
   __device__ __forceinline__ void put(int t, int m, const uint32_t w[32]) const {
-    uint4 *e = base + (t * ENT + m) * 8;
+    if (m == 0) return;
+    uint4 *e = base + (t * kStored + m - 1) * 8;
     HSV_UNROLL
-    for (int q = 0; q < 8; ++q) e[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    for (int q = 0; q < 8; ++q) {
+#ifdef HSV_TIMING_STUB_TABLE_STORES  // timing probe only: entries computed, never stored
+      asm volatile("" ::"v"(w[4 * q]), "v"(w[4 * q + 1]), "v"(w[4 * q + 2]), "v"(w[4 * q + 3]));
+#else
+      e[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+#endif
+    }
   }
   __device__ __forceinline__ void get(int t, uint32_t m, uint32_t w[32]) const {
-    const uint4 *e = base + (t * ENT + (int)m) * 8;
+    const uint4 *e = m ? base + (t * kStored + (int)m - 1) * 8 : kVtIdentity;
     HSV_UNROLL
     for (int q = 0; q < 8; ++q) {
       const uint4 v = e[q];
@@ -143,7 +157,7 @@ struct GlobalVarTab {
 };
 
 template <int WA>
-constexpr int vt_lane_uint4() { return 2 * ((1 << (WA - 1)) + 1) * 8; }
+constexpr int vt_lane_uint4() { return 2 * (1 << (WA - 1)) * 8; }
 
 #if HSV_ALL_VARIANTS
 // Half-size scalars with memory-resident variable-base tables.  Persistent

@@ -369,31 +369,37 @@ HSV_INL uint32_t verify_one_half(const uint32_t pk[8], const uint32_t sig[16], c
 // and a register-resident table is read with TS x 40 v_cndmask per addition.
 // Instead each lane writes its tables once to a private region (VT) and reads
 // one entry per addition by index: 8 x 16-byte loads issued a whole window
-// (WA doublings) ahead of their use, no selects.  Entries are packed
-// canonical field elements, 4 x 8 words = 128 bytes (one cache line).
+// (WA doublings) ahead of their use, no selects.  Entries are 4 field
+// elements in the loose 256-bit encoding, 4 x 8 words = 128 bytes (one
+// cache line).
 //   VT::put(t, m, const uint32_t w[32])   store entry m of table t
 //   VT::get(t, m, uint32_t w[32])         load it back
 // Entry 0 is the identity, so a zero digit needs no special case.
 
+// Entries use the loose 256-bit encoding (fe_pack_loose: one carry pass, no
+// reduction below p); the limbs read back are class R.
 HSV_INL void cached_pack(const ge_cached &c, uint32_t w[32]) {
-  fe_pack(c.YpX, w);
-  fe_pack(c.YmX, w + 8);
-  fe_pack(c.Z2, w + 16);
-  fe_pack(c.T2d, w + 24);
+  fe_pack_loose(c.YpX, w);
+  fe_pack_loose(c.YmX, w + 8);
+  fe_pack_loose(c.Z2, w + 16);
+  fe_pack_loose(c.T2d, w + 24);
 }
 
 HSV_INL ge_cached cached_unpack(const uint32_t w[32]) {
   ge_cached c;
-  c.YpX = fe_from_words_masked(w);
-  c.YmX = fe_from_words_masked(w + 8);
-  c.Z2 = fe_from_words_masked(w + 16);
-  c.T2d = fe_from_words_masked(w + 24);
+  c.YpX = fe_unpack_loose(w);
+  c.YmX = fe_unpack_loose(w + 8);
+  c.Z2 = fe_unpack_loose(w + 16);
+  c.T2d = fe_unpack_loose(w + 24);
   return c;
 }
 
 // table t of VT <- [0..TS]P for the affine point (x, y)
 template <int TS, class VT>
 HSV_INL void vt_build(VT &vt, int t, const fe &x, const fe &y) {
+#ifdef HSV_TIMING_STUB_TABLES  // tools/phase_probe.py only: tables left unwritten
+  return;
+#endif
   uint32_t w[32];
   cached_pack(ge_cached_identity(), w);
   vt.put(t, 0, w);

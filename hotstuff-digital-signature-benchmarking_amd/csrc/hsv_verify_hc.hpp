@@ -29,6 +29,9 @@ namespace hsv {
 template <int CB>
 HSV_INL ge_ext comb_add_b(ge_ext q, const uint32_t s[8], const uint32_t *tb) {
   static_assert(CB == 8 || CB == 16, "comb digit width");
+#ifdef HSV_TIMING_STUB_COMB  // tools/phase_probe.py only
+  return q;
+#endif
   constexpr int NP = 256 / CB;
   constexpr int ENT = 1 << (CB - 1);
   uint32_t sr[9];
@@ -60,12 +63,40 @@ HSV_INL uint32_t flags_byte(uint32_t s_ok, uint32_t a_ok, uint32_t r_ok, uint32_
 // Returns the accumulator with T valid (the comb phase follows).
 // flip_last: negate every digit of the last scalar (its table holds the
 // negated base).
+// Leading windows whose digits are zero in every lane of the wave only add
+// the identity to the identity and are skipped (wave-uniform: the window
+// count is the wave's largest scalar).  The lattice outputs of a 64-lane
+// wave fit 131 bits in ~88% of waves, which drops the top window and its
+// four doublings (tools/lattice_bits.py).
+template <class T>
+HSV_INL bool wave_any(T c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __ballot(c != 0) != 0;
+#else
+  return c != 0;
+#endif
+}
+
 template <int WA, int NW, int L, int NV, bool PREFETCH, class VT>
 HSV_INL ge_ext straus_vt(uint32_t d[NV][L], VT &vt, uint32_t flip_last = 0) {
   constexpr int TS = 1 << (WA - 1);
   ge_ext q = ge_identity();
+#ifdef HSV_TIMING_STUB_STRAUS  // tools/phase_probe.py only: wrong results, timing share of the window loop
+  return q;
+#endif
+  int top = NW - 1;
   HSV_NOUNROLL
-  for (int i = NW - 1; i >= 0; --i) {
+  while (top > 0) {
+    uint32_t nz = 0;
+    HSV_UNROLL
+    for (int v = 0; v < NV; ++v) nz |= (d[v][L - 1] >> (32 - WA)) ^ (uint32_t)TS;
+    if (wave_any(nz)) break;
+    HSV_UNROLL
+    for (int v = 0; v < NV; ++v) limbs_shl<L>(d[v], WA);
+    --top;
+  }
+  HSV_NOUNROLL
+  for (int i = top; i >= 0; --i) {
     uint32_t m[NV], neg[NV];
     HSV_UNROLL
     for (int v = 0; v < NV; ++v) {
@@ -78,7 +109,7 @@ HSV_INL ge_ext straus_vt(uint32_t d[NV][L], VT &vt, uint32_t flip_last = 0) {
       uint32_t w[NV][32];
       HSV_UNROLL
       for (int v = 0; v < NV; ++v) vt.get(v, m[v], w[v]);
-      if (i != NW - 1) {
+      if (i != top) {
         HSV_NOUNROLL
         for (int j = 0; j < WA; ++j) q = ge_dbl_rt(q, j == WA - 1);
       }
@@ -97,7 +128,7 @@ HSV_INL ge_ext straus_vt(uint32_t d[NV][L], VT &vt, uint32_t flip_last = 0) {
     } else {
       // entries loaded right before their addition (fewer live registers;
       // latency left to the other waves of the SIMD)
-      if (i != NW - 1) {
+      if (i != top) {
         HSV_NOUNROLL
         for (int j = 0; j < WA; ++j) q = ge_dbl_rt(q, j == WA - 1);
       }
