@@ -739,6 +739,10 @@ hipError_t launch_mt(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
 
 #endif  // HSV_ALL_VARIANTS
 
+#ifndef HSV_HP_WAVES
+#define HSV_HP_WAVES 3  // waves per SIMD of the point pass (launch bounds: 168 VGPRs)
+#endif
+
 // Two-pass launch (variants 19/20): prepass over all items, then the
 // persistent point pass.  Workspace: per-lane tables | counters (256 B) |
 // fallback list (4 B per item) | prep records (kPrepWords x 4 B per item).
@@ -874,7 +878,7 @@ extern "C" hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t
     case 21:
       if (n <= kPairMax)
         return launch_pair<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
-      return launch_hp<4, 3, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
+      return launch_hp<4, HSV_HP_WAVES, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
 #if HSV_ALL_VARIANTS
     default: break;
 #else
