@@ -16,13 +16,19 @@
 //   SignatureService::request_signature       lib.rs:229-254 -> crypto::SignatureService
 //
 // `Result` carries Ok or Err(CryptoError) exactly like Result<(), CryptoError>.
-// An infrastructure failure (no GPU, HIP error) is NOT an Err: it throws
-// crypto::InfrastructureError, so a broken device can never look like a
-// rejected signature.
+// An infrastructure failure (no GPU, HIP error) is NOT an Err: by default it
+// throws crypto::InfrastructureError, so a broken device can never look like a
+// rejected signature.  A deployment that must keep running through a device
+// fault installs an InfrastructureFallback (set_infrastructure_fallback): a
+// host verifier with the same semantics (ed25519-dalek in the Rust shim,
+// INTEGRATION.md section 2) that is consulted ONLY for calls libhsv could not
+// run, never to second-guess a rejection; every use is counted.  libhsv itself
+// has no CPU path.
 #ifndef HSV_CRYPTO_HPP_
 #define HSV_CRYPTO_HPP_
 
 #include <array>
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <cstring>
@@ -49,6 +55,25 @@ inline int check_infra(int rc, const char *what) {
   if (rc < 0) throw InfrastructureError(std::string(what) + ": " + hsv_last_error());
   return rc;
 }
+
+// Infrastructure-failure policy of the caller (see the header comment).
+// Install once at startup, before verify calls run on other threads.
+struct InfrastructureFallback {
+  // verify_strict over one 32-byte digest; true = Ok
+  std::function<bool(const uint8_t *digest, const uint8_t *pk, const uint8_t *sig)> verify_strict;
+  // the deterministic verify_batch rule over packed 96-byte pk || R || s votes
+  std::function<bool(const uint8_t *digest, const uint8_t *votes, size_t n)> verify_batch;
+};
+
+inline InfrastructureFallback &infrastructure_fallback() {
+  static InfrastructureFallback f;
+  return f;
+}
+inline std::atomic<uint64_t> &infrastructure_fallback_uses() {
+  static std::atomic<uint64_t> n{0};
+  return n;
+}
+inline void set_infrastructure_fallback(InfrastructureFallback f) { infrastructure_fallback() = std::move(f); }
 
 // ed25519::Error: opaque.
 struct CryptoError {
@@ -203,8 +228,12 @@ class Signature {
   // Signature::verify (lib.rs:204-208): ed25519-dalek verify_strict semantics.
   Result verify(const Digest &digest, const PublicKey &public_key) const {
     const std::array<uint8_t, 64> f = flatten();
-    const int rc = check_infra(hsv_verify_strict(digest.bytes.data(), public_key.bytes.data(), f.data()),
-                               "hsv_verify_strict");
+    int rc = hsv_verify_strict(digest.bytes.data(), public_key.bytes.data(), f.data());
+    if (rc < 0 && infrastructure_fallback().verify_strict) {
+      ++infrastructure_fallback_uses();
+      rc = infrastructure_fallback().verify_strict(digest.bytes.data(), public_key.bytes.data(), f.data()) ? 1 : 0;
+    }
+    check_infra(rc, "hsv_verify_strict");
     return rc == 1 ? Result::ok() : Result::err();
   }
 
@@ -216,8 +245,12 @@ class Signature {
       std::memcpy(packed.data() + 96 * i + 32, votes[i].second.part1.data(), 32);
       std::memcpy(packed.data() + 96 * i + 64, votes[i].second.part2.data(), 32);
     }
-    const int rc = check_infra(hsv_verify_batch_packed(digest.bytes.data(), packed.data(), votes.size()),
-                               "hsv_verify_batch_packed");
+    int rc = hsv_verify_batch_packed(digest.bytes.data(), packed.data(), votes.size());
+    if (rc < 0 && infrastructure_fallback().verify_batch) {
+      ++infrastructure_fallback_uses();
+      rc = infrastructure_fallback().verify_batch(digest.bytes.data(), packed.data(), votes.size()) ? 1 : 0;
+    }
+    check_infra(rc, "hsv_verify_batch_packed");
     return rc == 1 ? Result::ok() : Result::err();
   }
 };

@@ -2,6 +2,13 @@
 // and consensus verify_valid_qc (consensus/src/tests/messages_tests.rs:8-10),
 // written against include/hsv_crypto.hpp (the C++ mirror of the crate) and
 // run on the GPU through libhsv.so.  Exit code 0 = all passed.
+//
+// --fallback installs the caller-side infrastructure-failure policy
+// (crypto::set_infrastructure_fallback) with the C oracle
+// (oracle/ed25519_oracle.c, test infrastructure standing in for the host
+// ed25519-dalek a real shim would call) and prints how often it was used: on
+// a machine without a GPU every verify goes to it and the tests still pass;
+// on a GPU it must never be used.
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -9,6 +16,10 @@
 
 #include "hsv_crypto.hpp"
 #include "hsv_sha512.hpp"  // test-only: Hash for &[u8] = SHA-512(msg)[..32]
+
+extern "C" {  // oracle/ed25519_oracle.c (linked only into this test binary)
+uint8_t oracle_verify_flags(const uint8_t pk[32], const uint8_t sig[64], const uint8_t *msg, size_t msg_len);
+}
 
 using namespace crypto;
 
@@ -168,7 +179,24 @@ static void verify_valid_qc() {
   CHECK(Signature::verify_batch(qc_digest, {}).is_ok());
 }
 
-int main() {
+static void install_oracle_fallback() {
+  InfrastructureFallback f;
+  f.verify_strict = [](const uint8_t *digest, const uint8_t *pk, const uint8_t *sig) {
+    return (oracle_verify_flags(pk, sig, digest, 32) & HSV_STRICT_OK) != 0;
+  };
+  f.verify_batch = [](const uint8_t *digest, const uint8_t *votes, size_t n) {
+    for (size_t i = 0; i < n; ++i) {
+      const uint8_t fl = oracle_verify_flags(votes + 96 * i, votes + 96 * i + 32, digest, 32);
+      if ((fl & (HSV_PARSE_OK | HSV_EQ_OK)) != (HSV_PARSE_OK | HSV_EQ_OK)) return false;
+    }
+    return true;
+  };
+  set_infrastructure_fallback(std::move(f));
+}
+
+int main(int argc, char **argv) {
+  const bool fallback = argc > 1 && std::strcmp(argv[1], "--fallback") == 0;
+  if (fallback) install_oracle_fallback();
   import_export_public_key();
   import_export_secret_key();
   verify_valid_signature();
@@ -181,6 +209,7 @@ int main() {
     std::fprintf(stderr, "%d check(s) failed\n", g_failed);
     return 1;
   }
+  if (fallback) std::printf("infrastructure fallbacks: %llu\n", (unsigned long long)infrastructure_fallback_uses());
   std::printf("crypto_tests: all passed\n");
   return 0;
 }
