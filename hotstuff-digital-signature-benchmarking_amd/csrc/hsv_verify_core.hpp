@@ -412,12 +412,18 @@ HSV_INL void vt_build(VT &vt, int t, const fe &x, const fe &y) {
   cached_pack(c1, w);
   vt.put(t, 1, w);
   if (TS >= 2) {
+    // [m]P = [m-1]P + P with P as an affine Niels point (Z = 1: the mixed
+    // addition is one multiply cheaper than the cached one)
+    ge_niels n1;
+    n1.ypx = fe_add(y, x);
+    n1.ymx = fe_sub(y, x);
+    n1.xy2d = fe_mul(p1.T, fe_d2());
     ge_ext p = ge_dbl<true>(p1);
     cached_pack(ge_to_cached(p), w);
     vt.put(t, 2, w);
     HSV_NOUNROLL
     for (int m = 3; m <= TS; ++m) {
-      p = ge_add_cached<true>(p, c1);
+      p = ge_add_niels<true>(p, n1);
       cached_pack(ge_to_cached(p), w);
       vt.put(t, m, w);
     }
