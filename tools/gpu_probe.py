@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
 """Development probe: golden parity + throughput for each kernel variant on one GPU.
+The product library ships variants 19 and 21 only; run with HSV_LIB=libhsv_all.so
+(make ALL_VARIANTS=1) for the others.
 
 python tools/gpu_probe.py [--n 1048576] [--reps 5]
 """
@@ -32,7 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--variants", default="0,1,2,3")
+    ap.add_argument("--variants", default="19,21")
     ap.add_argument("--synth", action="store_true", help="bench workload (synth.independent_triples) instead of tiled golden")
     a = ap.parse_args()
     print("devices", _lib.device_count(), _lib.version(), flush=True)

@@ -3,7 +3,12 @@
 one phase replaced by a stub (tools/build_phase_libs.sh, -DHSV_TIMING_STUB_*).
 Stub builds give WRONG flags; only their launch times are reported.
 
-python tools/phase_probe.py [--variant 15] [--n 1048576]
+Round 2 measured the shares with tools/build_ab_libs.sh (st_sqrt, st_straus,
+st_tables, st_comb, st_lattice, st_sha: -DHSV_TIMING_STUB_<PHASE>) and
+tools/ab_probe.py, which alternates the builds on one box
+(profiles/r02_ab_log.txt).  This script does the same for the default variant.
+
+python tools/phase_probe.py [--variant 21] [--n 1048576]
 """
 import argparse
 import os
@@ -41,10 +46,11 @@ print('%.4f' % (e0.elapsed_time(e1) / {reps}))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variant", type=int, default=15)
+    ap.add_argument("--variant", type=int, default=21)
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--only", default=None, help="time only this build: full, lattice, sqrt or sha")
+    ap.add_argument("--only", default=None,
+                    help="time only this build: full, lattice, sqrt, sha, straus, tables or comb")
     a = ap.parse_args()
     if a.only:
         lib = os.path.join(PKG, "hsverify", "libhsv.so") if a.only == "full" else \
@@ -53,7 +59,7 @@ def main():
         return
     base = child(os.path.join(PKG, "hsverify", "libhsv.so"), a.variant, a.n, a.reps)
     print(f"variant {a.variant}  full kernel {base:.3f} ms", flush=True)
-    for name in ("lattice", "sqrt", "sha"):
+    for name in ("lattice", "sqrt", "sha", "straus", "tables", "comb"):
         t = child(os.path.join(PKG, f"build_stub_{name}", "libhsv.so"), a.variant, a.n, a.reps)
         print(f"  without {name:8s} {t:.3f} ms   share {100 * (base - t) / base:5.1f} %", flush=True)
 
