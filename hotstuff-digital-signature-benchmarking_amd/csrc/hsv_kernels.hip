@@ -457,24 +457,28 @@ __device__ __forceinline__ fe fe_swap_pair(const fe &a) {
   return r;
 }
 
-// Pair-lane point pass of a prepped (non-fallback) item; both lanes of the
-// pair return the item's flag byte.  p = lane parity: 0 owns R, 1 owns A.
-template <int WA, int CB, class VT>
-__device__ __forceinline__ uint32_t verify_pair_prepped(uint32_t p, const uint32_t pk[8], const uint32_t rb[8],
-                                                        const uint32_t *rec, uint64_t stride, uint32_t meta,
-                                                        const uint32_t *tb, VT &vt) {
-  using G = HalfCombWindows<WA>;
+// Pair-lane point pass of a prepped (non-fallback) item, in two phases; both
+// lanes of the pair return the item's flag byte.  p = lane parity: 0 owns R,
+// 1 owns A.  Phase 1 needs only the point: decompression and its table.
+template <int WA, class VT>
+__device__ __forceinline__ void pair_point_phase(uint32_t p, const uint32_t pk[8], const uint32_t rb[8], VT &vt,
+                                                 uint32_t &ok, uint32_t &small) {
   constexpr int TS = 1 << (WA - 1);
   uint32_t pt[8];
   HSV_UNROLL
   for (int i = 0; i < 8; ++i) pt[i] = p ? pk[i] : rb[i];
-  uint32_t ok, small;
-  {
-    fe x, y;
-    ok = ge_decompress(pt, x, y);
-    small = ok & y_is_small_order(y);
-    vt_build<TS>(vt, 0, fe_carry(fe_neg(x)), y);
-  }
+  fe x, y;
+  ok = ge_decompress(pt, x, y);
+  small = ok & y_is_small_order(y);
+  vt_build<TS>(vt, 0, fe_carry(fe_neg(x)), y);
+}
+
+// Phase 2: the scalars from the prepass record (word j of the item at
+// rec[j * stride]), one-scalar Straus, half of the B comb, the lane swap.
+template <int WA, int CB, class VT>
+__device__ __forceinline__ uint32_t pair_scalar_phase(uint32_t p, uint32_t ok, uint32_t small, const uint32_t *rec,
+                                                      uint64_t stride, uint32_t meta, const uint32_t *tb, VT &vt) {
+  using G = HalfCombWindows<WA>;
   uint32_t d[1][5];
   HSV_UNROLL
   for (int i = 0; i < 5; ++i) d[0][i] = rec[(uint64_t)(i + 5 * (int)p) * stride];
@@ -494,6 +498,15 @@ __device__ __forceinline__ uint32_t verify_pair_prepped(uint32_t p, const uint32
   const uint32_t a_ok = p ? ok : ok_o, small_a = p ? small : small_o;
   const uint32_t same = fe_is_zero(q.X) & fe_eq(q.Y, q.Z);
   return flags_byte(meta & kPrepSOk, a_ok, r_ok, small_a, small_r, same);
+}
+
+template <int WA, int CB, class VT>
+__device__ __forceinline__ uint32_t verify_pair_prepped(uint32_t p, const uint32_t pk[8], const uint32_t rb[8],
+                                                        const uint32_t *rec, uint64_t stride, uint32_t meta,
+                                                        const uint32_t *tb, VT &vt) {
+  uint32_t ok, small;
+  pair_point_phase<WA>(p, pk, rb, vt, ok, small);
+  return pair_scalar_phase<WA, CB>(p, ok, small, rec, stride, meta, tb, vt);
 }
 
 // Pass 2 of the latency form: a plain grid of 2n lanes; lane t works on item
@@ -532,6 +545,65 @@ hsv_verify_pair_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const
   if (valid && p == 0u) {
     if (flags_out) flags_out[idx] = (uint8_t)f;
     if (strict_bits && (f & kStrictOk)) atomicOr(&strict_bits[idx >> 5], 1u << (idx & 31u));
+  }
+}
+
+// Latency form in ONE launch (default at <= kPairMax items): a block of three
+// waves takes 64 items.  Waves 0 and 1 run the pair form's point phase (two
+// lanes per item: decompress R or A, build its table) while wave 2 runs the
+// scalar prepass of the same 64 items (SHA-512, k mod l, lattice reduction,
+// recoding) into an LDS record.  The waves run on different SIMDs, so the
+// prepass's latency hides behind the root chains; after the barrier the pair
+// waves read their scalars from LDS.  Fallback items run the full-length path
+// on both lanes of their pair.
+constexpr int kFusedItems = 64;
+template <int WA, int CB>
+__global__ void __launch_bounds__(3 * 64)
+hsv_verify_pair_fused_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const uint8_t *__restrict__ sig,
+                             uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
+                             uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
+                             uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b) {
+  constexpr int kEnt = (1 << (WA - 1)) + 1;
+  __shared__ uint32_t srec[kPrepWords * kFusedItems];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint32_t base = blockIdx.x * kFusedItems;
+  const uint32_t t = threadIdx.x;  // pair lanes: t < 128
+  const uint32_t p = t & 1u, item = base + (t >> 1);
+  GlobalVarTab<kEnt> vt{vt_ws + ((uint64_t)blockIdx.x * 2u * kFusedItems + (t & 127u)) * vt_lane_uint4<WA>()};
+  uint32_t ok = 0, small = 0;
+  if (wave == 2) {
+    const uint32_t li = base + lane < n ? base + lane : n - 1u;
+    uint32_t pkw[8], sigw[16], msgw[8];
+    load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, li, pkw, sigw, msgw);
+    (void)prep_scalars<WA>(pkw, sigw, msgw, srec + lane, kFusedItems);
+  } else {
+    const uint32_t li = item < n ? item : n - 1u;
+    uint32_t pkw[8], rw[8];
+    const uint4 *pp = reinterpret_cast<const uint4 *>(pk + (uint64_t)li * pk_stride);
+    const uint4 *rp = reinterpret_cast<const uint4 *>(sig + (uint64_t)li * sig_stride);
+    const uint4 p0 = pp[0], p1 = pp[1], r0 = rp[0], r1 = rp[1];
+    pkw[0] = p0.x; pkw[1] = p0.y; pkw[2] = p0.z; pkw[3] = p0.w;
+    pkw[4] = p1.x; pkw[5] = p1.y; pkw[6] = p1.z; pkw[7] = p1.w;
+    rw[0] = r0.x; rw[1] = r0.y; rw[2] = r0.z; rw[3] = r0.w;
+    rw[4] = r1.x; rw[5] = r1.y; rw[6] = r1.z; rw[7] = r1.w;
+    pair_point_phase<WA>(p, pkw, rw, vt, ok, small);
+  }
+  __syncthreads();
+  if (wave == 2) return;
+  const uint32_t il = t >> 1;
+  const uint32_t meta = srec[(kPrepWords - 1) * kFusedItems + il];
+  uint32_t f;
+  const uint32_t li = item < n ? item : n - 1u;
+  if (meta & kPrepFallback) {
+    uint32_t pkw[8], sigw[16], msgw[8];
+    load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, li, pkw, sigw, msgw);
+    f = verify_one_full_comb<WA, false, CB>(pkw, sigw, msgw, comb_b, vt);
+  } else {
+    f = pair_scalar_phase<WA, CB>(p, ok, small, srec + il, kFusedItems, meta, comb_b, vt);
+  }
+  if (item < n && p == 0u) {
+    if (flags_out) flags_out[item] = (uint8_t)f;
+    if (strict_bits && (f & kStrictOk)) atomicOr(&strict_bits[item >> 5], 1u << (item & 31u));
   }
 }
 
@@ -822,41 +894,27 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
   return e != hipSuccess ? e : ef;
 }
 
-// Latency form (variant 21 below kPairMax items): prepass, then the pair
-// kernel on a plain grid of 2n lanes.  Workspace: per-lane tables | counters
-// (256 B) | fallback list | prep records.
-// At 2^12 items the pair form is 27 % faster end to end; at 2^15 it is 7 %
-// slower (the grid no longer fits one wave per SIMD), profiles/r01o_qc_latency.json.
+// Latency form (variant 21 below kPairMax items): one launch of the fused
+// kernel (prepass wave + two pair waves per 64 items).  Workspace: the pair
+// lanes' tables.  Round 1 ran the prepass and hsv_verify_pair_kernel as two
+// launches; at 2^12 items the pair form is 27 % faster end to end than the
+// point pass, at 2^15 7 % slower (profiles/r01o_qc_latency.json).
 constexpr uint32_t kPairMax = 1u << 13;
 
 template <int WA, int CB>
 hipError_t launch_pair(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
                        const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
                        uint32_t *strict_bits, const uint32_t *comb_b, hipStream_t stream) {
-  const uint32_t lanes = 2u * n;
-  const uint32_t grid = (lanes + hsv::kBlock - 1) / hsv::kBlock;
-  const uint32_t prep_grid = (n + hsv::kBlock - 1) / hsv::kBlock;
-  const size_t ws_bytes = (size_t)grid * hsv::kBlock * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
-  const size_t fb_bytes = (size_t)n * sizeof(uint32_t);
-  const size_t rec_bytes = (size_t)n * hsv::kPrepWords * sizeof(uint32_t);
+  const uint32_t grid = (n + hsv::kFusedItems - 1) / hsv::kFusedItems;
+  const size_t ws_bytes = (size_t)grid * 2u * hsv::kFusedItems * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
   void *ws = nullptr;
-  hipError_t e = hipMallocAsync(&ws, ws_bytes + 256 + fb_bytes + rec_bytes, stream);
+  hipError_t e = hipMallocAsync(&ws, ws_bytes, stream);
   if (e != hipSuccess) return e;
-  uint8_t *ws8 = static_cast<uint8_t *>(ws);
-  uint4 *vt_ws = reinterpret_cast<uint4 *>(ws);
-  hsv::HcCounters *ctr = reinterpret_cast<hsv::HcCounters *>(ws8 + ws_bytes);
-  uint32_t *fb_list = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256);
-  uint32_t *rec = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256 + fb_bytes);
-  e = hipMemsetAsync(ctr, 0, sizeof(hsv::HcCounters), stream);
-  if (e == hipSuccess && strict_bits) e = hipMemsetAsync(strict_bits, 0, (size_t)((n + 31u) / 32u) * 4u, stream);
+  if (strict_bits) e = hipMemsetAsync(strict_bits, 0, (size_t)((n + 31u) / 32u) * 4u, stream);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL((hsv::hsv_prep_kernel<WA>), dim3(prep_grid), dim3(hsv::kBlock), 0, stream, pk, pk_stride,
-                       sig, sig_stride, msg, msg_stride, n, rec, ctr, fb_list);
-    e = hipGetLastError();
-  }
-  if (e == hipSuccess) {
-    hipLaunchKernelGGL((hsv::hsv_verify_pair_kernel<WA, CB>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
-                       pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, vt_ws, comb_b, rec);
+    hipLaunchKernelGGL((hsv::hsv_verify_pair_fused_kernel<WA, CB>), dim3(grid), dim3(3 * 64), 0, stream, pk,
+                       pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits,
+                       static_cast<uint4 *>(ws), comb_b);
     e = hipGetLastError();
   }
   const hipError_t ef = hipFreeAsync(ws, stream);
