@@ -10,8 +10,9 @@
 //                          64 mixed additions from the key's table and the B
 //                          table, then R decompression and the projective
 //                          comparison.  Same flag byte as hsv_verify_kernel.
-//  hsv_comb_verify_quad_kernel  the same check with four lanes per vote,
-//                          for batches of at most 2^12 votes (QC latency).
+//  hsv_comb_verify_quad_fused_kernel  the same check for batches of at most
+//                          2^12 votes (QC latency): four lanes per vote for
+//                          the additions, R decompressed by a second wave.
 #include <hip/hip_runtime.h>
 
 #include "hsv_comb.hpp"
@@ -75,9 +76,9 @@ hsv_comb_verify_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__re
 // 667 votes): four lanes per vote.  Lane g of a quad adds the comb entries of
 // positions 8g .. 8g+7 for both k (the key's table) and s (the B table): 16
 // mixed additions instead of 64; the quad's partial sums meet through two
-// lane-swap + addition rounds.  Every lane of the quad hashes and decompresses
-// R itself (same instruction stream, no extra latency), so flags come out of
-// lane 0 exactly as verify_one_comb computes them.
+// lane-swap + addition rounds.  Every lane of the quad hashes the vote (same
+// instruction stream, no extra latency); flags come out of lane 0 exactly as
+// verify_one_comb computes them.
 constexpr int kCombQuad = 4;
 constexpr int kCombPosPerLane = kCombPos / kCombQuad;
 
@@ -93,16 +94,48 @@ __device__ __forceinline__ ge_ext ge_swap_xor(const ge_ext &p, int m) {
   return r;
 }
 
-__global__ void __launch_bounds__(256)
-hsv_comb_verify_quad_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__restrict__ sig,
-                            uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride,
-                            uint32_t m, const uint8_t *__restrict__ pks, const uint8_t *__restrict__ key_flags,
-                            uint32_t nkeys, const uint32_t *const *__restrict__ key_tables,
-                            const uint32_t *__restrict__ btable, uint8_t *__restrict__ flags_out) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t i0 = t / kCombQuad, g = t % kCombQuad;
+// The latency form in two specialised waves (at <= kCombQuadMax votes): a
+// block of 128 threads takes 16 votes.  Wave 0 is 16 quads computing the
+// combined sum Q = [s]B - [k]A; wave 1 decompresses the 16 R (one lane each)
+// at the same time on another SIMD and leaves (x, y, flags) in LDS.  Round 1
+// had every quad lane decompress R after its additions.  R's root chain, the
+// longest single piece, no longer follows the hash and the comb additions on
+// the critical lane: the vote costs max(hash + comb, root chain) + the final
+// comparison.
+constexpr int kFusedVotes = 16;
+
+__global__ void __launch_bounds__(128)
+hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__restrict__ sig,
+                                  uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride,
+                                  uint32_t m, const uint8_t *__restrict__ pks, const uint8_t *__restrict__ key_flags,
+                                  uint32_t nkeys, const uint32_t *const *__restrict__ key_tables,
+                                  const uint32_t *__restrict__ btable, uint8_t *__restrict__ flags_out) {
+  __shared__ uint32_t r_x[kFusedVotes][kFeLimbs], r_y[kFusedVotes][kFeLimbs], r_fl[kFusedVotes];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint32_t base = blockIdx.x * kFusedVotes;
+  if (wave == 1) {
+    if (lane < (uint32_t)kFusedVotes) {
+      const uint32_t i = base + lane < m ? base + lane : m - 1u;
+      const uint4 *sp = reinterpret_cast<const uint4 *>(sig + (uint64_t)i * sig_stride);
+      const uint4 s0 = sp[0], s1 = sp[1];
+      const uint32_t rw[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      fe rx, ry;
+      const uint32_t r_ok = ge_decompress(rw, rx, ry);
+      const uint32_t small_r = r_ok & y_is_small_order(ry);
+      HSV_UNROLL
+      for (int l = 0; l < kFeLimbs; ++l) {
+        r_x[lane][l] = rx.v[l];
+        r_y[lane][l] = ry.v[l];
+      }
+      r_fl[lane] = r_ok | (small_r << 1);
+    }
+    __syncthreads();
+    return;
+  }
+  const uint32_t vl = lane / kCombQuad, g = lane % kCombQuad;
+  const uint32_t i0 = base + vl;
   const bool valid = i0 < m;
-  const uint32_t i = valid ? i0 : m - 1u;  // whole quads past the end compute a copy
+  const uint32_t i = valid ? i0 : m - 1u;
   const uint32_t kidx = key_idx[i];
   const bool kvalid = kidx < nkeys;
   const uint32_t kk = kvalid ? kidx : 0u;
@@ -130,7 +163,6 @@ hsv_comb_verify_quad_kernel(const uint32_t *__restrict__ key_idx, const uint8_t 
   uint32_t kr[9], sr[9];
   recode_add<9, 8, kCombPos>(k.v, 8, kr);
   recode_add<9, 8, kCombPos>(sigw + 8, 8, sr);
-  // this lane's 8 digits = bytes 8g .. 8g+7 = words 2g, 2g+1 (selects, no register indexing)
   uint64_t kd = 0, sd = 0;
   HSV_UNROLL
   for (int q4 = 0; q4 < kCombQuad; ++q4) {
@@ -153,10 +185,15 @@ hsv_comb_verify_quad_kernel(const uint32_t *__restrict__ key_idx, const uint8_t 
   }
   q = ge_add_cached_rt(q, ge_to_cached(ge_swap_xor(q, 1)), true);
   q = ge_add_cached_rt(q, ge_to_cached(ge_swap_xor(q, 2)), false);
-
+  __syncthreads();
   fe rx, ry;
-  const uint32_t r_ok = ge_decompress(sigw, rx, ry);
-  const uint32_t small_r = r_ok & y_is_small_order(ry);
+  HSV_UNROLL
+  for (int l = 0; l < kFeLimbs; ++l) {
+    rx.v[l] = r_x[vl][l];
+    ry.v[l] = r_y[vl][l];
+  }
+  const uint32_t rf = r_fl[vl];
+  const uint32_t r_ok = rf & 1u, small_r = (rf >> 1) & 1u;
   const uint32_t same = ge_eq_affine(q, rx, ry);
   const uint32_t kf = key_flags[kk];
   const uint32_t a_ok = (kf & kKeyAOk) ? 1u : 0u;
@@ -217,11 +254,10 @@ extern "C" hipError_t hsv_launch_comb_verify(const uint32_t *key_idx, const uint
                                              const uint32_t *const *key_tables, const uint32_t *btable,
                                              uint8_t *flags_out, hipStream_t stream) {
   if (m == 0) return hipSuccess;
-  if (m <= kCombQuadMax) {  // latency form: four lanes per vote
-    const uint64_t lanes = (uint64_t)m * hsv::kCombQuad;
-    hipLaunchKernelGGL(hsv::hsv_comb_verify_quad_kernel, dim3((uint32_t)((lanes + 255u) / 256u)), dim3(256), 0,
-                       stream, key_idx, sig, sig_stride, msg, msg_stride, m, pks, key_flags, nkeys, key_tables, btable,
-                       flags_out);
+  if (m <= kCombQuadMax) {  // latency form: four lanes per vote, R decompressed by a second wave
+    hipLaunchKernelGGL(hsv::hsv_comb_verify_quad_fused_kernel, dim3((m + hsv::kFusedVotes - 1) / hsv::kFusedVotes),
+                       dim3(128), 0, stream, key_idx, sig, sig_stride, msg, msg_stride, m, pks, key_flags, nkeys,
+                       key_tables, btable, flags_out);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(hsv::hsv_comb_verify_kernel, dim3((m + 255u) / 256u), dim3(256), 0, stream, key_idx, sig,
