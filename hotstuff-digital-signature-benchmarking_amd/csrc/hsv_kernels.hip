@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <unordered_map>
 
@@ -340,6 +341,11 @@ hsv_verify_fb_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
 
 #endif  // HSV_ALL_VARIANTS
 
+#ifdef HSV_PHASE_CLOCKS  // tools/phase_clock_probe.py only: 8 words per 64-item batch of the point pass
+constexpr uint32_t kPhaseCap = 1u << 16;
+__device__ uint64_t g_phase_clk[kPhaseCap * 8];
+#endif
+
 // Two-pass form (hsv_verify_hc.hpp, prep_scalars / verify_one_prepped).
 // Pass 1: one lane per item, scalar work only; records to `rec` (SoA, row
 // stride n), fallback items appended to fb_list.
@@ -347,12 +353,13 @@ template <int WA>
 __global__ void __launch_bounds__(kBlock)
 hsv_prep_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const uint8_t *__restrict__ sig,
                 uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
-                uint32_t *__restrict__ rec, HcCounters *__restrict__ ctr, uint32_t *__restrict__ fb_list) {
+                uint32_t *__restrict__ rec, HcCounters *__restrict__ ctr, uint32_t *__restrict__ fb_list,
+                int lat_bits) {
   const uint32_t idx = blockIdx.x * kBlock + threadIdx.x;
   if (idx >= n) return;
   uint32_t pkw[8], sigw[16], msgw[8];
   load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, idx, pkw, sigw, msgw);
-  if (prep_scalars<WA>(pkw, sigw, msgw, rec + idx, n)) fb_list[atomicAdd(&ctr->fb_count, 1u)] = idx;
+  if (prep_scalars<WA>(pkw, sigw, msgw, rec + idx, n, lat_bits)) fb_list[atomicAdd(&ctr->fb_count, 1u)] = idx;
 }
 
 // Pass 2: persistent grid, 64-item batches from ctr->next over a virtual
@@ -374,6 +381,16 @@ hsv_verify_hp_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const u
   const uint32_t nfb = __builtin_amdgcn_readfirstlane(ctr->fb_count);
   const uint32_t fb_end = (nfb + 63u) & ~63u;
   const uint32_t words = (n + 31u) / 32u;
+#ifdef HSV_STAGGER_US  // timing probe only: wave slot s of a SIMD starts s * HSV_STAGGER_US us late
+  {
+    const uint32_t slot = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 4) % 3u;  // HW_ID.WAVE_ID
+    const uint64_t until = wall_clock64() + (uint64_t)slot * HSV_STAGGER_US * 100u;
+    while (wall_clock64() < until) __builtin_amdgcn_s_sleep(64);
+  }
+#endif
+#ifdef HSV_PHASE_CLOCKS
+  uint32_t nbw = 0;  // batches this wave has taken
+#endif
   for (;;) {
     uint32_t base = 0;
     if (lane == 0) base = atomicAdd(&ctr->next, 64u);
@@ -408,7 +425,24 @@ hsv_verify_hp_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const u
     }
     const uint32_t meta = rec[18ull * n + li];
     const bool own = valid && !(meta & kPrepFallback);
+#ifdef HSV_PHASE_CLOCKS
+    uint64_t clk[5];
+    ++nbw;
+    clk[0] = wall_clock64();
+    const uint32_t f = verify_one_prepped<WA, CB>(pkw, rw, rec + li, n, meta, comb_b, vt, clk);
+    clk[4] = wall_clock64();
+    {  // lanes 0..7 store one word each (one store region keeps the work loop uniform)
+      uint64_t v = 1;
+      HSV_UNROLL
+      for (int j = 0; j < 5; ++j) v = lane == (uint32_t)j ? clk[j] : v;
+      v = lane == 5u ? (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4) : v;  // HW_ID
+      v = lane == 6u ? ((uint64_t)blockIdx.x << 8 | nbw) : v;
+      v = lane == 7u ? (0x100u | (uint64_t)__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20)) : v;  // XCC_ID
+      if (lane < 8u && b0 / 64u < kPhaseCap) g_phase_clk[(uint64_t)(b0 / 64u) * 8u + lane] = v;
+    }
+#else
     const uint32_t f = verify_one_prepped<WA, CB>(pkw, rw, rec + li, n, meta, comb_b, vt);
+#endif
     if (own && flags_out) flags_out[idx] = (uint8_t)f;
     if (strict_bits) {
       const uint64_t mask = __ballot(own && (f & kStrictOk));
@@ -562,7 +596,7 @@ __global__ void __launch_bounds__(3 * 64)
 hsv_verify_pair_fused_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const uint8_t *__restrict__ sig,
                              uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
                              uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
-                             uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b) {
+                             uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b, int lat_bits) {
   constexpr int kEnt = (1 << (WA - 1)) + 1;
   __shared__ uint32_t srec[kPrepWords * kFusedItems];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
@@ -575,7 +609,7 @@ hsv_verify_pair_fused_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
     const uint32_t li = base + lane < n ? base + lane : n - 1u;
     uint32_t pkw[8], sigw[16], msgw[8];
     load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, li, pkw, sigw, msgw);
-    (void)prep_scalars<WA>(pkw, sigw, msgw, srec + lane, kFusedItems);
+    (void)prep_scalars<WA>(pkw, sigw, msgw, srec + lane, kFusedItems, lat_bits);
   } else {
     const uint32_t li = item < n ? item : n - 1u;
     uint32_t pkw[8], rw[8];
@@ -741,6 +775,10 @@ extern "C" int hsv_num_variants(void) { return 23; }
 
 namespace {
 
+// Lattice bound of the comb-path prepass (hsv_set_lattice_bits; tests lower it
+// to 133 so the lattice-fallback fixtures take the full-length path).
+std::atomic<int> g_lat_bits{hsv::kLatCombBits};
+
 #if HSV_ALL_VARIANTS
 // Persistent-grid launch of hsv_verify_mt_kernel with a stream-ordered
 // workspace for the per-lane tables (freed on the same stream).
@@ -869,7 +907,7 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
   if (e == hipSuccess && strict_bits) e = hipMemsetAsync(strict_bits, 0, (size_t)((n + 31u) / 32u) * 4u, stream);
   if (e == hipSuccess) {
     hipLaunchKernelGGL((hsv::hsv_prep_kernel<WA>), dim3(blocks_needed), dim3(hsv::kBlock), 0, stream, pk, pk_stride,
-                       sig, sig_stride, msg, msg_stride, n, rec, ctr, fb_list);
+                       sig, sig_stride, msg, msg_stride, n, rec, ctr, fb_list, g_lat_bits.load());
     e = hipGetLastError();
   }
   if (e == hipSuccess) {
@@ -914,7 +952,7 @@ hipError_t launch_pair(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig
   if (e == hipSuccess) {
     hipLaunchKernelGGL((hsv::hsv_verify_pair_fused_kernel<WA, CB>), dim3(grid), dim3(3 * 64), 0, stream, pk,
                        pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits,
-                       static_cast<uint4 *>(ws), comb_b);
+                       static_cast<uint4 *>(ws), comb_b, g_lat_bits.load());
     e = hipGetLastError();
   }
   const hipError_t ef = hipFreeAsync(ws, stream);
@@ -1028,8 +1066,30 @@ extern "C" double hsv_launch_mad_peak(int device_cus) {
   return ms > 0.f ? macs / (ms * 1e-3) : -1.0;
 }
 
+// Test hook (not in hsv.h): the lattice bound of the comb-path prepass.
+// 0 restores the default (kLatCombBits); otherwise 128..kLatCombBits.
+// Returns the previous bound, or -1 for an out-of-range value.
+extern "C" int hsv_set_lattice_bits(int bits) {
+  if (bits == 0) bits = hsv::kLatCombBits;
+  if (bits < 128 || bits > hsv::kLatCombBits) return -1;
+  return g_lat_bits.exchange(bits);
+}
+
 extern "C" int hsv_variant_needs_comb(int variant) {
   if (variant >= 10 && variant <= 14) return 8;
   if (variant >= 15 && variant <= 22) return 16;
   return 0;
 }
+
+#ifdef HSV_PHASE_CLOCKS
+extern "C" int hsv_phase_clocks_read(uint64_t *dst, size_t words, int clear) {
+  const size_t nw = std::min<size_t>(words, (size_t)hsv::kPhaseCap * 8);
+  if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(hsv::g_phase_clk), nw * sizeof(uint64_t)) != hipSuccess) return -1;
+  if (clear) {
+    void *p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(hsv::g_phase_clk)) != hipSuccess) return -1;
+    if (hipMemset(p, 0, (size_t)hsv::kPhaseCap * 8 * sizeof(uint64_t)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif

@@ -15,8 +15,9 @@
 // estimated, so every step is an exact unimodular update).  It stops at the
 // first remainder below 2^128, where |t| <= N / 2^128 < 2^128.  If that t is
 // even, the odd partner is the previous vector reduced against it (one
-// Gauss step).  Vectors longer than kLatMaxBits are reported as !ok and the
-// caller falls back to the full-length path (probability ~2^-14 per lane).
+// Gauss step).  Vectors longer than max_bits are reported as !ok and the
+// caller falls back to the full-length path (probability ~2^-13.5 per lane at
+// 133 bits, ~2^-22.6 at the comb path's 138).
 #pragma once
 #include <math.h>
 
@@ -25,6 +26,13 @@
 namespace hsv {
 
 constexpr int kLatMaxBits = 133;  // |c0|, |c1| < 2^133 (recoding over 135 bits needs < 2^133.78)
+// Bound of the comb-path kernels (hsv_verify_hc.hpp: 35 windows of 4 bits,
+// c + C < 2^140 for c < 2^138.9).  A pair with max(|c0|, |c1|) >= 2^138 needs
+// a shortest vector below ~2^117 with an even cofactor: about 2^-22.6 of the
+// challenges, against ~2^-13.5 at 133 bits, so a 2^20 batch almost never holds
+// a full-length item (each one costs its SIMD a second batch of work at the
+// end of the persistent grid).
+constexpr int kLatCombBits = 138;
 
 struct LatOut {
   uint32_t c0[5];  // |c0|, little-endian
@@ -355,7 +363,8 @@ HSV_INL bool lat_congruent(const sc &k, const LatOut &o) {
   return nz == 0;
 }
 
-HSV_INL LatOut lattice_reduce(const sc &k) {
+// max_bits: the largest accepted bit length of |c0| and |c1| (<= 159).
+HSV_INL LatOut lattice_reduce(const sc &k, int max_bits = kLatMaxBits) {
 #ifdef HSV_TIMING_STUB_LATTICE  // tools/phase_probe.py only: wrong results, timing share of the reduction
   {
     LatOut o;
@@ -444,9 +453,9 @@ HSV_INL LatOut lattice_reduce(const sc &k) {
   // normalise c1 > 0 (negate the whole vector), then bound-check
   uint32_t n1;
   uint32_t c1mag[5], c0mag[5];
-  const bool f1 = mps_abs_fits<6>(c1, kLatMaxBits, c1mag, n1);
+  const bool f1 = mps_abs_fits<6>(c1, max_bits, c1mag, n1);
   uint32_t n0;
-  const bool f0 = mps_abs_fits<9>(c0, kLatMaxBits, c0mag, n0);
+  const bool f0 = mps_abs_fits<9>(c0, max_bits, c0mag, n0);
   const bool odd = (c1[0] & 1u) != 0;
   bool nz = false;
   HSV_UNROLL

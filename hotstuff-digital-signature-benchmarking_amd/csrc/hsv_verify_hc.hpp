@@ -4,7 +4,7 @@
 //   EQ_OK  <=>  [c1](-R) + [|c0|](-sign(c0) A) + [b]B == O,
 //   (c0, c1) = lattice_reduce(k),  b = (c1 s) mod l,
 // evaluated in two phases so the hot loop stays small:
-//   1. Straus over the two ~133-bit scalars c1, |c0|: NW windows of WA bits,
+//   1. Straus over the two ~128-bit scalars c1, |c0| (< 2^138): NW windows of WA bits,
 //      WA doublings + 2 cached additions per window, entries of the per-lane
 //      tables [0..2^(WA-1)](-R), [0..2^(WA-1)](-sign(c0) A) read from memory
 //      (VT, one 128-byte line per entry) a window ahead of their use;
@@ -12,7 +12,7 @@
 //      once per device, L2-resident): 32 mixed additions, no doublings.
 // Each phase has one copy of its point formula (runtime with_t flag), so the
 // window loop is ~3k instructions instead of ~10k and stays in the shared
-// instruction cache.  A lane whose lattice reduction fails (~2^-14) takes
+// instruction cache.  A lane whose lattice reduction fails (~2^-22.6) takes
 // verify_one_full_comb: the same two phases with the full-length k.
 #pragma once
 #include "hsv_comb.hpp"
@@ -173,14 +173,14 @@ HSV_INL uint32_t verify_one_full_comb(const uint32_t pk[8], const uint32_t sig[1
 
 template <int WA>
 struct HalfCombWindows {
-  static constexpr int NW = (kLatMaxBits + 1 + WA) / WA;  // c + C_WA < 2^(NW*WA) for c < 2^133
+  static constexpr int NW = (kLatCombBits + 1 + WA) / WA;  // c + C_WA < 2^(NW*WA) for c < 2^138
   static constexpr int BITS = NW * WA;
-  static_assert(BITS <= 160 && BITS >= kLatMaxBits + 2, "scalar bound vs loop length");
+  static_assert(BITS <= 160 && BITS >= kLatCombBits + 2, "scalar bound vs loop length");
 };
 
 template <int WA, bool PREFETCH = true, int CB = 8, class VT>
 HSV_INL uint32_t verify_one_half_comb(const uint32_t pk[8], const uint32_t sig[16], const uint32_t msg[8],
-                                      const uint32_t *tb, VT &vt, bool &fallback) {
+                                      const uint32_t *tb, VT &vt, bool &fallback, int lat_bits = kLatCombBits) {
   using G = HalfCombWindows<WA>;
   constexpr int TS = 1 << (WA - 1);
   const uint32_t s_ok = sc_is_canonical(sig + 8);
@@ -203,7 +203,7 @@ HSV_INL uint32_t verify_one_half_comb(const uint32_t pk[8], const uint32_t sig[1
     small_a = a_ok & y_is_small_order(y);
     vt_build<TS>(vt, 1, fe_carry(fe_neg(x)), y);  // -A; the sign of c0 flips the digits
   }
-  const LatOut lat = lattice_reduce(k);
+  const LatOut lat = lattice_reduce(k, lat_bits);
   fallback = !lat.ok;
   uint32_t d[2][5];
   recode_top5<WA, G::NW>(lat.c1, d[0]);
@@ -226,15 +226,17 @@ HSV_INL uint32_t verify_one_half_comb(const uint32_t pk[8], const uint32_t sig[1
 constexpr int kPrepWords = 19;  // d(c1)[5] | d(|c0|)[5] | b[8] | meta
 enum : uint32_t { kPrepSOk = 1u, kPrepC0Neg = 2u, kPrepFallback = 4u };
 
+// lat_bits: the lattice bound (kLatCombBits; lower values only to exercise the
+// full-length path in tests, hsv_set_lattice_bits).
 template <int WA>
 HSV_INL bool prep_scalars(const uint32_t pk[8], const uint32_t sig[16], const uint32_t msg[8], uint32_t *rec,
-                          uint64_t stride) {
+                          uint64_t stride, int lat_bits = kLatCombBits) {
   using G = HalfCombWindows<WA>;
   const uint32_t s_ok = sc_is_canonical(sig + 8);
   uint32_t h[16];
   sha512_96(sig, pk, msg, h);
   const sc k = sc_reduce512(h);
-  const LatOut lat = lattice_reduce(k);
+  const LatOut lat = lattice_reduce(k, lat_bits);
   uint32_t d[5];
   recode_top5<WA, G::NW>(lat.c1, d);
   HSV_UNROLL
@@ -252,9 +254,24 @@ HSV_INL bool prep_scalars(const uint32_t pk[8], const uint32_t sig[16], const ui
 // Point pass of a prepped item: the half-size equation of
 // verify_one_half_comb with the scalars read back from the record.
 // `rb` is R (the first 32 bytes of the signature).
+// HSV_PHASE_CLOCKS (tools/phase_clock_probe.py only): wall-clock stamps at the
+// phase boundaries of the point pass, clk[1..3] after decompression, tables
+// and the window loop.
+#ifdef HSV_PHASE_CLOCKS
+#define HSV_CLK(j)                       \
+  do {                                   \
+    if (clk) clk[j] = wall_clock64();    \
+  } while (0)
+#else
+#define HSV_CLK(j) \
+  do {             \
+  } while (0)
+#endif
+
 template <int WA, int CB, class VT>
 HSV_INL uint32_t verify_one_prepped(const uint32_t pk[8], const uint32_t rb[8], const uint32_t *rec,
-                                    uint64_t stride, const uint32_t meta, const uint32_t *tb, VT &vt) {
+                                    uint64_t stride, const uint32_t meta, const uint32_t *tb, VT &vt,
+                                    uint64_t *clk = nullptr) {
   using G = HalfCombWindows<WA>;
   constexpr int TS = 1 << (WA - 1);
   uint32_t a_ok, small_a, r_ok, small_r;
@@ -263,8 +280,10 @@ HSV_INL uint32_t verify_one_prepped(const uint32_t pk[8], const uint32_t rb[8], 
     ge_decompress2(rb, pk, xr, yr, xa, ya, r_ok, a_ok);  // both root chains at once
     small_r = r_ok & y_is_small_order(yr);
     small_a = a_ok & y_is_small_order(ya);
+    HSV_CLK(1);
     vt_build<TS>(vt, 0, fe_carry(fe_neg(xr)), yr);
     vt_build<TS>(vt, 1, fe_carry(fe_neg(xa)), ya);
+    HSV_CLK(2);
   }
   uint32_t d[2][5];
   HSV_UNROLL
@@ -273,6 +292,7 @@ HSV_INL uint32_t verify_one_prepped(const uint32_t pk[8], const uint32_t rb[8], 
     d[1][i] = rec[(5 + i) * stride];
   }
   ge_ext q = straus_vt<WA, G::NW, 5, 2, false>(d, vt, (meta & kPrepC0Neg) ? 1u : 0u);
+  HSV_CLK(3);
   uint32_t b[8];
   HSV_UNROLL
   for (int i = 0; i < 8; ++i) b[i] = rec[(10 + i) * stride];

@@ -92,10 +92,14 @@ def _declare(lib):
                                                        ctypes.c_void_p]),
         "hsv_set_variant": (ctypes.c_int, [ctypes.c_int]),
         "hsv_get_variant": (ctypes.c_int, []),
+        "hsv_set_lattice_bits": (ctypes.c_int, [ctypes.c_int]),
         "hsv_num_variants": (ctypes.c_int, []),
     }
+    optional = {"hsv_set_lattice_bits"}  # test hooks absent from older A/B builds (tools/ab_probe.py)
     for name, (res, args) in sig.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None) if name in optional else getattr(lib, name)
+        if fn is None:
+            continue
         fn.restype = res
         fn.argtypes = args
 

@@ -94,6 +94,16 @@ def set_variant(v: int) -> None:
     _lib.check(_lib.load().hsv_set_variant(v), "hsv_set_variant")
 
 
+def set_lattice_bits(bits: int) -> int:
+    """Test hook: the lattice bound of the comb-path prepass (0 = default, 138;
+    133 sends the tests/golden/lattice_fallback.bin challenges down the
+    full-length path).  Returns the previous bound."""
+    prev = _lib.load().hsv_set_lattice_bits(bits)
+    if prev < 0:
+        raise ValueError(f"lattice bound out of range: {bits}")
+    return prev
+
+
 def get_variant() -> int:
     return _lib.load().hsv_get_variant()
 

@@ -106,6 +106,10 @@ static void print_fe(const fe &a) {
   for (int i = 7; i >= 0; --i) printf("%08x", w[i]);
 }
 
+// Lattice bound of the comb paths (variants 16-21): HSV_LAT_BITS, default
+// kLatCombBits; the fallback fixtures are built for 133.
+static const int g_lat_bits = getenv("HSV_LAT_BITS") ? atoi(getenv("HSV_LAT_BITS")) : kLatCombBits;
+
 int main(int argc, char **argv) {
   if (argc > 1 && strcmp(argv[1], "--field") == 0) {
     // lines: op a_hex b_hex (big-endian hex of 256-bit values)
@@ -178,7 +182,8 @@ int main(int argc, char **argv) {
     return 0;
   }
   if (argc > 1 && strcmp(argv[1], "--lattice") == 0) {
-    // lines: k (big-endian hex, < l) -> "ok c0_neg c0 c1" (hex, big-endian)
+    // lines: k (big-endian hex, < l) -> "ok c0_neg c0 c1" (hex, big-endian);
+    // optional argv[2]: the bound in bits (default kLatMaxBits)
     std::string ks;
     while (std::cin >> ks) {
       uint8_t kb[32], tmp[32];
@@ -186,7 +191,7 @@ int main(int argc, char **argv) {
       for (int i = 0; i < 32; ++i) kb[i] = tmp[31 - i];
       sc k;
       to_words(kb, k.v, 8);
-      const LatOut o = lattice_reduce(k);
+      const LatOut o = lattice_reduce(k, argc > 2 ? atoi(argv[2]) : kLatMaxBits);
       printf("%u %u ", o.ok, o.c0_neg);
       for (int i = 4; i >= 0; --i) printf("%08x", o.c0[i]);
       printf(" ");
@@ -287,16 +292,16 @@ int main(int argc, char **argv) {
       case 19: {
         bool fb = false;
         HostVarTab vt;
-        f = variant == 16 ? verify_one_half_comb<3>(pw, sw, mw, comb_b(), vt, fb)
-          : variant == 17 ? verify_one_half_comb<4>(pw, sw, mw, comb_b(), vt, fb)
-                          : verify_one_half_comb<5>(pw, sw, mw, comb_b(), vt, fb);
+        f = variant == 16 ? verify_one_half_comb<3>(pw, sw, mw, comb_b(), vt, fb, g_lat_bits)
+          : variant == 17 ? verify_one_half_comb<4>(pw, sw, mw, comb_b(), vt, fb, g_lat_bits)
+                          : verify_one_half_comb<5>(pw, sw, mw, comb_b(), vt, fb, g_lat_bits);
         if (fb) f = verify_one_full_comb<3>(pw, sw, mw, comb_b(), vt) | 0x100u;
         break;
       }
       case 20: {
         bool fb = false;
         HostVarTab vt;
-        f = verify_one_half_comb<4, true, 16>(pw, sw, mw, comb16_b(), vt, fb);
+        f = verify_one_half_comb<4, true, 16>(pw, sw, mw, comb16_b(), vt, fb, g_lat_bits);
         if (fb) f = verify_one_full_comb<4, true, 16>(pw, sw, mw, comb16_b(), vt) | 0x100u;
         break;
       }
@@ -308,7 +313,7 @@ int main(int argc, char **argv) {
       case 21: {  // two-pass form (GPU variants 19/20): scalar prepass record, then the point pass
         HostVarTab vt;
         uint32_t rec[kPrepWords];
-        if (prep_scalars<4>(pw, sw, mw, rec, 1))
+        if (prep_scalars<4>(pw, sw, mw, rec, 1, g_lat_bits))
           f = verify_one_full_comb<4, true, 16>(pw, sw, mw, comb16_b(), vt) | 0x100u;
         else
           f = verify_one_prepped<4, 16>(pw, sw, rec, 1, rec[18], comb16_b(), vt);

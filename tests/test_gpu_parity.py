@@ -37,12 +37,21 @@ def test_golden_every_variant(api, golden):
         verifier.set_variant(default)
 
 
-def test_lattice_fallback_records_every_variant(api, fallback_records):
-    """Challenges the lattice reduction rejects take the full-length path inside
-    the half-size kernels; every variant must still match the oracle's flags."""
+@pytest.mark.parametrize("bits", [133, 0])
+def test_lattice_fallback_records_every_variant(api, fallback_records, bits):
+    """The fixture challenges have no lattice pair below 2^133: with the bound
+    lowered to 133 (hsv_set_lattice_bits) they take the full-length path inside
+    the half-size kernels (tests/test_kernel_host.py shows the same headers do);
+    at the default 138 they stay on the half-size path.  Every variant must
+    match the oracle's flags either way.  The automatic committee cache is off
+    so the generic kernels run."""
     _, verifier, _ = api
+    from hsverify import _lib
+    lib = _lib.load()
     fb = fallback_records
     default = verifier.get_variant()
+    prev = verifier.set_lattice_bits(bits)
+    lib.hsv_set_auto_committee(0)
     try:
         for v in verifier.variants():
             verifier.set_variant(v)
@@ -52,8 +61,14 @@ def test_lattice_fallback_records_every_variant(api, fallback_records):
             idx = np.arange(256) % len(fb["flags"])
             got = verifier.verify_flags(fb["pk"][idx], fb["sig"][idx], fb["msg"][idx])
             assert (got == fb["flags"][idx]).all(), v
+            # past the pair form's cut-over: the point pass deals fallback batches first
+            idx = np.arange((1 << 13) + 64) % len(fb["flags"])
+            got = verifier.verify_flags(fb["pk"][idx], fb["sig"][idx], fb["msg"][idx])
+            assert (got == fb["flags"][idx]).all(), v
     finally:
         verifier.set_variant(default)
+        verifier.set_lattice_bits(prev)
+        lib.hsv_set_auto_committee(1)
 
 
 # ---- the reference's own tests (crypto/src/tests/crypto_tests.rs) ---------

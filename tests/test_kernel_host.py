@@ -129,17 +129,19 @@ def test_committee_comb_path_matches_golden(core_host, golden):
     assert bad.size == 0, [golden["cases"][idx[i]] for i in bad[:10]]
 
 
-def test_lattice_reduction_properties(core_host):
+@pytest.mark.parametrize("bits", [133, 138])
+def test_lattice_reduction_properties(core_host, bits):
     """hsv_lattice.hpp: for challenges k < l the reduced pair satisfies
-    c0 == c1 k (mod 8l), c1 odd and 0 < c1, |c0| < 2^133 (ok == 1), or reports
+    c0 == c1 k (mod 8l), c1 odd and 0 < c1, |c0| < 2^bits (ok == 1), or reports
     ok == 0 (the kernel then takes the full-length path).  Includes k = 0, 1,
-    l - 1, small and structured values."""
+    l - 1, small and structured values.  133 is the register-table variants'
+    bound, 138 the comb path's (kLatCombBits)."""
     rnd = random.Random(11)
     N = 8 * o.L
     ks = [0, 1, 2, 3, 8, o.L - 1, o.L - 2, 2**128, 2**128 - 1, 2**127 + 1, 2**252, (o.L - 1) // 2,
           (o.L + 1) // 2, (o.L - 1) // 3, 2**200 + 12345]
     ks += [rnd.randrange(o.L) for _ in range(3000)]
-    got = _run(core_host, ["--lattice"], [f"{k:064x}" for k in ks])
+    got = _run(core_host, ["--lattice", str(bits)], [f"{k:064x}" for k in ks])
     assert len(got) == 4 * len(ks)
     n_ok = 0
     for i, k in enumerate(ks):
@@ -148,24 +150,47 @@ def test_lattice_reduction_properties(core_host):
             continue
         n_ok += 1
         c0s = -c0 if neg else c0
-        assert c1 % 2 == 1 and 0 < c1 < 2**133 and c0 < 2**133, k
+        assert c1 % 2 == 1 and 0 < c1 < 2**bits and c0 < 2**bits, k
         assert (c0s - c1 * k) % N == 0, k
+    # the structured k (l - 1, 2^252, (l - 1) / 2 ...) have a tiny shortest vector
+    # with an even cofactor: no short odd partner at any bound
     assert n_ok >= len(ks) - 8
+    if bits == 138:
+        assert all(int(got[4 * i]) for i in range(15, len(ks))), "a random challenge fell back at 138 bits"
+
+
+def test_lattice_comb_bound_accepts_fixture_challenges(core_host, fallback_records):
+    """The challenges of tests/golden/lattice_fallback.bin have no pair below
+    2^133 but all have one below the comb path's 2^138 (kLatCombBits): at the
+    default bound none of them takes the full-length path."""
+    fb = fallback_records
+    ks = sorted({o.scalar_from_hash(o.sha512(bytes(s[:32]) + bytes(p) + bytes(m)))
+                 for p, s, m in zip(fb["pk"], fb["sig"], fb["msg"])})
+    got = _run(core_host, ["--lattice", "138"], [f"{k:064x}" for k in ks])
+    oks = [int(got[4 * i]) for i in range(len(ks))]
+    assert sum(oks) == len(ks), "a fixture challenge still falls back at 138 bits"
+    got133 = _run(core_host, ["--lattice", "133"], [f"{k:064x}" for k in ks])
+    assert sum(int(got133[4 * i]) for i in range(len(ks))) <= len(ks) - 24
 
 
 @pytest.mark.parametrize("variant", [16, 17, 20, 21])
-def test_lattice_fallback_records(core_host, fallback_records, variant):
-    """Records built on challenges the lattice reduction rejects: the half-size
-    path hands them to the full-length path (reported on stderr) and the flags
-    equal the oracle's."""
+@pytest.mark.parametrize("bits", [133, 138])
+def test_lattice_fallback_records(core_host, fallback_records, variant, bits):
+    """Records built on challenges the lattice reduction rejects at 133 bits:
+    under that bound the half-size path hands them to the full-length path
+    (reported on stderr); at the comb path's default 138 they stay on the
+    half-size path.  The flags equal the oracle's either way."""
     fb = fallback_records
     lines = [f"{bytes(p).hex()} {bytes(s).hex()} {bytes(m).hex()}" for p, s, m in zip(fb["pk"], fb["sig"], fb["msg"])]
     r = subprocess.run([core_host, "--variant", str(variant)], input="\n".join(lines) + "\n",
-                       capture_output=True, text=True, check=True)
+                       capture_output=True, text=True, check=True, env=dict(os.environ, HSV_LAT_BITS=str(bits)))
     got = np.array([int(x, 16) for x in r.stdout.split()], np.uint8)
     assert (got == fb["flags"]).all()
-    # 24 challenges x (honest, flipped s, s + l) keep k; the mixed-order key changes it
-    assert r.stderr.count("fallback") >= 48
+    if bits == 133:
+        # 24 challenges x (honest, flipped s, s + l) keep k; the mixed-order key changes it
+        assert r.stderr.count("fallback") >= 48
+    else:
+        assert r.stderr.count("fallback") == 0
 
 
 def test_transaction_record_matches_hashlib(core_host):
