@@ -428,6 +428,7 @@ hsv_verify_hp_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const u
 #ifdef HSV_PHASE_CLOCKS
     uint64_t clk[5];
     ++nbw;
+    const uint64_t cyc0 = clock64();
     clk[0] = wall_clock64();
     const uint32_t f = verify_one_prepped<WA, CB>(pkw, rw, rec + li, n, meta, comb_b, vt, clk);
     clk[4] = wall_clock64();
@@ -437,7 +438,9 @@ hsv_verify_hp_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const u
       for (int j = 0; j < 5; ++j) v = lane == (uint32_t)j ? clk[j] : v;
       v = lane == 5u ? (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4) : v;  // HW_ID
       v = lane == 6u ? ((uint64_t)blockIdx.x << 8 | nbw) : v;
-      v = lane == 7u ? (0x100u | (uint64_t)__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20)) : v;  // XCC_ID
+      v = lane == 7u ? (0x100u | (uint64_t)__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) |  // XCC_ID
+                        ((clock64() - cyc0) << 16))  // shader clocks over the batch
+                     : v;
       if (lane < 8u && b0 / 64u < kPhaseCap) g_phase_clk[(uint64_t)(b0 / 64u) * 8u + lane] = v;
     }
 #else

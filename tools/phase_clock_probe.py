@@ -62,7 +62,8 @@ def main():
         assert rd(buf.ctypes.data, buf.size, 0) == 0
         runs.append((e0.elapsed_time(e1), buf.reshape(nb, 8).copy()))
     ms, rec = runs[-1]
-    assert ((rec[:, 7] >> 8) == 1).all(), "batches without a record"
+    assert (((rec[:, 7] >> 8) & 0xff) == 1).all(), "batches without a record"
+    cyc = (rec[:, 7] >> 16).astype(np.int64)
     xcc = (rec[:, 7] & 15).astype(np.int64)
     seq = (rec[:, 6] & 255).astype(np.int64)
     t = rec[:, :5].astype(np.int64)
@@ -97,8 +98,10 @@ def main():
         f1 = d[sx & (seq == 1)].mean(axis=0)
         fl_ = d[sx & (seq > 1)].mean(axis=0)
         out["xcc"].append({"xcc": x, "batches": int(sx.sum()), "span_us": span, "first": f1.tolist(), "later": fl_.tolist()})
+        mhz = float(cyc[sx].sum() / ((t[sx, 4] - t[sx, 0]).sum() * TICK_US))
+        out["xcc"][-1]["shader_mhz"] = mhz
         print(f"{x:3d}  {sx.sum():7d}  {span:7.0f}   " + " ".join(f"{v:7.1f}" for v in f1) + "     " +
-              " ".join(f"{v:7.1f}" for v in fl_))
+              " ".join(f"{v:7.1f}" for v in fl_) + f"   {mhz:6.0f} MHz")
     for k in range(1, int(seq.max()) + 1):
         sk = seq == k
         print(f"wave batch #{k}: {sk.sum()} batches, mean phases " + " ".join(f"{v:7.1f}" for v in d[sk].mean(axis=0)))
