@@ -7,6 +7,17 @@
 extern "C" {
 #endif
 
+// Stream-ordered workspace for a launch on `stream` (current device), freed
+// with hipFreeAsync on the same stream.  It comes from a memory pool the
+// library owns per device, which keeps its freed blocks (release threshold
+// max).  With hipMallocAsync on the default pool (release threshold 0), the
+// QC latency kernel of one thread, run while another thread made the
+// process's first committee-cache allocations, accepted a forged vote in 8 of
+// 16 runs of tests/native/crypto_tests.cpp; with this pool, 0 of 16
+// (tools/forgery_debug.sh).  HSV_WS_POOL=default
+// selects the default pool again (diagnosis only).
+hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream);
+
 // Enqueue one verification launch on `stream` (no synchronisation).
 int hsv_num_variants(void);            // id space
 int hsv_variant_list(int *out, int cap);  // ids built into this library; returns their count

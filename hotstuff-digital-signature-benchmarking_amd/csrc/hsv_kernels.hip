@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <atomic>
 #include <mutex>
 #include <unordered_map>
@@ -533,7 +535,7 @@ __device__ __forceinline__ uint32_t pair_scalar_phase(uint32_t p, uint32_t ok, u
   const uint32_t ok_o = (uint32_t)__shfl_xor((int)ok, 1, 64), small_o = (uint32_t)__shfl_xor((int)small, 1, 64);
   const uint32_t r_ok = p ? ok_o : ok, small_r = p ? small_o : small;
   const uint32_t a_ok = p ? ok : ok_o, small_a = p ? small : small_o;
-  const uint32_t same = fe_is_zero(q.X) & fe_eq(q.Y, q.Z);
+  const uint32_t same = ge_is_neutral(q);
   return flags_byte(meta & kPrepSOk, a_ok, r_ok, small_a, small_r, same);
 }
 
@@ -776,6 +778,39 @@ __global__ void __launch_bounds__(256) hsv_mad_peak_kernel(uint32_t *sink, uint3
 // id space of the variants (hsv_variant_list gives the ids built into this library)
 extern "C" int hsv_num_variants(void) { return 23; }
 
+extern "C" hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream) {
+  static const bool own = [] {
+    const char *v = std::getenv("HSV_WS_POOL");
+    return !(v && std::strcmp(v, "default") == 0);
+  }();
+  if (!own) return hipMallocAsync(p, bytes, stream);
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  static std::mutex mu;
+  static std::unordered_map<int, hipMemPool_t> pools;
+  hipMemPool_t pool = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = pools.find(dev);
+    if (it == pools.end()) {
+      hipMemPoolProps props = {};
+      props.allocType = hipMemAllocationTypePinned;
+      props.handleTypes = hipMemHandleTypeNone;
+      props.location.type = hipMemLocationTypeDevice;
+      props.location.id = dev;
+      e = hipMemPoolCreate(&pool, &props);
+      if (e != hipSuccess) return e;
+      uint64_t keep = UINT64_MAX;
+      e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+      if (e != hipSuccess) return e;
+      it = pools.emplace(dev, pool).first;
+    }
+    pool = it->second;
+  }
+  return hipMallocFromPoolAsync(p, bytes, pool, stream);
+}
+
 namespace {
 
 // Lattice bound of the comb-path prepass (hsv_set_lattice_bits; tests lower it
@@ -807,11 +842,6 @@ hipError_t launch_mt(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
       if (e != hipSuccess) return e;
       e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
       if (e != hipSuccess) return e;
-      hipMemPool_t pool;
-      if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-        uint64_t keep = UINT64_MAX;  // keep freed workspaces cached in the pool
-        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-      }
       it = slots_per_dev.emplace(dev, std::max(1, bpc) * std::max(1, cus)).first;
     }
     resident = it->second;
@@ -822,7 +852,7 @@ hipError_t launch_mt(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
   const size_t ws_bytes = (size_t)grid * hsv::kBlock * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
   const size_t fb_bytes = DEFER ? (size_t)n * sizeof(uint32_t) : 0;
   void *ws = nullptr;
-  e = hipMallocAsync(&ws, ws_bytes + 256 + fb_bytes, stream);
+  e = hsv_ws_malloc(&ws, ws_bytes + 256 + fb_bytes, stream);
   if (e != hipSuccess) return e;
   uint8_t *ws8 = static_cast<uint8_t *>(ws);
   hsv::HcCounters *ctr = reinterpret_cast<hsv::HcCounters *>(ws8 + ws_bytes);
@@ -884,11 +914,6 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
       if (e != hipSuccess) return e;
       e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
       if (e != hipSuccess) return e;
-      hipMemPool_t pool;
-      if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-        uint64_t keep = UINT64_MAX;
-        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-      }
       it = slots_per_dev.emplace(dev, std::max(1, bpc) * std::max(1, cus)).first;
     }
     resident = it->second;
@@ -899,7 +924,7 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
   const size_t fb_bytes = (size_t)n * sizeof(uint32_t);
   const size_t rec_bytes = (size_t)n * hsv::kPrepWords * sizeof(uint32_t);
   void *ws = nullptr;
-  e = hipMallocAsync(&ws, ws_bytes + 256 + fb_bytes + rec_bytes, stream);
+  e = hsv_ws_malloc(&ws, ws_bytes + 256 + fb_bytes + rec_bytes, stream);
   if (e != hipSuccess) return e;
   uint8_t *ws8 = static_cast<uint8_t *>(ws);
   uint4 *vt_ws = reinterpret_cast<uint4 *>(ws);
@@ -949,7 +974,7 @@ hipError_t launch_pair(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig
   const uint32_t grid = (n + hsv::kFusedItems - 1) / hsv::kFusedItems;
   const size_t ws_bytes = (size_t)grid * 2u * hsv::kFusedItems * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
   void *ws = nullptr;
-  hipError_t e = hipMallocAsync(&ws, ws_bytes, stream);
+  hipError_t e = hsv_ws_malloc(&ws, ws_bytes, stream);
   if (e != hipSuccess) return e;
   if (strict_bits) e = hipMemsetAsync(strict_bits, 0, (size_t)((n + 31u) / 32u) * 4u, stream);
   if (e == hipSuccess) {

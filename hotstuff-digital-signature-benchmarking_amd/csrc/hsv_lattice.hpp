@@ -214,6 +214,8 @@ HSV_INL void lat_combine(uint32_t out[N], const uint32_t x[N], const uint32_t y[
 HSV_INL double lat_floor_div(double n, double d) {
 #if defined(__HIP_DEVICE_COMPILE__)
   double q = floor(n * __builtin_amdgcn_rcp(d));
+#elif defined(HSV_LAT_HOST_RCP_ERR)  // host tests only: a reciprocal off by a relative error
+  double q = floor(n * ((1.0 / d) * (1.0 + HSV_LAT_HOST_RCP_ERR)));
 #else
   double q = floor(n / d);
 #endif
@@ -309,6 +311,168 @@ HSV_INL void lat_lehmer_to_128(uint32_t a[8], uint32_t b[8], uint32_t ta[6], uin
   }
 }
 
+// ---- lean Lehmer (default since round 2) -----------------------------------
+// The same Euclid sequence as lat_lehmer_to_128, in a form with a small outer
+// round.  Two facts of the Euclid cofactor sequence make it sign-free:
+//  - remainders are >= 0 and the 2x2 matrix rows have entries of opposite
+//    signs, so  A a + B b = | |A| a - |B| b |  (one product chain each side,
+//    the sign of the difference picks the orientation);
+//  - the cofactors t alternate in sign, so  A ta + B tb  adds two terms of the
+//    same sign:  |ta'| = |A| |ta| + |B| |tb|.
+// The cofactors are kept as magnitudes below 2^128 (|t| <= N / a and a >= 2^128
+// while a lane is active: 4 limbs) with `par` = 1 when tb < 0 (ta has the
+// other sign); the signed form is rebuilt once at the end.  A lane that is not
+// active keeps the identity matrix, so the update needs no selects.
+// The inner loop also takes the step that crosses 2^128 when its quotient is
+// provably exact, and stops after it, so the last division of a lane needs no
+// full-precision step.
+
+// out = | m1 x - m2 y |  (x, y 8 limbs, m1, m2 < 2^31, the result < 2^256)
+HSV_INL void lat_absdiff8(uint32_t out[8], const uint32_t x[8], const uint32_t y[8], uint32_t m1, uint32_t m2) {
+  uint32_t p[9], q[9];
+  uint64_t c = 0, e = 0;
+  HSV_UNROLL
+  for (int i = 0; i < 8; ++i) {
+    c = (uint64_t)x[i] * m1 + (c >> 32);
+    e = (uint64_t)y[i] * m2 + (e >> 32);
+    p[i] = (uint32_t)c;
+    q[i] = (uint32_t)e;
+  }
+  p[8] = (uint32_t)(c >> 32);
+  q[8] = (uint32_t)(e >> 32);
+  uint32_t d[8];
+  uint32_t br = 0;
+  HSV_UNROLL
+  for (int i = 0; i < 9; ++i) {
+    const uint64_t t = (uint64_t)p[i] - q[i] - br;
+    if (i < 8) d[i] = (uint32_t)t;
+    br = (uint32_t)(t >> 63);
+  }
+  const uint32_t m = 0u - br;  // all ones when m1 x < m2 y
+  uint64_t cc = br;
+  HSV_UNROLL
+  for (int i = 0; i < 8; ++i) {
+    cc += (uint64_t)(d[i] ^ m);
+    out[i] = (uint32_t)cc;
+    cc >>= 32;
+  }
+}
+
+// out = m1 x + m2 y  (4 limbs, modulo 2^128; m1, m2 < 2^31)
+HSV_INL void lat_addmul4(uint32_t out[4], const uint32_t x[4], const uint32_t y[4], uint32_t m1, uint32_t m2) {
+  uint64_t c = 0, e = 0;
+  HSV_UNROLL
+  for (int i = 0; i < 4; ++i) {
+    c = (uint64_t)x[i] * m1 + (c >> 32);
+    e = (uint64_t)y[i] * m2 + (uint32_t)c + (e >> 32);
+    out[i] = (uint32_t)e;
+  }
+}
+
+// One exact (possibly partial) division step on lanes with `on`, magnitudes
+// form of lat_exact_step:  q <= floor(a / b),  r = a - q b,  |t| = |ta| + q |tb|;
+// (a, b) <- (b, r) and par flips when r < b, else a <- r.
+HSV_INL void lat_exact_step_mag(uint32_t a[8], uint32_t b[8], uint32_t ua[4], uint32_t ub[4], uint32_t &par,
+                                bool on) {
+  const double qd = mp_to_double<8>(a) / mp_to_double<8>(b);
+  double qf = floor(qd * (1.0 - 0x1p-40));
+  qf = qf < 1.0 ? 1.0 : (qf > 0x1p50 ? 0x1p50 : qf);
+  const uint64_t q = on ? (uint64_t)qf : 0u;
+  uint32_t r[8], t[4];
+  mp_sub_mulq<8>(r, a, b, q);
+  {
+    const uint32_t ql = (uint32_t)q, qh = (uint32_t)(q >> 32);
+    uint64_t c = 0, e = 0;
+    HSV_UNROLL
+    for (int i = 0; i < 4; ++i) {
+      c = (uint64_t)ub[i] * ql + ua[i] + (c >> 32);
+      const uint32_t lo = (uint32_t)c;
+      e = (i >= 1 ? (uint64_t)ub[i - 1] * qh : 0u) + lo + (e >> 32);
+      t[i] = (uint32_t)e;
+    }
+  }
+  const bool swap = on && mp_lt<8>(r, b);
+  HSV_UNROLL
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t nb = swap ? r[i] : b[i];
+    a[i] = swap ? b[i] : (on ? r[i] : a[i]);
+    b[i] = nb;
+  }
+  HSV_UNROLL
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t nub = swap ? t[i] : ub[i];
+    ua[i] = swap ? ub[i] : (on ? t[i] : ua[i]);
+    ub[i] = nub;
+  }
+  par ^= swap ? 1u : 0u;
+}
+
+HSV_INL void lat_lehmer_lean_to_128(uint32_t a[8], uint32_t b[8], uint32_t ta[6], uint32_t tb[6]) {
+  uint32_t ua[4] = {0u, 0u, 0u, 0u}, ub[4] = {1u, 0u, 0u, 0u}, par = 0;
+  HSV_NOUNROLL
+  for (int round = 0; round < 256; ++round) {
+    const bool active = (b[4] | b[5] | b[6] | b[7]) != 0;
+    if (!hsv_any(active)) break;
+    const int h = lat_bitlen8(a);
+    const int s = active ? h - 52 : 0;  // h >= 129 while active
+    double x = lat_digits52(a, s), y = lat_digits52(b, s);
+    const double thr = ldexp(1.0, 128 - s);
+    double A = 1.0, B = 0.0, C = 0.0, D = 1.0;
+    bool go = active;
+    HSV_NOUNROLL
+    for (int j = 0; j < 64; ++j) {
+      if (!hsv_any(go)) break;
+      // true pair: r0 = x + A al + B be, r1 = y + C al + D be, al, be in [0, 1)
+      // (lat_lehmer_to_128); q is exact iff 0 <= r2 < r1 over the box.  The
+      // step is taken when q is exact; the round goes on only while r2 is
+      // provably >= 2^128.
+      bool ok = go && y >= 1.0;
+      const double q = ok ? lat_floor_div(x, y) : 0.0;
+      const double nC = fma(-q, C, A), nD = fma(-q, D, B), ny = fma(-q, y, x);
+      const double lo = ny + fmin(nC, nD);
+      ok = ok && q >= 1.0 && q < 0x1p30 && fabs(nC) < 0x1p31 && fabs(nD) < 0x1p31 && lo >= 0.0 &&
+           (y - ny) + fmin(C - nC, D - nD) >= 1.0;
+      if (ok) {
+        A = C; B = D; C = nC; D = nD;
+        x = y; y = ny;
+      }
+      go = ok && lo >= thr;
+    }
+    {  // identity on lanes that took no step
+      const uint32_t mA = (uint32_t)fabs(A), mB = (uint32_t)fabs(B), mC = (uint32_t)fabs(C), mD = (uint32_t)fabs(D);
+      uint32_t na[8], nb[8], nua[4], nub[4];
+      lat_absdiff8(na, a, b, mA, mB);
+      lat_absdiff8(nb, a, b, mC, mD);
+      lat_addmul4(nua, ua, ub, mA, mB);
+      lat_addmul4(nub, ua, ub, mC, mD);
+      HSV_UNROLL
+      for (int i = 0; i < 8; ++i) {
+        a[i] = na[i];
+        b[i] = nb[i];
+      }
+      HSV_UNROLL
+      for (int i = 0; i < 4; ++i) {
+        ua[i] = nua[i];
+        ub[i] = nub[i];
+      }
+      par ^= D < 0.0 ? 1u : 0u;  // sign(D) = (-1)^(steps taken)
+    }
+    const bool exact = active && B == 0.0;
+    if (hsv_any(exact)) lat_exact_step_mag(a, b, ua, ub, par, exact);
+  }
+  // signed cofactors: tb = (-1)^par |tb|, ta = -(-1)^par |ta|
+  const uint32_t ma = par ? 0u : ~0u, mb = par ? ~0u : 0u;
+  uint64_t ca = ma & 1u, cb = mb & 1u;
+  HSV_UNROLL
+  for (int i = 0; i < 6; ++i) {
+    ca += (uint64_t)((i < 4 ? ua[i] : 0u) ^ ma);
+    cb += (uint64_t)((i < 4 ? ub[i] : 0u) ^ mb);
+    ta[i] = (uint32_t)ca;
+    tb[i] = (uint32_t)cb;
+    ca >>= 32;
+    cb >>= 32;
+  }
+}
 
 // c0s == c1 k (mod 8l), c0s = (c0_neg ? -c0 : c0)?  Checked as
 // F = c1 k - c0s + 8l * 2^140 (>= 0):  F == 0 mod 8  and  F == 0 mod l.
@@ -393,10 +557,12 @@ HSV_INL LatOut lattice_reduce(const sc &k, int max_bits = kLatMaxBits) {
     ta[i] = 0;
     tb[i] = i == 0 ? 1u : 0u;
   }
-#ifdef HSV_LATTICE_EUCLID
+#if defined(HSV_LATTICE_EUCLID)
   lat_euclid_to_128(a, b, ta, tb);
-#else
+#elif defined(HSV_LATTICE_LEHMER1)  // round-1 Lehmer form (A/B and the host cross-check)
   lat_lehmer_to_128(a, b, ta, tb);
+#else
+  lat_lehmer_lean_to_128(a, b, ta, tb);
 #endif
   LatOut o;
   o.ok = 0;

@@ -237,10 +237,20 @@ HSV_INL uint32_t y_is_small_order(const fe &y) {
   return is0 | is1 | pm1 | e8 | ep8;
 }
 
-// Projective point == affine point (x, y): X == x Z and Y == y Z.
+// Projective point == affine point (x, y): X == x Z and Y == y Z, with Z != 0.
+// No point has Z == 0; a (0 : 0 : 0 : 0) accumulator only comes from zeroed
+// table memory and would satisfy both equations, so it fails closed here.
+#ifdef HSV_NEUTRAL_NO_Z_CHECK  // A/B diagnosis builds only: the round-2 checks without Z != 0
+#define HSV_Z_NONZERO(z) 1u
+#else
+#define HSV_Z_NONZERO(z) (fe_is_zero(z) ^ 1u)
+#endif
 HSV_INL uint32_t ge_eq_affine(const ge_ext &p, const fe &x, const fe &y) {
-  return fe_eq(p.X, fe_mul(x, p.Z)) & fe_eq(p.Y, fe_mul(y, p.Z));
+  return fe_eq(p.X, fe_mul(x, p.Z)) & fe_eq(p.Y, fe_mul(y, p.Z)) & HSV_Z_NONZERO(p.Z);
 }
+
+// Q == O: X == 0 and Y == Z != 0 (same fail-closed rule as ge_eq_affine).
+HSV_INL uint32_t ge_is_neutral(const ge_ext &q) { return fe_is_zero(q.X) & fe_eq(q.Y, q.Z) & HSV_Z_NONZERO(q.Z); }
 
 // Compress (x, y) = (X/Z, Y/Z) -> 32 bytes as 8 words (host-side signing).
 HSV_INL void ge_compress(const ge_ext &p, uint32_t out[8]) {

@@ -167,8 +167,8 @@ int hsv_verify_transactions_device(const uint8_t *d_txs, const uint64_t *d_offse
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const size_t per = std::min(n, kChunk);
   void *rec = nullptr;
-  hipError_t e = hipMallocAsync(&rec, per * 128, s);
-  if (e != hipSuccess) return hip_fail("hipMallocAsync (transaction records)", e);
+  hipError_t e = hsv_ws_malloc(reinterpret_cast<void **>(&rec), per * 128, s);
+  if (e != hipSuccess) return hip_fail("workspace allocation (transaction records)", e);
   for (size_t base = 0; base < n && rc == HSV_OK; base += per) {
     const size_t m = std::min(per, n - base);
     rc = tx_enqueue(v, comb_b, d_offsets ? d_txs : d_txs + base * tx_size, d_offsets ? d_offsets + base : nullptr,

@@ -352,7 +352,7 @@ HSV_INL uint32_t verify_one_half(const uint32_t pk[8], const uint32_t sig[16], c
     }
   }
   // Q == O  <=>  X == 0 and Y == Z
-  const uint32_t same = fe_is_zero(q.X) & fe_eq(q.Y, q.Z);
+  const uint32_t same = ge_is_neutral(q);
 
   const uint32_t parse_ok = s_ok & a_ok & r_ok;
   const uint32_t eq_ok = parse_ok & same;
@@ -574,7 +574,7 @@ HSV_INL uint32_t verify_one_half_mt(const uint32_t pk[8], const uint32_t sig[16]
       q = ge_add_cached<false>(q, qa);
     }
   }
-  const uint32_t same = fe_is_zero(q.X) & fe_eq(q.Y, q.Z);  // Q == O
+  const uint32_t same = ge_is_neutral(q);  // Q == O
 
   const uint32_t parse_ok = s_ok & a_ok & r_ok;
   const uint32_t eq_ok = parse_ok & same;

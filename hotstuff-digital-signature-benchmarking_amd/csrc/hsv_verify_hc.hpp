@@ -211,7 +211,7 @@ HSV_INL uint32_t verify_one_half_comb(const uint32_t pk[8], const uint32_t sig[1
   ge_ext q = straus_vt<WA, G::NW, 5, 2, PREFETCH>(d, vt, lat.c0_neg);
   const sc b = sc_mul_small(lat.c1, sig + 8);
   q = comb_add_b<CB>(q, b.v, tb);
-  const uint32_t same = fe_is_zero(q.X) & fe_eq(q.Y, q.Z);  // Q == O
+  const uint32_t same = ge_is_neutral(q);  // Q == O
   return flags_byte(s_ok, a_ok, r_ok, small_a, small_r, same);
 }
 
@@ -297,7 +297,7 @@ HSV_INL uint32_t verify_one_prepped(const uint32_t pk[8], const uint32_t rb[8], 
   HSV_UNROLL
   for (int i = 0; i < 8; ++i) b[i] = rec[(10 + i) * stride];
   q = comb_add_b<CB>(q, b, tb);
-  const uint32_t same = fe_is_zero(q.X) & fe_eq(q.Y, q.Z);
+  const uint32_t same = ge_is_neutral(q);
   return flags_byte(meta & kPrepSOk, a_ok, r_ok, small_a, small_r, same);
 }
 

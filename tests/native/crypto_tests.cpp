@@ -171,10 +171,16 @@ static void verify_valid_qc() {
     ks.pop_back();
     votes.emplace_back(pk, Signature::sign(qc_digest, sk));
   }
+  const size_t cached0 = hsv_auto_committee_size();
   CHECK(Signature::verify_batch(qc_digest, votes).is_ok());
   // QC::verify with one forged vote -> Err (InvalidSignature)
   votes[1].second.part2[5] ^= 0x10;
-  CHECK(Signature::verify_batch(qc_digest, votes).is_err());
+  const size_t cached1 = hsv_auto_committee_size();
+  const bool forged_rejected = Signature::verify_batch(qc_digest, votes).is_err();
+  if (!forged_rejected)
+    std::fprintf(stderr, "forged QC accepted; automatic committee cache held %zu / %zu keys before the two QCs\n",
+                 cached0, cached1);
+  CHECK(forged_rejected);
   // empty vote list: dalek verify_batch over zero items is Ok
   CHECK(Signature::verify_batch(qc_digest, {}).is_ok());
 }

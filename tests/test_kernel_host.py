@@ -159,6 +159,28 @@ def test_lattice_reduction_properties(core_host, bits):
         assert all(int(got[4 * i]) for i in range(15, len(ks))), "a random challenge fell back at 138 bits"
 
 
+@pytest.mark.parametrize("rcp_err", [None, "3e-6", "-3e-6"])
+def test_lean_lehmer_equals_round1_lehmer(core_host, rcp_err):
+    """The default reduction (lat_lehmer_lean_to_128: magnitude cofactors, the
+    crossing step taken inside a round) stops at the same Euclid state as the
+    round-1 form (-DHSV_LATTICE_LEHMER1), so every output is identical.  The
+    rcp_err builds give the quotient estimate a relative error, as the device's
+    hardware reciprocal does: the exactness checks must absorb it."""
+    defs = [f"-DHSV_LAT_HOST_RCP_ERR=({rcp_err})"] if rcp_err else []
+    tag = "" if rcp_err is None else ("_p" if rcp_err[0] != "-" else "_m")
+    lean = _build(BIN + "_lean" + tag, *defs) if defs else core_host
+    old = _build(BIN + "_lehmer1", "-DHSV_LATTICE_LEHMER1")
+    rnd = random.Random(21)
+    N = 8 * o.L
+    ks = [0, 1, 2, 7, 8, o.L - 1, 2**128 - 1, 2**128, 2**128 + 1, 2**129, 2**252, 2**31 + 5]
+    ks += [(N // d) % o.L for d in range(1, 120)] + [(N // d + 1) % o.L for d in range(1, 120)]
+    ks += [(N >> e) for e in (30, 31, 40, 50, 60, 100)] + [2**e % o.L for e in range(0, 253, 3)]
+    ks += [rnd.randrange(o.L) for _ in range(20000)]
+    lines = [f"{k:064x}" for k in ks]
+    for bits in ("138", "133"):
+        assert _run(lean, ["--lattice", bits], lines) == _run(old, ["--lattice", bits], lines)
+
+
 def test_lattice_comb_bound_accepts_fixture_challenges(core_host, fallback_records):
     """The challenges of tests/golden/lattice_fallback.bin have no pair below
     2^133 but all have one below the comb path's 2^138 (kLatCombBits): at the
