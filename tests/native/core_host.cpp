@@ -181,6 +181,19 @@ int main(int argc, char **argv) {
     }
     return 0;
   }
+  if (argc > 1 && strcmp(argv[1], "--degenerate") == 0) {
+    // the (0 : 0 : 0 : 0) accumulator (zeroed table memory) against the final
+    // checks: "neutral eq_affine" must print "0 0"; the neutral point "1 ..."
+    ge_ext z;
+    z.X = fe_small(0);
+    z.Y = fe_small(0);
+    z.Z = fe_small(0);
+    z.T = fe_small(0);
+    const ge_ext o = ge_identity();
+    const fe x = fe_small(0), y = fe_small(1);
+    printf("%u %u %u %u\n", ge_is_neutral(z), ge_eq_affine(z, x, y), ge_is_neutral(o), ge_eq_affine(o, x, y));
+    return 0;
+  }
   if (argc > 1 && strcmp(argv[1], "--lattice") == 0) {
     // lines: k (big-endian hex, < l) -> "ok c0_neg c0 c1" (hex, big-endian);
     // optional argv[2]: the bound in bits (default kLatMaxBits)

@@ -64,3 +64,15 @@ def test_cpp_port_of_reference_crypto_tests(crypto_tests_bin, hsv):
     r = subprocess.run([crypto_tests_bin], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert "all passed" in r.stdout
+
+
+@pytest.mark.gpu
+def test_cpp_mirror_repeated_with_concurrent_cache_build(crypto_tests_bin, hsv):
+    """Regression: the reference's QC test (forged vote -> Err) while the
+    automatic committee cache makes its first allocations on its build thread.
+    Before launch workspaces came from the library's own memory pool, 8 of 16
+    fresh processes accepted the forged vote (profiles/r02t_forgery/summary.txt);
+    each run is a fresh process, so each gets that race."""
+    for i in range(8):
+        r = subprocess.run([crypto_tests_bin], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, f"run {i}: {r.stderr}"

@@ -234,3 +234,11 @@ def test_transaction_record_matches_hashlib(core_host):
     got = _run(core_host, ["--txrec"], lines)
     bad = [(lines[i][:12], len(lines[i])) for i in range(len(exp)) if got[i] != exp[i]]
     assert not bad, bad[:5]
+
+
+def test_degenerate_accumulator_fails_closed(core_host):
+    """(0 : 0 : 0 : 0) -- what an accumulator becomes when its table entries
+    read back as zeros -- satisfies X == 0, Y == Z and X == xZ, Y == yZ; the
+    final checks (ge_is_neutral, ge_eq_affine) also require Z != 0, so it is
+    rejected, while the neutral point itself still compares equal."""
+    assert _run(core_host, ["--degenerate"], []) == ["0", "0", "1", "1"]
