@@ -12,7 +12,9 @@ touches a GPU) and exits with its status; WORLD_SIZE != N is an error.
 Workload (config C4 / C5 shards): each rank holds n = 2^20 independent
 (public key, 32-byte digest, signature) triples in HBM, 5 % corrupted across
 the SURVEY 8(d) corruption kinds.  A step is one verification launch over the
-rank's whole batch (per-item flag bytes + packed STRICT_OK bits).  Shards are
+rank's whole batch (per-item flag bytes + packed STRICT_OK bits); consecutive
+steps alternate over --streams (default 2) HIP streams with their own outputs,
+so one batch's launch starts in the previous one's grid end.  Shards are
 contiguous and independent: no collective touches the data path; the gloo
 group only carries the timing barrier, the max-over-ranks reduction and the
 final bitmask gather.  --global-n 16777216 runs C5 (2^24 split over the ranks,
@@ -21,8 +23,10 @@ gather on CPU (gloo, no GPU, no verification) for tests/test_bench_launcher.py.
 
 Reported beside it:
   roofline         int32-VALU bound; achieved = 192,000 u32 MACs per verification
-                   (SURVEY 8(d) convention) x items per launch / mean launch time
-                   from HIP events on the launch stream; per rank with --global-n.
+                   (SURVEY 8(d) convention) x items per launch / GPU time per step
+                   from HIP events around the timed steps; isolated_launch_ms is
+                   one launch alone on one stream (what rocprofv3 reports per
+                   kernel pair); per rank with --global-n.
   cpu_baseline     rank 0, N = 1 only: the C restatement of ed25519-dalek's
                    verify_strict (oracle/ed25519_oracle.c, "port") on every host
                    core this job may use, over the full C4 batch, flag-for-flag
@@ -421,6 +425,9 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", "--per-gpu", dest="n", type=int, default=1 << 20, help="triples per GPU")
     ap.add_argument("--variant", type=int, default=None)
+    ap.add_argument("--streams", type=int, default=2,
+                    help="consecutive batches alternate over this many HIP streams, so a batch's launch can "
+                         "start in the previous one's grid end (1: every batch on one stream)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20,
                     help="triples the CPU port verifies (default: the whole C4 batch)")
     ap.add_argument("--qc-reps", type=int, default=200)
@@ -529,12 +536,23 @@ def main():
     w = synth.independent_triples(a.n, seed=0xC4 * 1000 + rank, corrupt_frac=0.05, nthreads=host_threads)
     log(f"[rank {rank}] synthesized {a.n} triples in {time.perf_counter() - t0:.1f}s")
     pk, sig, msg = (torch.from_numpy(x).to(dev) for x in (w.pk, w.sig, w.msg))
-    flags = torch.zeros(a.n, dtype=torch.uint8, device=dev)
-    bits = torch.zeros((a.n + 31) // 32, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
+    # Consecutive batches alternate over a.streams streams, each with its own
+    # outputs: independent batches, as a verification pipeline would issue
+    # them.  The next batch's prepass and point pass then fill the SIMDs the
+    # previous point pass leaves idle at its grid end.
+    nst = max(1, a.streams)
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(nst - 1)]
+    outs = [(torch.zeros(a.n, dtype=torch.uint8, device=dev),
+             torch.zeros((a.n + 31) // 32, dtype=torch.int32, device=dev)) for _ in range(nst)]
+    flags, bits = outs[0]
 
-    for _ in range(a.warmup):
-        verifier.verify_device(pk, sig, msg, flags, bits, stream=stream.cuda_stream)
+    def step(i):
+        o = outs[i % nst]
+        verifier.verify_device(pk, sig, msg, o[0], o[1], stream=streams[i % nst].cuda_stream)
+
+    for i in range(max(a.warmup, nst)):
+        step(i)
     torch.cuda.synchronize(dev)
 
     e0 = torch.cuda.Event(enable_timing=True)
@@ -544,13 +562,29 @@ def main():
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
     e0.record(stream)
-    for _ in range(a.steps):
-        verifier.verify_device(pk, sig, msg, flags, bits, stream=stream.cuda_stream)
+    for s in streams[1:]:
+        s.wait_event(e0)
+    for i in range(a.steps):
+        step(i)
+    for s in streams[1:]:
+        ev = torch.cuda.Event()
+        ev.record(s)
+        stream.wait_event(ev)
     e1.record(stream)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t_start
     kernel_ms = e0.elapsed_time(e1) / a.steps
-    mine = {"rank": rank, "kernel_ms": kernel_ms, "elapsed_s": elapsed}
+    # one launch alone on one stream (outside the timed region): the per-launch
+    # duration rocprofv3 reports for the two kernels
+    i0, i1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    i0.record(stream)
+    for _ in range(3):
+        verifier.verify_device(pk, sig, msg, flags, bits, stream=stream.cuda_stream)
+    i1.record(stream)
+    torch.cuda.synchronize(dev)
+    isolated_ms = i0.elapsed_time(i1) / 3
+    same_out = all(torch.equal(outs[0][0], o[0]) and torch.equal(outs[0][1], o[1]) for o in outs[1:])
+    mine = {"rank": rank, "kernel_ms": kernel_ms, "isolated_launch_ms": isolated_ms, "elapsed_s": elapsed}
     per_rank = [mine]
     if world > 1:
         dist.barrier()
@@ -607,6 +641,7 @@ def main():
             "global_batch": a.n * world,
             "parallelism": f"dp{world} (contiguous shards, no collective on the data path)",
             "kernel_variant": verifier.get_variant(),
+            "streams": nst,
         },
         "roofline": {
             "bound": "valu",
@@ -621,11 +656,15 @@ def main():
             "peak_probe": probe / 1e12,
             "work_per_verify": f"{WORK_MACS} u32 MACs (SURVEY 8(d)); {IO_BYTES} HBM bytes algorithmic",
             "kernel_ms": kernel_ms,
+            "kernel_ms_is": (f"GPU time per step, HIP events around the {a.steps} steps "
+                             f"(consecutive launches on {nst} alternating streams)"),
+            "isolated_launch_ms": isolated_ms,
+            "frac_isolated_launch": a.n * WORK_MACS / (isolated_ms * 1e-3) / PEAK_MACS,
             "kernels": "hsv_prep_kernel + hsv_verify_hp_kernel (one verify launch: scalar prepass, point pass)",
             "per_rank": per_rank,
         },
         "checks": {"honest_all_accepted": honest_ok, "corrupted_all_rejected": corrupt_rejected,
-                   "strict_accepted_global": global_accepted},
+                   "strict_accepted_global": global_accepted, "outputs_identical_across_streams": same_out},
     }
     if world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(w, f, a.cpu_sample)
