@@ -556,15 +556,40 @@ int hsv_verify_device_bits(const uint8_t *d_pk, size_t pk_stride, const uint8_t 
   rc = comb_table_for(ctx(dev), v, &comb_b);
   if (rc != HSV_OK) return rc;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  for (size_t base = 0; base < n; base += kChunk) {
-    const size_t m = std::min(kChunk, n - base);
-    hipError_t e = hsv_launch_verify(v, d_pk + base * pk_stride, pk_stride, d_sig + base * sig_stride, sig_stride,
-                                     d_msg + base * msg_stride, msg_stride, (uint32_t)m,
-                                     d_flags ? d_flags + base : nullptr,
-                                     d_strict_bits ? d_strict_bits + base / 32 : nullptr, comb_b, s);
-    if (e != hipSuccess) return hip_fail("verify kernel launch", e);
+  // Batches of several kChunk launches alternate them over the caller's stream
+  // and a second library stream (fork/join through events on the caller's
+  // stream): a chunk's launch starts on the SIMDs the previous chunk's point
+  // pass leaves idle at its grid end.  Chunks write disjoint outputs (kChunk
+  // is a multiple of 32, so no strict-bits word is shared).
+  hipStream_t s2 = s;
+  hipEvent_t fork = nullptr, join = nullptr;
+  if (n > kChunk) {
+    DevCtx &c = ctx(dev);
+    {
+      std::lock_guard<std::mutex> lk(c.side_mu);
+      if (!c.side && hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking) != hipSuccess) c.side = nullptr;
+    }
+    if (c.side && hipEventCreateWithFlags(&fork, hipEventDisableTiming) == hipSuccess &&
+        hipEventCreateWithFlags(&join, hipEventDisableTiming) == hipSuccess &&
+        hipEventRecord(fork, s) == hipSuccess && hipStreamWaitEvent(c.side, fork, 0) == hipSuccess)
+      s2 = c.side;
   }
-  return HSV_OK;
+  hipError_t e = hipSuccess;
+  size_t k = 0;
+  for (size_t base = 0; base < n && e == hipSuccess; base += kChunk, ++k) {
+    const size_t m = std::min(kChunk, n - base);
+    e = hsv_launch_verify(v, d_pk + base * pk_stride, pk_stride, d_sig + base * sig_stride, sig_stride,
+                          d_msg + base * msg_stride, msg_stride, (uint32_t)m, d_flags ? d_flags + base : nullptr,
+                          d_strict_bits ? d_strict_bits + base / 32 : nullptr, comb_b, (k & 1) ? s2 : s);
+  }
+  if (s2 != s) {  // join: the caller's stream waits for the side stream's chunks
+    hipError_t ej = hipEventRecord(join, s2);
+    if (ej == hipSuccess) ej = hipStreamWaitEvent(s, join, 0);
+    if (e == hipSuccess) e = ej;
+  }
+  if (fork) (void)hipEventDestroy(fork);
+  if (join) (void)hipEventDestroy(join);
+  return e == hipSuccess ? HSV_OK : hip_fail("verify kernel launch", e);
 }
 
 int hsv_verify_device(const uint8_t *d_pk, size_t pk_stride, const uint8_t *d_sig, size_t sig_stride,

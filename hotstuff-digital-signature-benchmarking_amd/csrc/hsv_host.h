@@ -56,6 +56,8 @@ struct DevCtx {
   uint32_t *d_btable16 = nullptr;  // wide comb of B (generic kernels)
   std::vector<std::unique_ptr<Slot>> slots;
   std::atomic<unsigned> rr{0};
+  std::mutex side_mu;               // guards `side`
+  hipStream_t side = nullptr;       // second stream of multi-chunk device-API batches
 };
 
 // Makes `device` current for the calling thread and restores the previous
