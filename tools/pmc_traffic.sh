@@ -8,7 +8,7 @@ R=$(pwd); OUT=$R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $OUT/pmc_traffic_$c -o p -- \
-    python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-qc > $OUT/pmc_traffic_$c.json 2> $OUT/pmc_traffic_$c.err || exit 1
+    python3 $R/bench.py --steps 3 --warmup 1 --streams 1 --no-cpu-baseline --no-qc > $OUT/pmc_traffic_$c.json 2> $OUT/pmc_traffic_$c.err || exit 1
 done
 cd $R && python3 - <<'PY'
 import csv, glob, json, collections
