@@ -130,7 +130,9 @@ int hsv_auto_committee_wait(int timeout_ms);
  * pk + i*pk_stride (32 B), sig + i*sig_stride (64 B), msg + i*msg_stride
  * (32 B; msg_stride may be 0).  Pointers and strides must be multiples of 16.
  * Writes n flag bytes to d_flags.  stream: a hipStream_t (NULL = default).
- * Does not synchronise. */
+ * Does not synchronise.  Batches above 2^22 items run as 2^22-item launches
+ * alternating over `stream` and a library stream forked from and joined back
+ * into `stream` by events: the call stays ordered on `stream` as one unit. */
 int hsv_verify_device(const uint8_t *d_pk, size_t pk_stride, const uint8_t *d_sig,
                       size_t sig_stride, const uint8_t *d_msg, size_t msg_stride, size_t n,
                       uint8_t *d_flags, void *stream);
