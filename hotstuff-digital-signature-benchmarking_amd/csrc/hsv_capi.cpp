@@ -480,7 +480,16 @@ void hsv_shutdown(void) {
       s.d_buf = s.h_buf = nullptr;
       s.d_cap = s.h_cap = 0;
     }
+    {
+      std::lock_guard<std::mutex> ls(c->side_mu);
+      if (c->side) {
+        (void)hipStreamSynchronize(c->side);
+        (void)hipStreamDestroy(c->side);
+        c->side = nullptr;
+      }
+    }
   }
+  hsv_ws_trim();
 }
 
 int hsv_device_count(void) {

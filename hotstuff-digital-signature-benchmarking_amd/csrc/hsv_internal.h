@@ -17,6 +17,7 @@ extern "C" {
 // (tools/forgery_debug.sh).  HSV_WS_POOL=default
 // selects the default pool again (diagnosis only).
 hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream);
+void hsv_ws_trim(void);  // hsv_shutdown: release the pools' free blocks
 
 // Enqueue one verification launch on `stream` (no synchronisation).
 int hsv_num_variants(void);            // id space

@@ -778,6 +778,25 @@ __global__ void __launch_bounds__(256) hsv_mad_peak_kernel(uint32_t *sink, uint3
 // id space of the variants (hsv_variant_list gives the ids built into this library)
 extern "C" int hsv_num_variants(void) { return 23; }
 
+namespace {
+struct WsPools {
+  std::mutex mu;
+  std::unordered_map<int, hipMemPool_t> pools;  // device -> the library's workspace pool
+};
+WsPools &ws_pools() {
+  static WsPools p;
+  return p;
+}
+}  // namespace
+
+// hsv_shutdown: return the pools' free blocks to the driver (blocks still in
+// use by enqueued work stay)
+extern "C" void hsv_ws_trim(void) {
+  WsPools &wp = ws_pools();
+  std::lock_guard<std::mutex> lk(wp.mu);
+  for (auto &kv : wp.pools) (void)hipMemPoolTrimTo(kv.second, 0);
+}
+
 extern "C" hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream) {
   static const bool own = [] {
     const char *v = std::getenv("HSV_WS_POOL");
@@ -787,11 +806,11 @@ extern "C" hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream) 
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
-  static std::mutex mu;
-  static std::unordered_map<int, hipMemPool_t> pools;
+  WsPools &wp = ws_pools();
   hipMemPool_t pool = nullptr;
   {
-    std::lock_guard<std::mutex> lk(mu);
+    std::lock_guard<std::mutex> lk(wp.mu);
+    auto &pools = wp.pools;
     auto it = pools.find(dev);
     if (it == pools.end()) {
       hipMemPoolProps props = {};
