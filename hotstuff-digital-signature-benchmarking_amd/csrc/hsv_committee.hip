@@ -73,14 +73,22 @@ hsv_comb_verify_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__re
 }
 
 // Latency form of hsv_comb_verify_kernel for small batches (a QC is 67 or
-// 667 votes): four lanes per vote.  Lane g of a quad adds the comb entries of
-// positions 8g .. 8g+7 for both k (the key's table) and s (the B table): 16
-// mixed additions instead of 64; the quad's partial sums meet through two
-// lane-swap + addition rounds.  Every lane of the quad hashes the vote (same
-// instruction stream, no extra latency); flags come out of lane 0 exactly as
-// verify_one_comb computes them.
-constexpr int kCombQuad = 4;
-constexpr int kCombPosPerLane = kCombPos / kCombQuad;
+// 667 votes): L lanes per vote (HSV_COMB_LANES, default 4).  Lane g of a
+// vote's group adds the comb entries of positions [g P, (g+1) P), P = 32 / L,
+// for both k (the key's table) and s (the B table): 2P mixed additions on the
+// critical lane instead of 64; the group's partial sums meet through log2(L)
+// lane-swap + addition rounds (16 lanes: 4 + 4 additions in sequence, 4 lanes:
+// 16 + 2).  Every lane of the group hashes the vote (same instruction stream,
+// no extra latency); flags come out of lane 0 exactly as verify_one_comb
+// computes them.  The vote's critical path is R's root chain on wave 1 (below),
+// not the additions: 16 lanes per vote measured 4-7 % slower than 4 (more
+// waves, same chain; profiles/r02w_qc_ab.txt).
+#ifndef HSV_COMB_LANES
+#define HSV_COMB_LANES 4
+#endif
+constexpr int kCombLanes = HSV_COMB_LANES;
+static_assert(kCombLanes == 4 || kCombLanes == 8 || kCombLanes == 16, "lanes per vote");
+constexpr int kCombPosPerLane = kCombPos / kCombLanes;
 
 __device__ __forceinline__ ge_ext ge_swap_xor(const ge_ext &p, int m) {
   ge_ext r;
@@ -95,14 +103,13 @@ __device__ __forceinline__ ge_ext ge_swap_xor(const ge_ext &p, int m) {
 }
 
 // The latency form in two specialised waves (at <= kCombQuadMax votes): a
-// block of 128 threads takes 16 votes.  Wave 0 is 16 quads computing the
-// combined sum Q = [s]B - [k]A; wave 1 decompresses the 16 R (one lane each)
-// at the same time on another SIMD and leaves (x, y, flags) in LDS.  Round 1
-// had every quad lane decompress R after its additions.  R's root chain, the
-// longest single piece, no longer follows the hash and the comb additions on
-// the critical lane: the vote costs max(hash + comb, root chain) + the final
+// block of 128 threads takes 64 / L votes.  Wave 0 computes each vote's
+// combined sum Q = [s]B - [k]A over L lanes; wave 1 decompresses the votes' R
+// (one lane each) at the same time on another SIMD and leaves (x, y, flags)
+// in LDS.  R's root chain, the longest single piece, runs beside the hash and
+// the comb additions: the vote costs max(hash + comb, root chain) + the final
 // comparison.
-constexpr int kFusedVotes = 16;
+constexpr int kFusedVotes = 64 / kCombLanes;
 
 __global__ void __launch_bounds__(128)
 hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__restrict__ sig,
@@ -132,7 +139,7 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
     __syncthreads();
     return;
   }
-  const uint32_t vl = lane / kCombQuad, g = lane % kCombQuad;
+  const uint32_t vl = lane / kCombLanes, g = lane % kCombLanes;
   const uint32_t i0 = base + vl;
   const bool valid = i0 < m;
   const uint32_t i = valid ? i0 : m - 1u;
@@ -163,12 +170,17 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
   uint32_t kr[9], sr[9];
   recode_add<9, 8, kCombPos>(k.v, 8, kr);
   recode_add<9, 8, kCombPos>(sigw + 8, 8, sr);
+  // this lane's 8P digit bits, starting at bit 8 g P
   uint64_t kd = 0, sd = 0;
   HSV_UNROLL
-  for (int q4 = 0; q4 < kCombQuad; ++q4) {
-    const bool me = g == (uint32_t)q4;
-    kd = me ? ((uint64_t)kr[2 * q4 + 1] << 32) | kr[2 * q4] : kd;
-    sd = me ? ((uint64_t)sr[2 * q4 + 1] << 32) | sr[2 * q4] : sd;
+  for (int q = 0; q < kCombLanes; ++q) {
+    constexpr int kBits = 8 * kCombPosPerLane;
+    const int w = (q * kBits) / 32, sh = (q * kBits) % 32;
+    const uint64_t kq = ((((uint64_t)kr[w + 1] << 32) | kr[w]) >> sh) & (kBits == 64 ? ~0ull : ((1ull << kBits) - 1));
+    const uint64_t sq = ((((uint64_t)sr[w + 1] << 32) | sr[w]) >> sh) & (kBits == 64 ? ~0ull : ((1ull << kBits) - 1));
+    const bool me = g == (uint32_t)q;
+    kd = me ? kq : kd;
+    sd = me ? sq : sd;
   }
   const uint32_t *ta = key_tables[kk];
   ge_ext q = ge_identity();
@@ -183,8 +195,9 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
     q = ge_add_niels<true>(q, select_niels<8>(tpa, ca));
     q = ge_add_niels<true>(q, select_niels<8>(tpb, cb));
   }
-  q = ge_add_cached_rt(q, ge_to_cached(ge_swap_xor(q, 1)), true);
-  q = ge_add_cached_rt(q, ge_to_cached(ge_swap_xor(q, 2)), false);
+  HSV_UNROLL
+  for (int mask = 1; mask < kCombLanes; mask <<= 1)
+    q = ge_add_cached_rt(q, ge_to_cached(ge_swap_xor(q, mask)), mask < kCombLanes / 2);
   __syncthreads();
   fe rx, ry;
   HSV_UNROLL
