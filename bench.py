@@ -364,7 +364,7 @@ def qc_cpu(reps=5):
     return res
 
 
-def mempool_bench(dev, n=1 << 20, tx_size=512, cpu_sample=1 << 17):
+def mempool_bench(dev, n=1 << 20, tx_size=512, cpu_sample=1 << 17, nstreams=2):
     """Mempool transactions: n client transactions of
     tx_size bytes (the reference benchmark's default, benchmark/fabfile.py),
     resident in HBM; one step = digest records + verification
@@ -374,20 +374,32 @@ def mempool_bench(dev, n=1 << 20, tx_size=512, cpu_sample=1 << 17):
     from hsverify import mempool, synth
     w = synth.transactions(n, tx_size=tx_size, seed=9)
     d = torch.from_numpy(w.txs.reshape(-1)).to(dev)
-    flags = torch.zeros(n, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
-    mempool.verify_transactions_device(d, None, tx_size=tx_size, n=n, flags=flags)
+    # consecutive batches alternate over nstreams streams, as for the C4 line
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(max(1, nstreams) - 1)]
+    outs = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in streams]
+    flags = outs[0]
+    for j, s in enumerate(streams):
+        mempool.verify_transactions_device(d, None, tx_size=tx_size, n=n, flags=outs[j], stream=s.cuda_stream)
     torch.cuda.synchronize(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    steps = 5
+    steps = 6
     e0.record(stream)
-    for _ in range(steps):
-        mempool.verify_transactions_device(d, None, tx_size=tx_size, n=n, flags=flags)
+    for s in streams[1:]:
+        s.wait_event(e0)
+    for i in range(steps):
+        j = i % len(streams)
+        mempool.verify_transactions_device(d, None, tx_size=tx_size, n=n, flags=outs[j], stream=streams[j].cuda_stream)
+    for s in streams[1:]:
+        ev = torch.cuda.Event()
+        ev.record(s)
+        stream.wait_event(ev)
     e1.record(stream)
     torch.cuda.synchronize(dev)
     ms = e0.elapsed_time(e1) / steps
     f = flags.cpu().numpy()
-    res = {"txs": n, "tx_size": tx_size, "ms_per_step": ms, "tx_per_s": n / (ms * 1e-3),
+    res = {"txs": n, "tx_size": tx_size, "ms_per_step": ms, "tx_per_s": n / (ms * 1e-3), "streams": len(streams),
+           "outputs_identical_across_streams": all(bool(torch.equal(outs[0], o)) for o in outs[1:]),
            "honest_all_accepted": bool((f[w.honest] & 1).all()),
            "corrupted_all_rejected": bool(not (f[~w.honest] & 1).any())}
     lib = _oracle()
@@ -674,7 +686,7 @@ def main():
         out["tc_latency"] = tc_latency(a.qc_reps, auto=True)
         _lib.load().hsv_set_auto_committee(1)
         out["committee_cache"] = committee_bench(a.qc_reps, dev)
-        out["mempool_tx"] = mempool_bench(dev)
+        out["mempool_tx"] = mempool_bench(dev, nstreams=nst)
         if world == 1 and not a.no_cpu_baseline:
             out["qc_cpu_baseline"] = qc_cpu()
         out["host_api"] = host_api_bench(w)

@@ -7,12 +7,13 @@
 // each loop body is read from the ISA (tools/isa_mix.py) to turn the times
 // into a mix-weighted ceiling.
 //
-// Build: hipcc --offload-arch=gfx950 -O3 -fno-slp-vectorize -std=c++17
+// Build: hipcc --offload-arch=gfx950 -O3 -fno-slp-vectorize -std=c++17 [-DHSV_FE26_PARALLEL_CARRY]
 //        -I hotstuff-digital-signature-benchmarking_amd/csrc tools/ubench_fe.hip -o tools/ubench_fe
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 
 #include "hsv_point.hpp"
 
@@ -217,7 +218,7 @@ static Cost cost_per_op(kfn k, int ops_per_iter, uint32_t *sink, unsigned long l
   return r;
 }
 
-int main() {
+int main(int argc, char **argv) {
   hipDeviceProp_t prop;
   (void)hipGetDeviceProperties(&prop, 0);
   uint32_t *sink;
@@ -235,7 +236,15 @@ int main() {
       {"ge_dbl_rt (with T)", k_dbl<true>, 1}, {"ge_add_cached_rt (no T)", k_add<false>, 1},
       {"ge_add_cached_rt (with T)", k_add<true>, 1},
   };
-  for (int bpc : {3, 4, 6, 8}) {
+  // argv: waves per SIMD to measure (default 3 4 6 8; 1 = a lone wave, the
+  // latency forms' situation)
+  int list[8] = {3, 4, 6, 8}, nl = 4;
+  if (argc > 1) {
+    nl = 0;
+    for (int i = 1; i < argc && nl < 8; ++i) list[nl++] = std::atoi(argv[i]);
+  }
+  for (int li = 0; li < nl; ++li) {
+    const int bpc = list[li];
     std::printf("%s CUs=%d waves/SIMD=%d (per wave-op per SIMD: wall ns, shader cycles, implied GHz)\n",
                 prop.gcnArchName, ncu, bpc);
     for (auto &e : tab) {
