@@ -437,7 +437,7 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", "--per-gpu", dest="n", type=int, default=1 << 20, help="triples per GPU")
     ap.add_argument("--variant", type=int, default=None)
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=3,
                     help="consecutive batches alternate over this many HIP streams, so a batch's launch can "
                          "start in the previous one's grid end (1: every batch on one stream)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20,

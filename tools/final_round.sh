@@ -16,7 +16,7 @@ python -c "import json; d=json.load(open('$OUT/${TAG}_bench.json')); r=d['roofli
 step c5; timeout -k 10 600 python bench.py --global-n 16777216 --steps 5 --warmup 1 --no-cpu-baseline --no-qc > $OUT/${TAG}_c5_2p24_1gpu_bench.json 2> $OUT/${TAG}_c5.err; rc=$?
 [ $rc -eq 0 ] || { tail -5 $OUT/${TAG}_c5.err; exit $rc; }
 python -c "import json; d=json.load(open('$OUT/${TAG}_c5_2p24_1gpu_bench.json')); print(d['value']/1e6, d['ms_per_step'])"
-step probe; timeout -k 10 200 python -u tools/pipeline_probe.py > $OUT/${TAG}_pipeline_probe.txt 2>&1; rc=$?
+step probe; timeout -k 10 300 python -u tools/pipeline_probe.py --rounds 5 > $OUT/${TAG}_pipeline_probe.txt 2>&1; rc=$?
 tail -4 $OUT/${TAG}_pipeline_probe.txt; [ $rc -eq 0 ] || exit $rc
 step rocprof; cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_prof -o bench -- python3 $R/bench.py --steps 5 --warmup 1 --streams 1 --no-cpu-baseline --no-qc > $OUT/${TAG}_prof_bench.json 2> $OUT/${TAG}_prof.err; rc=$?
