@@ -419,19 +419,26 @@ HSV_INL void lat_lehmer_lean_to_128(uint32_t a[8], uint32_t b[8], uint32_t ta[6]
     const double thr = ldexp(1.0, 128 - s);
     double A = 1.0, B = 0.0, C = 0.0, D = 1.0;
     bool go = active;
+    // At most kLatRoundSteps steps per round: a lane that could go on resumes
+    // in the next round (any prefix of exact steps is a valid state).  Rounds
+    // are wave-synchronous, so the inner loop runs the wave's longest round;
+    // the cap trims that tail (121 -> 99 inner iterations per wave in a
+    // Python simulation of this loop over random challenges, rounds unchanged
+    // at 6.1).
+    constexpr int kLatRoundSteps = 17;
     HSV_NOUNROLL
-    for (int j = 0; j < 64; ++j) {
+    for (int j = 0; j < kLatRoundSteps; ++j) {
       if (!hsv_any(go)) break;
       // true pair: r0 = x + A al + B be, r1 = y + C al + D be, al, be in [0, 1)
       // (lat_lehmer_to_128); q is exact iff 0 <= r2 < r1 over the box.  The
       // step is taken when q is exact; the round goes on only while r2 is
-      // provably >= 2^128.
+      // provably >= 2^128.  |nD| < 2^31 also bounds q and |nC|: in a Euclid
+      // cofactor matrix |D| >= |C| and |D| >= 1, so |nD| >= |nC| and |nD| >= q.
       bool ok = go && y >= 1.0;
       const double q = ok ? lat_floor_div(x, y) : 0.0;
       const double nC = fma(-q, C, A), nD = fma(-q, D, B), ny = fma(-q, y, x);
       const double lo = ny + fmin(nC, nD);
-      ok = ok && q >= 1.0 && q < 0x1p30 && fabs(nC) < 0x1p31 && fabs(nD) < 0x1p31 && lo >= 0.0 &&
-           (y - ny) + fmin(C - nC, D - nD) >= 1.0;
+      ok = ok && q >= 1.0 && fabs(nD) < 0x1p31 && lo >= 0.0 && (y - ny) + fmin(C - nC, D - nD) >= 1.0;
       if (ok) {
         A = C; B = D; C = nC; D = nD;
         x = y; y = ny;

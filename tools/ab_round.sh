@@ -10,6 +10,6 @@ if [ -n "$LIBS" ]; then
   tail -$(( $(echo $LIBS | wc -w) + 1 )) $OUT/${TAG}_ab.txt; [ $rc -eq 0 ] || exit $rc
 fi
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_prof -o bench -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-qc > $OUT/${TAG}_prof_bench.json 2> $OUT/${TAG}_prof.err; rc=$?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_prof -o bench -- python3 $R/bench.py --steps 5 --warmup 1 --streams 1 --no-cpu-baseline --no-qc > $OUT/${TAG}_prof_bench.json 2> $OUT/${TAG}_prof.err; rc=$?
 [ $rc -eq 0 ] || { tail -5 $OUT/${TAG}_prof.err; exit $rc; }
 f=$(find $OUT/${TAG}_prof -name "*kernel_stats.csv" | head -1); cp "$f" $OUT/${TAG}_kernel_stats.csv; cut -d, -f1-4 $OUT/${TAG}_kernel_stats.csv | head -4
