@@ -109,6 +109,38 @@ def test_many_concurrent_small_calls(mods, golden):
     assert not errors
 
 
+def test_device_batches_on_concurrent_streams(mods, golden):
+    """bench.py's form: consecutive device batches alternating over three
+    streams, with a mid-size batch (two-pass kernels) and a small one (latency
+    form) in flight together; each launch takes its workspace from the
+    library's pool on its own stream.  Every output equals the one-stream
+    result and the golden flags."""
+    import torch
+    _, _, synth, verifier = mods
+    dev = torch.device("cuda", 0)
+    n = (1 << 15) + 333
+    w = synth.independent_triples(n, seed=77, corrupt_frac=0.05)
+    pk, sig, msg = (torch.from_numpy(x).to(dev) for x in (w.pk, w.sig, w.msg))
+    g = golden
+    gpk, gsig, gmsg = (torch.from_numpy(np.ascontiguousarray(g[k])).to(dev) for k in ("pk", "sig", "msg"))
+    ref = torch.zeros(n, dtype=torch.uint8, device=dev)
+    verifier.verify_device(pk, sig, msg, ref)
+    torch.cuda.synchronize(dev)
+    streams = [torch.cuda.Stream(dev) for _ in range(3)]
+    outs = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(6)]
+    gouts = [torch.zeros(len(g["flags"]), dtype=torch.uint8, device=dev) for _ in range(6)]
+    for i in range(6):
+        s = streams[i % 3].cuda_stream
+        verifier.verify_device(pk, sig, msg, outs[i], stream=s)
+        verifier.verify_device(gpk, gsig, gmsg, gouts[i], stream=s)
+    torch.cuda.synchronize(dev)
+    for i in range(6):
+        assert torch.equal(outs[i], ref), i
+        assert (gouts[i].cpu().numpy() == g["flags"]).all(), i
+    f = ref.cpu().numpy()
+    assert (f[w.honest] & o.STRICT_OK).all() and not (f[~w.honest] & o.STRICT_OK).any()
+
+
 def test_committee_survives_shutdown(mods, hsv, golden):
     _, committee, _, _ = mods
     keys = golden["pk"][:8]
