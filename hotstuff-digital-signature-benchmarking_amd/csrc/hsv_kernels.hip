@@ -144,6 +144,12 @@ struct GlobalVarTab {
     for (int q = 0; q < 8; ++q) {
 #ifdef HSV_TIMING_STUB_TABLE_STORES  // timing probe only: entries computed, never stored
       asm volatile("" ::"v"(w[4 * q]), "v"(w[4 * q + 1]), "v"(w[4 * q + 2]), "v"(w[4 * q + 3]));
+#elif defined(HSV_VT_NT_STORES)  // A/B probe: streaming (nontemporal) table stores
+      {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 v = {w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(e + q));
+      }
 #else
       e[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 #endif
