@@ -256,7 +256,11 @@ int comb_table_for(DevCtx &c, int v, const uint32_t **out) {
 }
 
 void stage_copy(uint8_t *dst, const uint8_t *src, size_t bytes) {
-  constexpr size_t kSplit = size_t(8) << 20;
+  static const size_t kSplit = [] {  // HSV_STAGE_SPLIT_MB: measurement switch
+    const char *v = std::getenv("HSV_STAGE_SPLIT_MB");
+    const int mb = v ? std::atoi(v) : 0;
+    return size_t(mb >= 1 && mb <= 64 ? mb : 8) << 20;
+  }();
   const size_t nt = std::min<size_t>(4, bytes / kSplit);
   if (nt < 2) {
     std::memcpy(dst, src, bytes);
@@ -302,10 +306,18 @@ int device_for_call(const void *d_ptr, void *stream, int *dev) {
 namespace {
 
 // Records at pk + i*pk_stride etc. (msg_stride 0 = shared), [0, n) on one
-// device, chunk by chunk.  Batches of at least 2 * kPipeChunk items run as a
+// device, chunk by chunk.  Batches of at least 2 * pipe_chunk() items run as a
 // two-stage pipeline: two staging buffers and two streams, so the host packs
 // chunk i+1 and the DMA engine copies it while the kernels verify chunk i.
-constexpr size_t kPipeChunk = size_t(1) << 18;  // 32 MiB of inputs per pipelined chunk
+constexpr size_t kPipeChunkDefault = size_t(1) << 17;  // 16 MiB of inputs per pipelined chunk
+size_t pipe_chunk() {  // HSV_PIPE_CHUNK_LOG2 (14..22): measurement switch
+  static const size_t c = [] {
+    const char *v = std::getenv("HSV_PIPE_CHUNK_LOG2");
+    const int l = v ? std::atoi(v) : 0;
+    return (l >= 14 && l <= 22) ? (size_t(1) << l) : kPipeChunkDefault;
+  }();
+  return c;
+}
 
 int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t *sig, size_t sig_stride,
                   const uint8_t *msg, size_t msg_stride, size_t n, uint8_t *flags_out) {
@@ -319,8 +331,9 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
   if (rc != HSV_OK) return rc;
   SlotLease lease(c);
   Slot &s = lease.slot();
-  const bool pipe = !no_pipe && n >= 2 * kPipeChunk;
-  const size_t chunk = pipe ? kPipeChunk : std::min(n, kChunk);
+  const size_t pchunk = pipe_chunk();
+  const bool pipe = !no_pipe && n >= 2 * pchunk;
+  const size_t chunk = pipe ? pchunk : std::min(n, kChunk);
   const int nbuf = pipe ? 2 : 1;
   const size_t pk_off = 0;
   const size_t sig_off = round_up(chunk * 32, kAlign);
