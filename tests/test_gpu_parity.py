@@ -305,7 +305,7 @@ def test_c4_full_size_properties(api, oracle_lib):
 
 
 def test_host_api_pipelined_chunks_match_device_api(api, oracle_lib):
-    """Host batches of >= 2^19 items run as a two-stream pipeline of 2^18-item
+    """Host batches of >= 2^18 items run as a two-stream pipeline of 2^17-item
     chunks (hsv_capi.cpp run_on_device): an uneven tail chunk, every flag equal
     to the device-resident launch, and an oracle-checked sample."""
     import torch
