@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """Back-to-back C4 launches (2^20 triples in HBM) on one stream against the
-same launches alternating over two or three streams, where a launch can start in the
+same launches alternating over two or more streams, where a launch can start in the
 previous launch's grid end.  Both forms produce the
 same flags; prints ms per launch (median of rounds) for each.
 
-python tools/pipeline_probe.py [--n 1048576] [--steps 20] [--rounds 3]
+python tools/pipeline_probe.py [--n 1048576] [--steps 20] [--rounds 3] [--max-streams 3]
 """
 import argparse
 import os
@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--max-streams", type=int, default=3)
     a = ap.parse_args()
     import torch
     from hsverify import _lib, synth, verifier
@@ -28,7 +29,8 @@ def main():
     dev = torch.device("cuda", 0)
     w = synth.independent_triples(a.n, seed=0xC4 * 1000, corrupt_frac=0.05, nthreads=16)
     pk, sig, msg = (torch.from_numpy(x).to(dev) for x in (w.pk, w.sig, w.msg))
-    streams = [torch.cuda.Stream(dev) for _ in range(3)]
+    ks = list(range(1, a.max_streams + 1))
+    streams = [torch.cuda.Stream(dev) for _ in ks]
     outs = [(torch.zeros(a.n, dtype=torch.uint8, device=dev),
              torch.zeros((a.n + 31) // 32, dtype=torch.int32, device=dev)) for _ in streams]
 
@@ -41,13 +43,14 @@ def main():
         torch.cuda.synchronize(dev)
         return (time.perf_counter() - t) * 1e3 / a.steps
 
-    run(1), run(2), run(3)  # warm-up (workspace pools, tables)
-    res = {1: [], 2: [], 3: []}
+    for k in ks:  # warm-up (workspace pools, tables)
+        run(k)
+    res = {k: [] for k in ks}
     for _ in range(a.rounds):
-        for k in (1, 2, 3):
+        for k in ks:
             res[k].append(run(k))
     same = all(torch.equal(outs[0][0], o[0]) and torch.equal(outs[0][1], o[1]) for o in outs[1:])
-    for k in (1, 2, 3):
+    for k in ks:
         med = statistics.median(res[k])
         print(f"{k} stream(s): {med:.3f} ms per launch ({a.n / med / 1e3:.2f} M verif/s) "
               f"all {[round(x, 3) for x in res[k]]}")
