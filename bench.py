@@ -128,6 +128,31 @@ def _oracle():
     return lib
 
 
+def dalek_probe():
+    """BASELINE.md asks for ed25519-dalek itself as the CPU baseline when the
+    GPU box can build it: record whether cargo / rustc and an offline crate
+    registry exist here.  (They never have: the baseline is then the C port.)"""
+    import shutil
+    res = {"cargo": shutil.which("cargo"), "rustc": shutil.which("rustc")}
+    for tool in ("cargo", "rustc"):
+        if res[tool]:
+            try:
+                res[f"{tool}_version"] = subprocess.run([tool, "--version"], capture_output=True, text=True,
+                                                        timeout=30).stdout.strip()
+            except (OSError, subprocess.SubprocessError) as e:
+                res[f"{tool}_version"] = f"error: {e}"
+    home = os.environ.get("CARGO_HOME", os.path.expanduser("~/.cargo"))
+    reg = os.path.join(home, "registry")
+    res["registry"] = reg if os.path.isdir(reg) else None
+    res["ed25519_dalek_in_registry"] = bool(res["registry"]) and any(
+        "ed25519-dalek" in d for _, dirs, _ in os.walk(reg) for d in dirs)
+    res["dalek_buildable"] = bool(res["cargo"] and res["ed25519_dalek_in_registry"])
+    res["consequence"] = ("dalek buildable: not wired in this round" if res["dalek_buildable"] else
+                          "no cargo / no offline ed25519-dalek crate on this box: the baseline is the C port "
+                          "(oracle/ed25519_oracle.c), kind 'port'")
+    return res
+
+
 def cpu_baseline(w, gpu_flags, sample):
     """C4 on the host cores: the C port of dalek's verify_strict per item (the
     reference's Signature::verify, which gives the per-signature vector), and
@@ -153,7 +178,7 @@ def cpu_baseline(w, gpu_flags, sample):
                   f"double-scalar multiplication), {threads} threads, {dt:.2f} s wall",
         "sample_parity_vs_gpu": bool((out == gpu_flags[:m]).all()),
         "nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": quota,
-        "cpu_model": cpu_model(),
+        "cpu_model": cpu_model(), "dalek_probe": dalek_probe(),
         "batch64": {"value": m / dt64, "unit": "verif/s", "cores": threads,
                     "algorithm": "dalek verify_batch (random linear combination, Straus MSM) over chunks of 64, "
                                  "verify_strict per item for the chunks that fail",
@@ -182,13 +207,15 @@ def member_corrupted(make, committee, seed, frac=0.05):
     """A C3 certificate with `frac` corrupted votes whose keys all stay committee
     members: the reference rejects a vote by a non-member before any signature
     check (QC::verify / TC::verify stake lookups, consensus/src/messages.rs:186,296),
-    so the small_order_A kind (which swaps the key) is reverted to an honest vote."""
+    so the kinds that swap the key (small-order and mixed-order A) are reverted
+    to honest votes."""
     from hsverify import synth
     w = make(committee, seed=seed, corrupt_frac=frac)
     clean = make(committee, seed=seed)
-    swap = w.kind == synth.CORRUPTIONS.index("small_order_A")
+    swap = np.isin(w.kind, [synth.CORRUPTIONS.index(k) for k in synth.KEY_KINDS])
     w.pk[swap], w.sig[swap] = clean.pk[swap], clean.sig[swap]
     w.honest[swap] = True
+    w.accept[swap] = True
     return w
 
 
@@ -227,7 +254,7 @@ def qc_latency(reps, auto=True):
     call = lambda: lib.hsv_verify_batch_packed(digest, packed, w.n)
     settle(call)
     assert call() == 0
-    res["n1000_votes667_corrupt5pct"] = dict(_p(_timed(call, reps)), corrupted=int((~w.honest).sum()))
+    res["n1000_votes667_corrupt5pct"] = dict(_p(_timed(call, reps)), corrupted=int((~w.accept).sum()))
     # one strict verification (Vote::verify / Block::verify, consensus/src/messages.rs:136-146)
     w = synth.qc_votes(4, seed=4)
     pk0, sig0, d0 = bytes(w.pk[0]), bytes(w.sig[0]), bytes(w.msg)
@@ -400,8 +427,8 @@ def mempool_bench(dev, n=1 << 20, tx_size=512, cpu_sample=1 << 17, nstreams=2):
     f = flags.cpu().numpy()
     res = {"txs": n, "tx_size": tx_size, "ms_per_step": ms, "tx_per_s": n / (ms * 1e-3), "streams": len(streams),
            "outputs_identical_across_streams": all(bool(torch.equal(outs[0], o)) for o in outs[1:]),
-           "honest_all_accepted": bool((f[w.honest] & 1).all()),
-           "corrupted_all_rejected": bool(not (f[~w.honest] & 1).any())}
+           "honest_all_accepted": bool((f[w.accept] & 1).all()),
+           "corrupted_all_rejected": bool(not (f[~w.accept] & 1).any())}
     lib = _oracle()
     m = min(cpu_sample, n)
     threads, _ = host_cores()
@@ -415,19 +442,42 @@ def mempool_bench(dev, n=1 << 20, tx_size=512, cpu_sample=1 << 17, nstreams=2):
     return res
 
 
-def host_api_bench(w, reps=3):
+def host_api_bench(w, dev, reps=5):
     """The drop-in boundary hands over host buffers: hsv_verify on the C4 batch
-    from numpy arrays (pinned staging, H2D, kernels, D2H), PCIe-inclusive."""
-    from hsverify import verifier
+    from numpy arrays (pinned staging, H2D, kernels, D2H), PCIe-inclusive.
+    Beside it: the library's own account of the call (host time spent packing
+    into pinned staging, bytes sent host-to-device) and the link's H2D rate for
+    the same bytes measured alone (one pinned 128 MiB copy, HIP events)."""
+    import torch
+    from hsverify import _testing, verifier
     verifier.verify_flags(w.pk, w.sig, w.msg)
-    ts = []
+    ts, stats = [], []
     for _ in range(reps):
         t0 = time.perf_counter()
         f = verifier.verify_flags(w.pk, w.sig, w.msg)
         ts.append(time.perf_counter() - t0)
-    ms = float(np.median(ts) * 1e3)
-    return {"items": int(w.n), "ms": ms, "verif_per_s": w.n / (ms * 1e-3),
-            "honest_all_accepted": bool((f[w.honest] & 1).all())}
+        stats.append(_testing.host_call_stats())
+    k = int(np.argsort(ts)[len(ts) // 2])
+    ms = float(ts[k] * 1e3)
+    st = stats[k]
+    nbytes = w.n * 128
+    src = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    dst = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(3):
+        dst.copy_(src, non_blocking=True)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    h2d_ms = e0.elapsed_time(e1) / 3
+    return {"items": int(w.n), "ms": ms, "verif_per_s": w.n / (ms * 1e-3), "reps": reps,
+            "pack_ms": st["pack_ms"], "pack_threads": _testing.pack_threads() + 1,
+            "h2d_bytes": st["h2d_bytes"], "input_rate_GBps": st["h2d_bytes"] / (ms * 1e-3) / 1e9,
+            "h2d_alone_ms_for_128MiB": h2d_ms, "h2d_link_GBps": nbytes / (h2d_ms * 1e-3) / 1e9,
+            "honest_all_accepted": bool((f[w.accept] & 1).all()),
+            "corrupted_all_rejected": bool(not (f[~w.accept] & 1).any())}
 
 
 def parse_args(argv=None):
@@ -442,7 +492,8 @@ def parse_args(argv=None):
                          "start in the previous one's grid end (1: every batch on one stream)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20,
                     help="triples the CPU port verifies (default: the whole C4 batch)")
-    ap.add_argument("--qc-reps", type=int, default=200)
+    ap.add_argument("--qc-reps", type=int, default=1000,
+                    help="repetitions per latency figure (BASELINE.md: >= 1,000 for C2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-qc", action="store_true")
     ap.add_argument("--global-n", type=int, default=None,
@@ -609,14 +660,15 @@ def main():
         r["frac"] = a.n * WORK_MACS / (r["kernel_ms"] * 1e-3) / PEAK_MACS
 
     f = flags.cpu().numpy()
-    honest_ok = bool((f[w.honest] & 1).all())
-    corrupt_rejected = bool(not (f[~w.honest] & 1).any())
+    honest_ok = bool((f[w.accept] & 1).all())
+    corrupt_rejected = bool(not (f[~w.accept] & 1).any())
+    faults = verifier.device_faults(local_rank)  # device self-checks of every launch above
     global_accepted = int((f & 1).sum())
     if world > 1:
         # host gather of the per-signature STRICT_OK bitmask (outside the timed region)
         from hsverify import dist as hd
         strict_all = hd.gather_strict(f, a.n * world)
-        honest_all = hd.gather_strict(w.honest.astype(np.uint8), a.n * world)
+        honest_all = hd.gather_strict(w.accept.astype(np.uint8), a.n * world)
         honest_ok = bool(strict_all[honest_all].all())
         corrupt_rejected = bool(not strict_all[~honest_all].any())
         global_accepted = int(strict_all.sum())
@@ -676,7 +728,9 @@ def main():
             "per_rank": per_rank,
         },
         "checks": {"honest_all_accepted": honest_ok, "corrupted_all_rejected": corrupt_rejected,
-                   "strict_accepted_global": global_accepted, "outputs_identical_across_streams": same_out},
+                   "strict_accepted_global": global_accepted, "outputs_identical_across_streams": same_out,
+                   "device_self_check_faults": faults,
+                   "expected_accept": "honest items and the mixed-order-A items with k = 0 mod 8"},
     }
     if world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(w, f, a.cpu_sample)
@@ -689,7 +743,7 @@ def main():
         out["mempool_tx"] = mempool_bench(dev, nstreams=nst)
         if world == 1 and not a.no_cpu_baseline:
             out["qc_cpu_baseline"] = qc_cpu()
-        out["host_api"] = host_api_bench(w)
+        out["host_api"] = host_api_bench(w, dev)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

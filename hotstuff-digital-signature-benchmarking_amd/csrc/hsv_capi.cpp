@@ -13,6 +13,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -255,25 +257,159 @@ int comb_table_for(DevCtx &c, int v, const uint32_t **out) {
   return HSV_OK;
 }
 
+// ---- persistent host threads for the staging copies ----------------------------
+// A host-buffer batch must be packed into pinned memory before the DMA engine
+// can read it (128 MiB for 2^20 triples).  One thread copies ~10 GB/s, which
+// made the pack -- not PCIe -- the bound of the drop-in path in round 2.  The
+// pool's threads and the caller split every pack; a caller that finds the
+// pool busy (another thread's pack) copies its parts itself.
+namespace {
+
+class PackPool {
+ public:
+  static PackPool &get() {
+    static PackPool p;
+    return p;
+  }
+  int threads() const { return (int)workers_.size(); }
+  // fn(part) for part in [0, nparts), spread over the pool and the caller
+  void run(int nparts, const std::function<void(int)> &fn) {
+    std::unique_lock<std::mutex> busy(job_mu_, std::try_to_lock);
+    if (!busy.owns_lock() || workers_.empty() || nparts < 2) {
+      for (int p = 0; p < nparts; ++p) fn(p);
+      return;
+    }
+    auto job = std::make_shared<Job>();
+    job->fn = &fn;
+    job->nparts = nparts;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = job;
+    }
+    cv_.notify_all();
+    work(*job);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return job->done == job->nparts; });
+    job_.reset();
+  }
+
+ private:
+  // A job outlives late workers: one that wakes after the job finished finds
+  // its part counter exhausted and never calls fn.
+  struct Job {
+    const std::function<void(int)> *fn = nullptr;
+    int nparts = 0;
+    int done = 0;  // guarded by mu_
+    std::atomic<int> next{0};
+  };
+
+  PackPool() {
+    int n = 6;  // the GPU box's cgroup gives a job 16 CPUs; 7 copying threads
+    if (const char *v = std::getenv("HSV_PACK_THREADS")) n = std::atoi(v);
+    n = std::max(0, std::min(n, 32));
+    for (int i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
+  }
+  ~PackPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : workers_) t.join();
+  }
+  void work(Job &j) {
+    int mine = 0;
+    for (int p; (p = j.next.fetch_add(1)) < j.nparts;) {
+      (*j.fn)(p);
+      ++mine;
+    }
+    std::lock_guard<std::mutex> lk(mu_);
+    j.done += mine;
+    if (j.done == j.nparts) done_cv_.notify_all();
+  }
+  void loop() {
+    std::shared_ptr<Job> last;
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || (job_ && job_ != last); });
+      if (stop_) return;
+      last = job_;
+      lk.unlock();
+      work(*last);
+      lk.lock();
+    }
+  }
+
+  std::mutex job_mu_;  // one pack at a time
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  std::shared_ptr<Job> job_;
+  bool stop_ = false;
+  std::vector<std::thread> workers_;
+};
+
+constexpr size_t kPackPart = size_t(1) << 20;  // bytes per part of a split copy
+
+}  // namespace
+
 void stage_copy(uint8_t *dst, const uint8_t *src, size_t bytes) {
-  static const size_t kSplit = [] {  // HSV_STAGE_SPLIT_MB: measurement switch
-    const char *v = std::getenv("HSV_STAGE_SPLIT_MB");
-    const int mb = v ? std::atoi(v) : 0;
-    return size_t(mb >= 1 && mb <= 64 ? mb : 8) << 20;
-  }();
-  const size_t nt = std::min<size_t>(4, bytes / kSplit);
-  if (nt < 2) {
+  const int nparts = (int)std::min<size_t>(64, (bytes + kPackPart - 1) / kPackPart);
+  if (nparts < 2) {
     std::memcpy(dst, src, bytes);
     return;
   }
-  std::vector<std::thread> th;
-  const size_t part = (bytes / nt + 63) & ~size_t(63);
-  for (size_t t = 1; t < nt; ++t) {
-    const size_t lo = std::min(bytes, t * part), hi = std::min(bytes, (t + 1) * part);
-    if (hi > lo) th.emplace_back([=] { std::memcpy(dst + lo, src + lo, hi - lo); });
+  PackPool::get().run(nparts, [&](int p) {
+    const size_t lo = bytes * p / nparts & ~size_t(63), hi = p + 1 == nparts ? bytes : bytes * (p + 1) / nparts & ~size_t(63);
+    std::memcpy(dst + lo, src + lo, hi - lo);
+  });
+}
+
+// ---- device self-check words ------------------------------------------------------
+int check_faults(const uint8_t *words, const char *where) {
+  uint32_t w[2];
+  std::memcpy(w, words, sizeof(w));
+  if (!(w[0] | w[1])) return HSV_OK;
+  std::string why;
+  if (w[0]) why = "a final point failed the curve self-check";
+  if (w[1]) why += std::string(why.empty() ? "" : "; ") + "a workspace canary changed";
+  return fail(HSV_ERR_DEVICE_FAULT, std::string(where) + ": device self-check failed (" + why +
+                                        "): the flags of this launch are not a verdict");
+}
+
+int device_fault_words(DevCtx &c, uint32_t **out) {
+  std::lock_guard<std::mutex> lk(c.table_mu);
+  if (!c.d_fault) {
+    uint32_t *p = nullptr;
+    hipError_t e = hipMalloc(&p, 256);
+    if (e == hipSuccess) e = hipMemset(p, 0, 256);
+    if (e != hipSuccess) {
+      if (p) (void)hipFree(p);
+      return hip_fail("allocating the device self-check words", e);
+    }
+    c.d_fault = p;
   }
-  std::memcpy(dst, src, std::min(bytes, part));
-  for (auto &x : th) x.join();
+  *out = c.d_fault;
+  return HSV_OK;
+}
+
+SideStreamLease::SideStreamLease(DevCtx &c) : c_(c) {
+  std::lock_guard<std::mutex> lk(c.side_mu);
+  if (!c.side_free.empty()) {
+    s_ = c.side_free.back();
+    c.side_free.pop_back();
+    return;
+  }
+  if (hipStreamCreateWithFlags(&s_, hipStreamNonBlocking) != hipSuccess) {
+    s_ = nullptr;
+    return;
+  }
+  c.side_all.push_back(s_);
+}
+
+SideStreamLease::~SideStreamLease() {
+  if (!s_) return;
+  std::lock_guard<std::mutex> lk(c_.side_mu);
+  c_.side_free.push_back(s_);
 }
 
 int pointer_device(const void *p) {
@@ -319,10 +455,23 @@ size_t pipe_chunk() {  // HSV_PIPE_CHUNK_LOG2 (14..22): measurement switch
   return c;
 }
 
+// Stats of the calling thread's last host-buffer call (hsv_host_call_stats,
+// a measurement hook): host time spent packing into pinned staging, bytes
+// copied host-to-device, and the call's wall time.
+thread_local double t_pack_ms = 0, t_call_ms = 0;
+thread_local uint64_t t_h2d_bytes = 0;
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
 int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t *sig, size_t sig_stride,
                   const uint8_t *msg, size_t msg_stride, size_t n, uint8_t *flags_out) {
   static const bool no_pipe = std::getenv("HSV_NO_PIPELINE") != nullptr;        // measurement switch
   static const bool no_zero_copy = std::getenv("HSV_NO_ZERO_COPY") != nullptr;  // measurement switch
+  const auto t_call = std::chrono::steady_clock::now();
+  t_pack_ms = 0;
+  t_h2d_bytes = 0;
   DeviceGuard guard(c.device);
   if (guard.status() != hipSuccess) return hip_fail("hipSetDevice", guard.status());
   const int v = variant();
@@ -335,42 +484,70 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
   const bool pipe = !no_pipe && n >= 2 * pchunk;
   const size_t chunk = pipe ? pchunk : std::min(n, kChunk);
   const int nbuf = pipe ? 2 : 1;
+  // staging layout of one buffer: pk 32 | sig 64 | msg 32 (or one shared
+  // digest) | flags 1 | self-check words (kFaultBytes); the same in HBM
   const size_t pk_off = 0;
   const size_t sig_off = round_up(chunk * 32, kAlign);
   const size_t msg_off = sig_off + round_up(chunk * 64, kAlign);
   const size_t msg_bytes = msg_stride ? chunk * 32 : 32;
   const size_t flag_off = msg_off + round_up(msg_bytes, kAlign);
-  const size_t total = flag_off + round_up(chunk, kAlign);
+  const size_t fault_off = flag_off + round_up(chunk, kAlign);
+  const size_t total = fault_off + kAlign;
   rc = slot_prepare(s, total * nbuf, total * nbuf);
   if (rc == HSV_OK && pipe) rc = slot_stream2(s);
   if (rc != HSV_OK) return rc;
   size_t pend_base[2] = {0, 0}, pend_m[2] = {0, 0};
-  // wait for buffer b's chunk and hand its flags to the caller
+  // an error leaves no copy or kernel of this call in flight on the slot
+  auto drain = [&](int code) -> int {
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (s.stream2) (void)hipStreamSynchronize(s.stream2);
+    return code;
+  };
+  // wait for buffer b's chunk, check its self-check words, hand its flags over
   auto retire = [&](int b) -> int {
     if (pend_m[b] == 0) return HSV_OK;
     const hipError_t e = hipStreamSynchronize(b ? s.stream2 : s.stream);
     if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
-    std::memcpy(flags_out + pend_base[b], s.h_buf + (size_t)b * total + flag_off, pend_m[b]);
+    const uint8_t *h = s.h_buf + (size_t)b * total;
+    const int frc = check_faults(h + fault_off, "verify");
+    if (frc != HSV_OK) return frc;
+    std::memcpy(flags_out + pend_base[b], h + flag_off, pend_m[b]);
     pend_m[b] = 0;
     return HSV_OK;
+  };
+  // pack items [base, base + m) into the dense layout the kernels read, split
+  // over the pack pool by item range
+  auto pack = [&](uint8_t *h, size_t base, size_t m) {
+    const int nparts = (int)std::min<size_t>(64, (m * 128 + kPackPart - 1) / kPackPart);
+    auto part = [&](int p) {
+      const size_t lo = m * p / nparts, hi = m * (p + 1) / nparts;
+      if (pk_stride == 32) std::memcpy(h + pk_off + 32 * lo, pk + (base + lo) * 32, (hi - lo) * 32);
+      else for (size_t i = lo; i < hi; ++i) std::memcpy(h + pk_off + 32 * i, pk + (base + i) * pk_stride, 32);
+      if (sig_stride == 64) std::memcpy(h + sig_off + 64 * lo, sig + (base + lo) * 64, (hi - lo) * 64);
+      else for (size_t i = lo; i < hi; ++i) std::memcpy(h + sig_off + 64 * i, sig + (base + i) * sig_stride, 64);
+      if (msg_stride == 32) std::memcpy(h + msg_off + 32 * lo, msg + (base + lo) * 32, (hi - lo) * 32);
+      else if (msg_stride != 0)
+        for (size_t i = lo; i < hi; ++i) std::memcpy(h + msg_off + 32 * i, msg + (base + i) * msg_stride, 32);
+    };
+    if (nparts < 2) part(0);
+    else PackPool::get().run(nparts, part);
+    if (msg_stride == 0) std::memcpy(h + msg_off, msg, 32);
+    // a flag the kernels failed to write reads as a rejection, never as an
+    // earlier call's verdict; the self-check words start at zero
+    std::memset(h + flag_off, 0, m);
+    std::memset(h + fault_off, 0, kFaultBytes);
   };
   int b = 0;
   for (size_t base = 0; base < n; base += chunk, b = (b + 1) % nbuf) {
     const size_t m = std::min(chunk, n - base);
     rc = retire(b);
-    if (rc != HSV_OK) return rc;
+    if (rc != HSV_OK) return drain(rc);
     hipStream_t st = b ? s.stream2 : s.stream;
     uint8_t *h = s.h_buf + (size_t)b * total;
     uint8_t *d = s.d_buf + (size_t)b * total;
-    // pack into the dense layout the kernel reads (pk 32 | sig 64 | msg 32)
-    if (pk_stride == 32) stage_copy(h + pk_off, pk + base * 32, m * 32);
-    else for (size_t i = 0; i < m; ++i) std::memcpy(h + pk_off + 32 * i, pk + (base + i) * pk_stride, 32);
-    if (sig_stride == 64) stage_copy(h + sig_off, sig + base * 64, m * 64);
-    else for (size_t i = 0; i < m; ++i) std::memcpy(h + sig_off + 64 * i, sig + (base + i) * sig_stride, 64);
-    if (msg_stride == 0) std::memcpy(h + msg_off, msg, 32);
-    else if (msg_stride == 32) stage_copy(h + msg_off, msg + base * 32, m * 32);
-    else for (size_t i = 0; i < m; ++i) std::memcpy(h + msg_off + 32 * i, msg + (base + i) * msg_stride, 32);
-    const size_t in_bytes = msg_off + (msg_stride ? m * 32 : 32);
+    const auto t_pack = std::chrono::steady_clock::now();
+    pack(h, base, m);
+    t_pack_ms += ms_since(t_pack);
     // small batches (a QC of non-cached keys, a single vote): the kernels read
     // the pinned staging buffer and write the flags through its device
     // mapping, so no copy launches sit on the latency path
@@ -378,26 +555,31 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
     if (!no_zero_copy && n <= kZeroCopyMax && hipHostGetDevicePointer(&hd, h, 0) == hipSuccess && hd) {
       uint8_t *dh = static_cast<uint8_t *>(hd);
       hipError_t e = hsv_launch_verify(v, dh + pk_off, 32, dh + sig_off, 64, dh + msg_off, msg_stride ? 32 : 0,
-                                       (uint32_t)m, dh + flag_off, nullptr, comb_b, st);
-      if (e != hipSuccess) return hip_fail("verify kernel launch", e);
+                                       (uint32_t)m, dh + flag_off, nullptr, comb_b,
+                                       reinterpret_cast<uint32_t *>(dh + fault_off), st);
+      if (e != hipSuccess) return drain(hip_fail("verify kernel launch", e));
       pend_base[b] = base;
       pend_m[b] = m;
       continue;
     }
+    // inputs, the zeroed flags and the zeroed self-check words in one copy
+    const size_t in_bytes = fault_off + kFaultBytes;
     hipError_t e = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, st);
-    if (e != hipSuccess) return hip_fail("hipMemcpyAsync H2D", e);
+    if (e != hipSuccess) return drain(hip_fail("hipMemcpyAsync H2D", e));
+    t_h2d_bytes += in_bytes;
     e = hsv_launch_verify(v, d + pk_off, 32, d + sig_off, 64, d + msg_off, msg_stride ? 32 : 0, (uint32_t)m,
-                          d + flag_off, nullptr, comb_b, st);
-    if (e != hipSuccess) return hip_fail("verify kernel launch", e);
-    e = hipMemcpyAsync(h + flag_off, d + flag_off, m, hipMemcpyDeviceToHost, st);
-    if (e != hipSuccess) return hip_fail("hipMemcpyAsync D2H", e);
+                          d + flag_off, nullptr, comb_b, reinterpret_cast<uint32_t *>(d + fault_off), st);
+    if (e != hipSuccess) return drain(hip_fail("verify kernel launch", e));
+    e = hipMemcpyAsync(h + flag_off, d + flag_off, fault_off + kFaultBytes - flag_off, hipMemcpyDeviceToHost, st);
+    if (e != hipSuccess) return drain(hip_fail("hipMemcpyAsync D2H", e));
     pend_base[b] = base;
     pend_m[b] = m;
   }
   for (int k = 0; k < nbuf; ++k) {
     rc = retire(k);
-    if (rc != HSV_OK) return rc;
+    if (rc != HSV_OK) return drain(rc);
   }
+  t_call_ms = ms_since(t_call);
   return HSV_OK;
 }
 
@@ -469,22 +651,35 @@ int hsv_set_virtual_shards(int k) {
   return HSV_OK;
 }
 
+// Lifecycle call: must not run concurrently with verify calls (hsv.h).  It
+// still quiesces first -- every slot locked and drained, every side stream
+// drained, the device idle -- before it frees the tables those calls read.
 void hsv_shutdown(void) {
   auto_committee_shutdown();
   Global &g = G();
   std::lock_guard<std::mutex> lk(g.mu);
   for (DevCtx *c : g.ctx) {
     DeviceGuard guard(c->device);
+    std::vector<std::unique_lock<std::mutex>> held;
+    for (auto &sp : c->slots) held.emplace_back(sp->mu);
+    std::lock_guard<std::mutex> ls(c->side_mu);
+    for (auto &sp : c->slots) {
+      if (sp->stream) (void)hipStreamSynchronize(sp->stream);
+      if (sp->stream2) (void)hipStreamSynchronize(sp->stream2);
+    }
+    for (hipStream_t st : c->side_all) (void)hipStreamSynchronize(st);
+    (void)hipDeviceSynchronize();
     {
       std::lock_guard<std::mutex> lt(c->table_mu);
       if (c->d_btable) (void)hipFree(c->d_btable);
       if (c->d_btable16) (void)hipFree(c->d_btable16);
+      if (c->d_fault) (void)hipFree(c->d_fault);
       c->d_btable = nullptr;
       c->d_btable16 = nullptr;
+      c->d_fault = nullptr;
     }
     for (auto &sp : c->slots) {
       Slot &s = *sp;
-      std::lock_guard<std::mutex> ls(s.mu);
       if (s.stream) (void)hipStreamDestroy(s.stream);
       if (s.stream2) (void)hipStreamDestroy(s.stream2);
       if (s.d_buf) (void)hipFree(s.d_buf);
@@ -493,14 +688,9 @@ void hsv_shutdown(void) {
       s.d_buf = s.h_buf = nullptr;
       s.d_cap = s.h_cap = 0;
     }
-    {
-      std::lock_guard<std::mutex> ls(c->side_mu);
-      if (c->side) {
-        (void)hipStreamSynchronize(c->side);
-        (void)hipStreamDestroy(c->side);
-        c->side = nullptr;
-      }
-    }
+    for (hipStream_t st : c->side_all) (void)hipStreamDestroy(st);
+    c->side_all.clear();
+    c->side_free.clear();
   }
   hsv_ws_trim();
 }
@@ -575,26 +765,28 @@ int hsv_verify_device_bits(const uint8_t *d_pk, size_t pk_stride, const uint8_t 
   if (guard.status() != hipSuccess) return hip_fail("hipSetDevice", guard.status());
   const int v = variant();
   const uint32_t *comb_b = nullptr;
-  rc = comb_table_for(ctx(dev), v, &comb_b);
+  DevCtx &c = ctx(dev);
+  rc = comb_table_for(c, v, &comb_b);
+  if (rc != HSV_OK) return rc;
+  uint32_t *fault = nullptr;
+  rc = device_fault_words(c, &fault);
   if (rc != HSV_OK) return rc;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // Batches of several kChunk launches alternate them over the caller's stream
-  // and a second library stream (fork/join through events on the caller's
-  // stream): a chunk's launch starts on the SIMDs the previous chunk's point
-  // pass leaves idle at its grid end.  Chunks write disjoint outputs (kChunk
-  // is a multiple of 32, so no strict-bits word is shared).
+  // and a second library stream leased for this call (fork/join through
+  // events on the caller's stream): a chunk's launch starts on the SIMDs the
+  // previous chunk's point pass leaves idle at its grid end.  Chunks write
+  // disjoint outputs (kChunk is a multiple of 32, so no strict-bits word is
+  // shared).
   hipStream_t s2 = s;
   hipEvent_t fork = nullptr, join = nullptr;
+  std::unique_ptr<SideStreamLease> side;
   if (n > kChunk) {
-    DevCtx &c = ctx(dev);
-    {
-      std::lock_guard<std::mutex> lk(c.side_mu);
-      if (!c.side && hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking) != hipSuccess) c.side = nullptr;
-    }
-    if (c.side && hipEventCreateWithFlags(&fork, hipEventDisableTiming) == hipSuccess &&
+    side.reset(new SideStreamLease(c));
+    if (side->stream() && hipEventCreateWithFlags(&fork, hipEventDisableTiming) == hipSuccess &&
         hipEventCreateWithFlags(&join, hipEventDisableTiming) == hipSuccess &&
-        hipEventRecord(fork, s) == hipSuccess && hipStreamWaitEvent(c.side, fork, 0) == hipSuccess)
-      s2 = c.side;
+        hipEventRecord(fork, s) == hipSuccess && hipStreamWaitEvent(side->stream(), fork, 0) == hipSuccess)
+      s2 = side->stream();
   }
   hipError_t e = hipSuccess;
   size_t k = 0;
@@ -602,7 +794,7 @@ int hsv_verify_device_bits(const uint8_t *d_pk, size_t pk_stride, const uint8_t 
     const size_t m = std::min(kChunk, n - base);
     e = hsv_launch_verify(v, d_pk + base * pk_stride, pk_stride, d_sig + base * sig_stride, sig_stride,
                           d_msg + base * msg_stride, msg_stride, (uint32_t)m, d_flags ? d_flags + base : nullptr,
-                          d_strict_bits ? d_strict_bits + base / 32 : nullptr, comb_b, (k & 1) ? s2 : s);
+                          d_strict_bits ? d_strict_bits + base / 32 : nullptr, comb_b, fault, (k & 1) ? s2 : s);
   }
   if (s2 != s) {  // join: the caller's stream waits for the side stream's chunks
     hipError_t ej = hipEventRecord(join, s2);
@@ -619,6 +811,42 @@ int hsv_verify_device(const uint8_t *d_pk, size_t pk_stride, const uint8_t *d_si
   if (!d_flags && n) return fail(HSV_ERR_INVALID_ARG, "null d_flags");
   return hsv_verify_device_bits(d_pk, pk_stride, d_sig, sig_stride, d_msg, msg_stride, n, d_flags, nullptr, stream);
 }
+
+int hsv_device_faults(int device, int clear) {
+  int rc = ensure_init();
+  if (rc != HSV_OK) return rc;
+  const int nd = device_count_inited();
+  if (device < -1 || device >= nd) return fail(HSV_ERR_INVALID_ARG, "device index out of range");
+  int bits = 0;
+  for (int d = device < 0 ? 0 : device; d < (device < 0 ? nd : device + 1); ++d) {
+    DevCtx &c = ctx(d);
+    uint32_t *words = nullptr;
+    {
+      std::lock_guard<std::mutex> lk(c.table_mu);
+      words = c.d_fault;
+    }
+    if (!words) continue;  // no device-resident call has run there
+    DeviceGuard guard(d);
+    if (guard.status() != hipSuccess) return hip_fail("hipSetDevice", guard.status());
+    uint32_t w[2] = {0, 0};
+    hipError_t e = hipMemcpy(w, words, sizeof(w), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && clear) e = hipMemset(words, 0, sizeof(w));
+    if (e != hipSuccess) return hip_fail("reading the device self-check words", e);
+    bits |= (w[0] ? 1 : 0) | (w[1] ? 2 : 0);
+  }
+  return bits;
+}
+
+// Measurement hook (not in hsv.h): the calling thread's last host-buffer
+// verification -- host milliseconds spent packing into pinned staging, bytes
+// copied host-to-device, and the call's wall milliseconds.
+void hsv_host_call_stats(double *pack_ms, double *h2d_bytes, double *call_ms) {
+  if (pack_ms) *pack_ms = t_pack_ms;
+  if (h2d_bytes) *h2d_bytes = (double)t_h2d_bytes;
+  if (call_ms) *call_ms = t_call_ms;
+}
+
+int hsv_pack_threads(void) { return PackPool::get().threads(); }
 
 double hsv_measure_mad_peak(void) {
   if (ensure_init() != HSV_OK) return -1.0;

@@ -170,12 +170,27 @@ struct CombPosTab {
   }
 };
 
+// Fault injection (tests only): what a corrupted key-table entry reads back as.
+HSV_INL ge_niels niels_injected(const ge_niels &n, uint32_t inject) {
+  ge_niels r = n;
+  if (inject == kInjectZeroTables) {
+    r.ypx = fe_small(0);
+    r.ymx = fe_small(0);
+    r.xy2d = fe_small(0);
+  } else if (inject == kInjectFlipTables) {
+    r.ypx.v[0] ^= 1u;
+  }
+  return r;
+}
+
 // Verification against a cached committee key.  ta: the key's table of -A,
 // tb: the table of B, pk: the key's original 32 bytes (hashed as-is),
 // key_flags: kKeyAOk / kKeySmallA computed when the table was built.
-// Returns the same flag byte as verify_one for (pk, sig, msg).
+// Returns the same flag byte as verify_one for (pk, sig, msg), plus kFault
+// (fault_bit).  inject: fault injection (tests), applied to the first key entry.
 HSV_INL uint32_t verify_one_comb(const uint32_t pk[8], uint32_t key_flags, const uint32_t sig[16],
-                                 const uint32_t msg[8], const uint32_t *ta, const uint32_t *tb) {
+                                 const uint32_t msg[8], const uint32_t *ta, const uint32_t *tb,
+                                 uint32_t inject = kInjectNone) {
   const uint32_t s_ok = sc_is_canonical(sig + 8);
   uint32_t h[16];
   sha512_96(sig, pk, msg, h);
@@ -199,7 +214,9 @@ HSV_INL uint32_t verify_one_comb(const uint32_t pk[8], uint32_t key_flags, const
     sr[8] >>= 8;
     const CombPosTab tpa{ta + (uint64_t)j * kCombEnt * kCombEntryWords};
     const CombPosTab tpb{tb + (uint64_t)j * kCombEnt * kCombEntryWords};
-    q = ge_add_niels<true>(q, select_niels<8>(tpa, ca));
+    ge_niels na = select_niels<8>(tpa, ca);
+    if (inject != kInjectNone && j == 0) na = niels_injected(na, inject);
+    q = ge_add_niels<true>(q, na);
     q = ge_add_niels<true>(q, select_niels<8>(tpb, cb));
   }
 
@@ -215,7 +232,7 @@ HSV_INL uint32_t verify_one_comb(const uint32_t pk[8], uint32_t key_flags, const
   const uint32_t strict_ok = eq_ok & (small_a ^ 1u) & (small_r ^ 1u);
   return (strict_ok ? kStrictOk : 0u) | (eq_ok ? kEqOk : 0u) | (parse_ok ? kParseOk : 0u) |
          (small_a ? kSmallA : 0u) | (small_r ? kSmallR : 0u) | (s_ok ? kSOk : 0u) |
-         (a_ok ? kAOk : 0u) | (r_ok ? kROk : 0u);
+         (a_ok ? kAOk : 0u) | (r_ok ? kROk : 0u) | fault_bit(a_ok, r_ok, q);
 }
 
 }  // namespace hsv

@@ -45,7 +45,8 @@ hsv_comb_verify_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__re
                        uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride,
                        uint32_t m, const uint8_t *__restrict__ pks, const uint8_t *__restrict__ key_flags,
                        uint32_t nkeys, const uint32_t *const *__restrict__ key_tables,
-                       const uint32_t *__restrict__ btable, uint8_t *__restrict__ flags_out) {
+                       const uint32_t *__restrict__ btable, uint8_t *__restrict__ flags_out, uint32_t inject,
+                       uint32_t *__restrict__ fault) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
   const uint32_t kidx = key_idx[i];
@@ -68,7 +69,8 @@ hsv_comb_verify_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__re
     msgw[0] = m0.x; msgw[1] = m0.y; msgw[2] = m0.z; msgw[3] = m0.w;
     msgw[4] = m1.x; msgw[5] = m1.y; msgw[6] = m1.z; msgw[7] = m1.w;
   }
-  const uint32_t f = verify_one_comb(pkw, key_flags[kk], sigw, msgw, key_tables[kk], btable);
+  const uint32_t f = verify_one_comb(pkw, key_flags[kk], sigw, msgw, key_tables[kk], btable, inject);
+  if (f & kFault) fault[0] = 1u;  // device self-check (hsv_kernels.hip report_faults)
   flags_out[i] = kvalid ? (uint8_t)f : (uint8_t)0;
 }
 
@@ -116,7 +118,8 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
                                   uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride,
                                   uint32_t m, const uint8_t *__restrict__ pks, const uint8_t *__restrict__ key_flags,
                                   uint32_t nkeys, const uint32_t *const *__restrict__ key_tables,
-                                  const uint32_t *__restrict__ btable, uint8_t *__restrict__ flags_out) {
+                                  const uint32_t *__restrict__ btable, uint8_t *__restrict__ flags_out,
+                                  uint32_t inject, uint32_t *__restrict__ fault) {
   __shared__ uint32_t r_x[kFusedVotes][kFeLimbs], r_y[kFusedVotes][kFeLimbs], r_fl[kFusedVotes];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint32_t base = blockIdx.x * kFusedVotes;
@@ -192,7 +195,9 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
     sd >>= 8;
     const CombPosTab tpa{ta + (uint64_t)j * kCombEnt * kCombEntryWords};
     const CombPosTab tpb{btable + (uint64_t)j * kCombEnt * kCombEntryWords};
-    q = ge_add_niels<true>(q, select_niels<8>(tpa, ca));
+    ge_niels na = select_niels<8>(tpa, ca);
+    if (inject != kInjectNone && jj == 0) na = niels_injected(na, inject);
+    q = ge_add_niels<true>(q, na);
     q = ge_add_niels<true>(q, select_niels<8>(tpb, cb));
   }
   HSV_UNROLL
@@ -217,6 +222,7 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
   const uint32_t f = (strict_ok ? kStrictOk : 0u) | (eq_ok ? kEqOk : 0u) | (parse_ok ? kParseOk : 0u) |
                      (small_a ? kSmallA : 0u) | (small_r ? kSmallR : 0u) | (s_ok ? kSOk : 0u) |
                      (a_ok ? kAOk : 0u) | (r_ok ? kROk : 0u);
+  if (fault_bit(a_ok, r_ok, q)) fault[0] = 1u;  // device self-check (hsv_kernels.hip report_faults)
   if (valid && g == 0u) flags_out[i0] = kvalid ? (uint8_t)f : (uint8_t)0;
 }
 
@@ -265,16 +271,19 @@ extern "C" hipError_t hsv_launch_comb_verify(const uint32_t *key_idx, const uint
                                              const uint8_t *msg, uint64_t msg_stride, uint32_t m,
                                              const uint8_t *pks, const uint8_t *key_flags, uint32_t nkeys,
                                              const uint32_t *const *key_tables, const uint32_t *btable,
-                                             uint8_t *flags_out, hipStream_t stream) {
+                                             uint8_t *flags_out, uint32_t *fault, hipStream_t stream) {
   if (m == 0) return hipSuccess;
+  if (!fault) return hipErrorInvalidValue;
+  const uint32_t inject = (uint32_t)hsv_test_inject_mode();
   if (m <= kCombQuadMax) {  // latency form: four lanes per vote, R decompressed by a second wave
     hipLaunchKernelGGL(hsv::hsv_comb_verify_quad_fused_kernel, dim3((m + hsv::kFusedVotes - 1) / hsv::kFusedVotes),
                        dim3(128), 0, stream, key_idx, sig, sig_stride, msg, msg_stride, m, pks, key_flags, nkeys,
-                       key_tables, btable, flags_out);
+                       key_tables, btable, flags_out, inject, fault);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(hsv::hsv_comb_verify_kernel, dim3((m + 255u) / 256u), dim3(256), 0, stream, key_idx, sig,
-                     sig_stride, msg, msg_stride, m, pks, key_flags, nkeys, key_tables, btable, flags_out);
+                     sig_stride, msg, msg_stride, m, pks, key_flags, nkeys, key_tables, btable, flags_out, inject,
+                     fault);
   return hipGetLastError();
 }
 

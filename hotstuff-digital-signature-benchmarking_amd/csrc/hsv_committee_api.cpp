@@ -95,32 +95,38 @@ int committee_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t
     const size_t msg_off = sig_off + round_up(k * 64, kAlign);
     const size_t msg_bytes = msg_stride ? k * 32 : 32;
     const size_t flag_off = msg_off + round_up(msg_bytes, kAlign);
-    const size_t total = flag_off + round_up(k, kAlign);
+    const size_t fault_off = flag_off + round_up(k, kAlign);
+    const size_t total = fault_off + kAlign;
     rc = slot_prepare(s, total, total);
     if (rc != HSV_OK) return rc;
     uint8_t *h = s.h_buf;
     std::memcpy(h + idx_off, key_idx + base, k * 4);
     std::memcpy(h + sig_off, sig + base * 64, k * 64);
     std::memcpy(h + msg_off, msg + base * msg_stride, msg_bytes);
+    // unwritten flags read as rejections; self-check words start at zero
+    std::memset(h + flag_off, 0, k);
+    std::memset(h + fault_off, 0, kFaultBytes);
     void *hd = nullptr;
     uint8_t *dbuf = s.d_buf;
     const bool zero_copy = k <= kZeroCopyMax && hipHostGetDevicePointer(&hd, h, 0) == hipSuccess && hd;
     if (zero_copy) {
       dbuf = static_cast<uint8_t *>(hd);
     } else {
-      const hipError_t e = hipMemcpyAsync(s.d_buf, h, msg_off + msg_bytes, hipMemcpyHostToDevice, s.stream);
+      const hipError_t e = hipMemcpyAsync(s.d_buf, h, fault_off + kFaultBytes, hipMemcpyHostToDevice, s.stream);
       if (e != hipSuccess) return hip_fail("hipMemcpyAsync H2D", e);
     }
     hipError_t e = hsv_launch_comb_verify(reinterpret_cast<const uint32_t *>(dbuf + idx_off), dbuf + sig_off, 64,
                                           dbuf + msg_off, msg_stride ? 32 : 0, (uint32_t)k, cd.d_pks, cd.d_kflags, cd.n,
-                                          cd.d_tabptr, c.d_btable, dbuf + flag_off, s.stream);
+                                          cd.d_tabptr, c.d_btable, dbuf + flag_off,
+                                          reinterpret_cast<uint32_t *>(dbuf + fault_off), s.stream);
+    if (e == hipSuccess && !zero_copy)
+      e = hipMemcpyAsync(h + flag_off, s.d_buf + flag_off, fault_off + kFaultBytes - flag_off, hipMemcpyDeviceToHost,
+                         s.stream);
+    const hipError_t es = hipStreamSynchronize(s.stream);  // nothing of this call stays in flight
     if (e != hipSuccess) return hip_fail("committee verify launch", e);
-    if (!zero_copy) {
-      e = hipMemcpyAsync(h + flag_off, s.d_buf + flag_off, k, hipMemcpyDeviceToHost, s.stream);
-      if (e != hipSuccess) return hip_fail("hipMemcpyAsync D2H", e);
-    }
-    e = hipStreamSynchronize(s.stream);
-    if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
+    if (es != hipSuccess) return hip_fail("hipStreamSynchronize", es);
+    rc = check_faults(h + fault_off, "committee verify");
+    if (rc != HSV_OK) return rc;
     std::memcpy(flags_out + base, h + flag_off, k);
   }
   return HSV_OK;
@@ -244,8 +250,11 @@ int hsv_committee_verify_device(const hsv_committee *cm, const uint32_t *d_key_i
   if (guard.status() != hipSuccess) return hip_fail("hipSetDevice", guard.status());
   rc = ensure_btable(c);  // the B table is rebuilt if hsv_shutdown released it
   if (rc != HSV_OK) return rc;
+  uint32_t *fault = nullptr;
+  rc = device_fault_words(c, &fault);
+  if (rc != HSV_OK) return rc;
   const hipError_t e = hsv_launch_comb_verify(d_key_idx, d_sig, sig_stride, d_msg, msg_stride, (uint32_t)m, cm->dev.d_pks,
-                                              cm->dev.d_kflags, cm->dev.n, cm->dev.d_tabptr, c.d_btable, d_flags,
+                                              cm->dev.d_kflags, cm->dev.n, cm->dev.d_tabptr, c.d_btable, d_flags, fault,
                                               reinterpret_cast<hipStream_t>(stream));
   return e == hipSuccess ? HSV_OK : hip_fail("committee verify launch", e);
 }

@@ -51,13 +51,15 @@ struct Slot {
 struct DevCtx {
   int device = 0;
   int cus = 0;
-  std::mutex table_mu;             // guards the two B tables below
+  std::mutex table_mu;             // guards the two B tables and d_fault below
   uint32_t *d_btable = nullptr;    // narrow comb of B (committee kernels)
   uint32_t *d_btable16 = nullptr;  // wide comb of B (generic kernels)
+  uint32_t *d_fault = nullptr;     // self-check words of the device-resident calls (hsv_device_faults)
   std::vector<std::unique_ptr<Slot>> slots;
   std::atomic<unsigned> rr{0};
-  std::mutex side_mu;               // guards `side`
-  hipStream_t side = nullptr;       // second stream of multi-chunk device-API batches
+  std::mutex side_mu;                    // guards the side-stream pool
+  std::vector<hipStream_t> side_free;    // idle second streams of multi-chunk device-API batches
+  std::vector<hipStream_t> side_all;     // every side stream created (hsv_shutdown)
 };
 
 // Makes `device` current for the calling thread and restores the previous
@@ -102,6 +104,28 @@ class SlotLease {
 // Stream and buffers of a slot (current device must be c.device).
 int slot_prepare(Slot &s, size_t dev_bytes, size_t host_bytes);
 int slot_stream2(Slot &s);
+
+// Device self-check words (hsv_kernels.hip report_faults): two words per
+// launch, zeroed before it; non-zero after it -> HSV_ERR_DEVICE_FAULT.
+constexpr size_t kFaultBytes = 8;
+int check_faults(const uint8_t *words, const char *where);
+// The per-device words of the stream-ordered device API (current device
+// must be c.device); allocated and zeroed on first use.
+int device_fault_words(DevCtx &c, uint32_t **out);
+
+// A side stream of device c for one call (current device must be c.device),
+// returned to the pool when the lease ends: concurrent device-API calls never
+// share one, so a call's join event only waits for its own chunks.
+class SideStreamLease {
+ public:
+  explicit SideStreamLease(DevCtx &c);
+  ~SideStreamLease();
+  hipStream_t stream() const { return s_; }
+
+ private:
+  DevCtx &c_;
+  hipStream_t s_ = nullptr;
+};
 
 // B tables of device c (current device must be c.device).
 int ensure_btable(DevCtx &c);

@@ -15,7 +15,8 @@ extern "C" {
 // process's first committee-cache allocations, accepted a forged vote in 8 of
 // 16 runs of tests/native/crypto_tests.cpp; with this pool, 0 of 16
 // (tools/forgery_debug.sh).  HSV_WS_POOL=default
-// selects the default pool again (diagnosis only).
+// selects the default pool again in the measurement build (ALL_VARIANTS=1)
+// only; the product library always uses its own pool.
 hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream);
 void hsv_ws_trim(void);  // hsv_shutdown: release the pools' free blocks
 
@@ -23,10 +24,16 @@ void hsv_ws_trim(void);  // hsv_shutdown: release the pools' free blocks
 int hsv_num_variants(void);            // id space
 int hsv_variant_list(int *out, int cap);  // ids built into this library; returns their count
 int hsv_variant_available(int variant);
+// fault: two device-visible words the caller zeroed before the launch; the
+// kernels set fault[0] (an item's final point failed the self-check) and
+// fault[1] (a workspace canary changed) -- see hsv_kernels.hip report_faults.
+// Required (non-null) for the product variants.
 hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig,
                              uint64_t sig_stride, const uint8_t *msg, uint64_t msg_stride,
                              uint32_t n, uint8_t *flags_out, uint32_t *strict_bits,
-                             const uint32_t *comb_b, hipStream_t stream);
+                             const uint32_t *comb_b, uint32_t *fault, hipStream_t stream);
+// fault injection mode of the next launches (tests only; hsv_kernels.hip)
+int hsv_test_inject_mode(void);
 // digit width of the B comb table a variant reads: 8 (hsv_comb_table_bytes),
 // 16 (the wide table, hsv_comb16_table_bytes) or 0 (none); comb_b must be
 // that table for such variants
@@ -49,7 +56,7 @@ hipError_t hsv_launch_comb_build(const uint8_t *encs, uint32_t nkeys, uint32_t n
 hipError_t hsv_launch_comb_verify(const uint32_t *key_idx, const uint8_t *sig, uint64_t sig_stride,
                                   const uint8_t *msg, uint64_t msg_stride, uint32_t m, const uint8_t *pks,
                                   const uint8_t *key_flags, uint32_t nkeys, const uint32_t *const *key_tables,
-                                  const uint32_t *btable, uint8_t *flags_out, hipStream_t stream);
+                                  const uint32_t *btable, uint8_t *flags_out, uint32_t *fault, hipStream_t stream);
 uint64_t hsv_comb_table_bytes(void);
 uint64_t hsv_comb_tmp_bytes(uint32_t nkeys);
 // wide (16-bit digit) comb table of B, hsv_comb.hpp

@@ -133,13 +133,26 @@ hsv_verify_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
 __device__ const uint4 kVtIdentity[8] = {{1u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {1u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u},
                                          {2u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
 
+// Fault injection (hsv_test_inject_fault, tests only; uniform kernel argument,
+// kInject* in hsv_verify_core.hpp): the table stores of every lane are
+// replaced, between the table build and the window loop, by what a corrupted
+// workspace would hold.
 template <int ENT>
 struct GlobalVarTab {
   static constexpr int kStored = ENT - 1;  // entries 1 .. ENT-1 per table
   uint4 *base;
+  uint32_t inject = kInjectNone;
   __device__ __forceinline__ void put(int t, int m, const uint32_t w[32]) const {
     if (m == 0) return;
     uint4 *e = base + (t * kStored + m - 1) * 8;
+    if (__builtin_expect(inject == kInjectZeroTables || (inject == kInjectFlipTables && t == 0), 0)) {
+      HSV_UNROLL
+      for (int q = 0; q < 8; ++q)
+        e[q] = inject == kInjectZeroTables ? make_uint4(0u, 0u, 0u, 0u)
+                                           : make_uint4(w[4 * q] ^ (q == 0 ? 1u : 0u), w[4 * q + 1], w[4 * q + 2],
+                                                        w[4 * q + 3]);
+      return;
+    }
     HSV_UNROLL
     for (int q = 0; q < 8; ++q) {
 #ifdef HSV_TIMING_STUB_TABLE_STORES  // timing probe only: entries computed, never stored
@@ -370,6 +383,20 @@ hsv_prep_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const uint8_
   if (prep_scalars<WA>(pkw, sigw, msgw, rec + idx, n, lat_bits)) fb_list[atomicAdd(&ctr->fb_count, 1u)] = idx;
 }
 
+// Device self-checks of the product kernels (a device failure must
+// never become a silent reject).  Each launch gets
+//   fault[2]  two words the host zeroed: fault[0] <- 1 when an item's final
+//             point fails ge_is_sane (kFault), fault[1] <- 1 when a lane's
+//             canary changed; written with plain stores once the work loop
+//             is done (no atomics, so the words may live in pinned host memory);
+//   canary    one word per lane slot of the workspace, set to the launch's
+//             nonce when the lane starts and compared after every batch.
+// The host turns a non-zero word into HSV_ERR_DEVICE_FAULT.
+__device__ __forceinline__ void report_faults(uint32_t *fault, uint32_t bad) {
+  if (bad & 1u) fault[0] = 1u;
+  if (bad & 2u) fault[1] = 1u;
+}
+
 // Pass 2: persistent grid, 64-item batches from ctr->next over a virtual
 // range [fallback items | all items].  Fallback batches come first and run
 // the full-length path; in the regular range a fallback item's lane computes
@@ -382,10 +409,14 @@ hsv_verify_hp_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const u
                      uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
                      uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b,
                      const uint32_t *__restrict__ rec, HcCounters *__restrict__ ctr,
-                     const uint32_t *__restrict__ fb_list) {
+                     const uint32_t *__restrict__ fb_list, uint32_t *__restrict__ canary, uint32_t nonce,
+                     uint32_t inject, uint32_t *__restrict__ fault) {
   constexpr int kEnt = (1 << (WA - 1)) + 1;
-  GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)(blockIdx.x * kBlock + threadIdx.x) * vt_lane_uint4<WA>()};
+  const uint32_t slot = blockIdx.x * kBlock + threadIdx.x;
+  GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)slot * vt_lane_uint4<WA>(), inject};
   const uint32_t lane = threadIdx.x & 63u;
+  canary[slot] = nonce;
+  uint32_t bad = 0;
   const uint32_t nfb = __builtin_amdgcn_readfirstlane(ctr->fb_count);
   const uint32_t fb_end = (nfb + 63u) & ~63u;
   const uint32_t words = (n + 31u) / 32u;
@@ -404,6 +435,7 @@ hsv_verify_hp_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const u
     if (lane == 0) base = atomicAdd(&ctr->next, 64u);
     base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
     if (base >= fb_end + n) break;
+    if (inject == kInjectCanary) canary[slot] = ~nonce;
     if (base < fb_end) {
       const uint32_t j = base + lane;
       const bool valid = j < nfb;
@@ -411,6 +443,7 @@ hsv_verify_hp_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const u
       uint32_t pkw[8], sigw[16], msgw[8];
       load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, idx, pkw, sigw, msgw);
       const uint32_t f = verify_one_full_comb<WA, false, CB>(pkw, sigw, msgw, comb_b, vt);
+      bad |= ((f & kFault) ? 1u : 0u) | (canary[slot] != nonce ? 2u : 0u);
       if (valid) {
         if (flags_out) flags_out[idx] = (uint8_t)f;
         if (strict_bits && (f & kStrictOk)) atomicOr(&strict_bits[idx >> 5], 1u << (idx & 31u));
@@ -454,6 +487,7 @@ hsv_verify_hp_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const u
 #else
     const uint32_t f = verify_one_prepped<WA, CB>(pkw, rw, rec + li, n, meta, comb_b, vt);
 #endif
+    bad |= ((f & kFault) ? 1u : 0u) | (canary[slot] != nonce ? 2u : 0u);
     if (own && flags_out) flags_out[idx] = (uint8_t)f;
     if (strict_bits) {
       const uint64_t mask = __ballot(own && (f & kStrictOk));
@@ -462,6 +496,7 @@ hsv_verify_hp_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const u
       if (lane < 2u && w < words && part) atomicOr(&strict_bits[w], part);
     }
   }
+  report_faults(fault, bad);
 }
 
 // ---- latency form for small batches: two lanes per item ------------------
@@ -542,7 +577,7 @@ __device__ __forceinline__ uint32_t pair_scalar_phase(uint32_t p, uint32_t ok, u
   const uint32_t r_ok = p ? ok_o : ok, small_r = p ? small_o : small;
   const uint32_t a_ok = p ? ok : ok_o, small_a = p ? small : small_o;
   const uint32_t same = ge_is_neutral(q);
-  return flags_byte(meta & kPrepSOk, a_ok, r_ok, small_a, small_r, same);
+  return flags_byte(meta & kPrepSOk, a_ok, r_ok, small_a, small_r, same) | fault_bit(a_ok, r_ok, q);
 }
 
 template <int WA, int CB, class VT>
@@ -607,14 +642,18 @@ __global__ void __launch_bounds__(3 * 64)
 hsv_verify_pair_fused_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const uint8_t *__restrict__ sig,
                              uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
                              uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
-                             uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b, int lat_bits) {
+                             uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b, int lat_bits,
+                             uint32_t *__restrict__ canary, uint32_t nonce, uint32_t inject,
+                             uint32_t *__restrict__ fault) {
   constexpr int kEnt = (1 << (WA - 1)) + 1;
   __shared__ uint32_t srec[kPrepWords * kFusedItems];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint32_t base = blockIdx.x * kFusedItems;
   const uint32_t t = threadIdx.x;  // pair lanes: t < 128
   const uint32_t p = t & 1u, item = base + (t >> 1);
-  GlobalVarTab<kEnt> vt{vt_ws + ((uint64_t)blockIdx.x * 2u * kFusedItems + (t & 127u)) * vt_lane_uint4<WA>()};
+  const uint32_t slot = blockIdx.x * 2u * kFusedItems + (t & 127u);
+  GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)slot * vt_lane_uint4<WA>(), inject};
+  if (wave < 2) canary[slot] = inject == kInjectCanary ? ~nonce : nonce;
   uint32_t ok = 0, small = 0;
   if (wave == 2) {
     const uint32_t li = base + lane < n ? base + lane : n - 1u;
@@ -646,6 +685,7 @@ hsv_verify_pair_fused_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
   } else {
     f = pair_scalar_phase<WA, CB>(p, ok, small, srec + il, kFusedItems, meta, comb_b, vt);
   }
+  report_faults(fault, ((f & kFault) ? 1u : 0u) | (canary[slot] != nonce ? 2u : 0u));
   if (item < n && p == 0u) {
     if (flags_out) flags_out[item] = (uint8_t)f;
     if (strict_bits && (f & kStrictOk)) atomicOr(&strict_bits[item >> 5], 1u << (item & 31u));
@@ -804,11 +844,13 @@ extern "C" void hsv_ws_trim(void) {
 }
 
 extern "C" hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream) {
+#if HSV_ALL_VARIANTS  // diagnosis of DESIGN.md 6.2 only: the default pool (HSV_WS_POOL=default)
   static const bool own = [] {
     const char *v = std::getenv("HSV_WS_POOL");
     return !(v && std::strcmp(v, "default") == 0);
   }();
   if (!own) return hipMallocAsync(p, bytes, stream);
+#endif
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
@@ -841,6 +883,15 @@ namespace {
 // Lattice bound of the comb-path prepass (hsv_set_lattice_bits; tests lower it
 // to 133 so the lattice-fallback fixtures take the full-length path).
 std::atomic<int> g_lat_bits{hsv::kLatCombBits};
+
+// Fault injection mode of the next launches (hsv_test_inject_fault; tests only).
+std::atomic<uint32_t> g_inject{hsv::kInjectNone};
+
+// Per-launch canary nonce: odd, so never 0 (zeroed memory) or all-ones.
+uint32_t next_nonce() {
+  static std::atomic<uint32_t> ctr{0x9e3779b9u};
+  return (ctr.fetch_add(0x61c88646u) * 2654435761u) | 1u;
+}
 
 #if HSV_ALL_VARIANTS
 // Persistent-grid launch of hsv_verify_mt_kernel with a stream-ordered
@@ -917,7 +968,7 @@ hipError_t launch_mt(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
 template <int WA, int WAVES, int CB, bool TAIL = false>
 hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
                      const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
-                     uint32_t *strict_bits, const uint32_t *comb_b, hipStream_t stream) {
+                     uint32_t *strict_bits, const uint32_t *comb_b, uint32_t *fault, hipStream_t stream) {
   const void *kern = reinterpret_cast<const void *>(hsv::hsv_verify_hp_kernel<WA, WAVES, CB>);
 #if HSV_ALL_VARIANTS
   if constexpr (TAIL) kern = reinterpret_cast<const void *>(hsv::hsv_verify_hpt_kernel<WA, WAVES, CB>);
@@ -946,16 +997,18 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
   const uint32_t blocks_needed = (n + hsv::kBlock - 1) / hsv::kBlock;
   const uint32_t grid = std::min<uint32_t>(blocks_needed, (uint32_t)resident);
   const size_t ws_bytes = (size_t)grid * hsv::kBlock * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
+  const size_t canary_bytes = ((size_t)grid * hsv::kBlock * sizeof(uint32_t) + 255) & ~(size_t)255;
   const size_t fb_bytes = (size_t)n * sizeof(uint32_t);
   const size_t rec_bytes = (size_t)n * hsv::kPrepWords * sizeof(uint32_t);
   void *ws = nullptr;
-  e = hsv_ws_malloc(&ws, ws_bytes + 256 + fb_bytes + rec_bytes, stream);
+  e = hsv_ws_malloc(&ws, ws_bytes + 256 + canary_bytes + fb_bytes + rec_bytes, stream);
   if (e != hipSuccess) return e;
   uint8_t *ws8 = static_cast<uint8_t *>(ws);
   uint4 *vt_ws = reinterpret_cast<uint4 *>(ws);
   hsv::HcCounters *ctr = reinterpret_cast<hsv::HcCounters *>(ws8 + ws_bytes);
-  uint32_t *fb_list = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256);
-  uint32_t *rec = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256 + fb_bytes);
+  uint32_t *canary = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256);
+  uint32_t *fb_list = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256 + canary_bytes);
+  uint32_t *rec = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256 + canary_bytes + fb_bytes);
   e = hipMemsetAsync(ctr, 0, sizeof(hsv::HcCounters), stream);
   if (e == hipSuccess && strict_bits) e = hipMemsetAsync(strict_bits, 0, (size_t)((n + 31u) / 32u) * 4u, stream);
   if (e == hipSuccess) {
@@ -977,7 +1030,7 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
     {
       hipLaunchKernelGGL((hsv::hsv_verify_hp_kernel<WA, WAVES, CB>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
                          pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, vt_ws, comb_b, rec,
-                         ctr, fb_list);
+                         ctr, fb_list, canary, next_nonce(), g_inject.load(), fault);
     }
     e = hipGetLastError();
   }
@@ -995,17 +1048,20 @@ constexpr uint32_t kPairMax = 1u << 13;
 template <int WA, int CB>
 hipError_t launch_pair(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
                        const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
-                       uint32_t *strict_bits, const uint32_t *comb_b, hipStream_t stream) {
+                       uint32_t *strict_bits, const uint32_t *comb_b, uint32_t *fault, hipStream_t stream) {
   const uint32_t grid = (n + hsv::kFusedItems - 1) / hsv::kFusedItems;
-  const size_t ws_bytes = (size_t)grid * 2u * hsv::kFusedItems * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
+  const size_t slots = (size_t)grid * 2u * hsv::kFusedItems;
+  const size_t ws_bytes = slots * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
   void *ws = nullptr;
-  hipError_t e = hsv_ws_malloc(&ws, ws_bytes, stream);
+  hipError_t e = hsv_ws_malloc(&ws, ws_bytes + slots * sizeof(uint32_t), stream);
   if (e != hipSuccess) return e;
   if (strict_bits) e = hipMemsetAsync(strict_bits, 0, (size_t)((n + 31u) / 32u) * 4u, stream);
   if (e == hipSuccess) {
     hipLaunchKernelGGL((hsv::hsv_verify_pair_fused_kernel<WA, CB>), dim3(grid), dim3(3 * 64), 0, stream, pk,
                        pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits,
-                       static_cast<uint4 *>(ws), comb_b, g_lat_bits.load());
+                       static_cast<uint4 *>(ws), comb_b, g_lat_bits.load(),
+                       reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(ws) + ws_bytes), next_nonce(),
+                       g_inject.load(), fault);
     e = hipGetLastError();
   }
   const hipError_t ef = hipFreeAsync(ws, stream);
@@ -1018,16 +1074,20 @@ extern "C" hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t
                                         const uint8_t *sig, uint64_t sig_stride,
                                         const uint8_t *msg, uint64_t msg_stride, uint32_t n,
                                         uint8_t *flags_out, uint32_t *strict_bits,
-                                        const uint32_t *comb_b, hipStream_t stream) {
+                                        const uint32_t *comb_b, uint32_t *fault, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   if (hsv_variant_needs_comb(variant) && !comb_b) return hipErrorInvalidValue;
+  if (!fault && variant >= 19) return hipErrorInvalidValue;
   switch (variant) {
     case 19:
-      return launch_hp<4, 3, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
+      return launch_hp<4, 3, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b,
+                                 fault, stream);
     case 21:
       if (n <= kPairMax)
-        return launch_pair<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
-      return launch_hp<4, HSV_HP_WAVES, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream);
+        return launch_pair<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b,
+                                  fault, stream);
+      return launch_hp<4, HSV_HP_WAVES, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits,
+                                            comb_b, fault, stream);
 #if HSV_ALL_VARIANTS
     default: break;
 #else
@@ -1041,6 +1101,7 @@ extern "C" hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t
                      stream, pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out,   \
                      strict_bits)
 #define HSV_ARGS pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream
+#define HSV_ARGS_F pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, fault, stream
   switch (variant) {
     case 0: HSV_LAUNCH(2, 8, 2, false); break;
     case 1: HSV_LAUNCH(3, 9, 1, false); break;
@@ -1061,13 +1122,14 @@ extern "C" hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t
     case 16: return launch_mt<4, 4, 2, true, false, 16>(HSV_ARGS);
     case 17: return launch_mt<4, 4, 3, true, false, 16, true>(HSV_ARGS);
     case 18: return launch_mt<4, 4, 2, true, false, 16, true>(HSV_ARGS);
-    case 20: return launch_hp<4, 2, 16>(HSV_ARGS);
+    case 20: return launch_hp<4, 2, 16>(HSV_ARGS_F);
     case 22:
-      if (n <= kPairMax) return launch_pair<4, 16>(HSV_ARGS);
-      return launch_hp<4, 3, 16, true>(HSV_ARGS);
+      if (n <= kPairMax) return launch_pair<4, 16>(HSV_ARGS_F);
+      return launch_hp<4, 3, 16, true>(HSV_ARGS_F);
     default: return hipErrorInvalidValue;
   }
 #undef HSV_ARGS
+#undef HSV_ARGS_F
 #undef HSV_LAUNCH
   return hipGetLastError();
 #endif
@@ -1127,6 +1189,15 @@ extern "C" int hsv_set_lattice_bits(int bits) {
   if (bits < 128 || bits > hsv::kLatCombBits) return -1;
   return g_lat_bits.exchange(bits);
 }
+
+// Test hook (not in hsv.h): fault injection mode of the following launches
+// (kInject*: 1 zeroed tables, 2 overwritten canary, 3 flipped table bits;
+// 0 = off).  Returns the previous mode, or -1 for an unknown one.
+extern "C" int hsv_test_inject_fault(int mode) {
+  if (mode < 0 || mode > (int)hsv::kInjectFlipTables) return -1;
+  return (int)g_inject.exchange((uint32_t)mode);
+}
+extern "C" int hsv_test_inject_mode(void) { return (int)g_inject.load(); }
 
 extern "C" int hsv_variant_needs_comb(int variant) {
   if (variant >= 10 && variant <= 14) return 8;

@@ -252,6 +252,23 @@ HSV_INL uint32_t ge_eq_affine(const ge_ext &p, const fe &x, const fe &y) {
 // Q == O: X == 0 and Y == Z != 0 (same fail-closed rule as ge_eq_affine).
 HSV_INL uint32_t ge_is_neutral(const ge_ext &q) { return fe_is_zero(q.X) & fe_eq(q.Y, q.Z) & HSV_Z_NONZERO(q.Z); }
 
+// Device self-check of a final accumulator: 1 iff (X : Y : Z) is a point of
+// the curve, (Y^2 - X^2) Z^2 == Z^4 + d X^2 Y^2 with Z != 0 (T not needed).
+// Every formula above is exact and complete, so sums and multiples of curve
+// points are curve points: a final Q that fails this was computed from
+// something other than what the kernel wrote or was given (table memory,
+// workspace, comb tables or registers corrupted).  All-zero entries give
+// (0 : 0 : 0 : 0), which satisfies the equation but not Z != 0; a garbage
+// entry gives an off-curve sum.  7 field operations per verification.
+HSV_INL uint32_t ge_is_sane(const ge_ext &p) {
+  fe xx, yy, zz, lhs, xy, z4, dxy;
+  fe_sq2(p.X, p.Y, xx, yy);
+  zz = fe_sq(p.Z);
+  fe_mul2(fe_sub(yy, xx), zz, xx, yy, lhs, xy);
+  fe_mul2(zz, zz, xy, fe_d(), z4, dxy);
+  return fe_eq(lhs, fe_add(z4, dxy)) & (fe_is_zero(p.Z) ^ 1u);
+}
+
 // Compress (x, y) = (X/Z, Y/Z) -> 32 bytes as 8 words (host-side signing).
 HSV_INL void ge_compress(const ge_ext &p, uint32_t out[8]) {
   const fe zi = fe_invert(p.Z);

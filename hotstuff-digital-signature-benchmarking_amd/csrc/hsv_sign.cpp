@@ -137,9 +137,80 @@ void sign_expanded(const Expanded &e, const uint8_t *msg, size_t len, uint8_t si
   words_to_bytes(s.v, sig + 32, 8);
 }
 
+// [t]T8 for a point T8 of order 8 (encoding c7176a70...ac037a, one of the
+// eight torsion points), t in 1..7
+ge_ext torsion_multiple(int t) {
+  const uint8_t enc[32] = {0xc7, 0x17, 0x6a, 0x70, 0x3d, 0x4d, 0xd8, 0x4f, 0xba, 0x3c, 0x0b,
+                           0x76, 0x0d, 0x10, 0x67, 0x0f, 0x2a, 0x20, 0x53, 0xfa, 0x2c, 0x39,
+                           0xcc, 0xc6, 0x4e, 0xc7, 0xfd, 0x77, 0x92, 0xac, 0x03, 0x7a};
+  uint32_t w[8];
+  bytes_to_words(enc, w, 8);
+  fe x, y;
+  (void)ge_decompress(w, x, y);
+  ge_ext p;
+  p.X = x;
+  p.Y = y;
+  p.Z = fe_small(1);
+  p.T = fe_mul(x, y);
+  const ge_cached c = ge_to_cached(p);
+  ge_ext q = p;
+  for (int i = 1; i < t; ++i) q = ge_add_cached<true>(q, c);
+  return q;
+}
+
 }  // namespace
 
 extern "C" {
+
+// Synthesis helper (not on the hot path): a
+// mixed-order key A' = [a]B + [t]T8 (a from `seed` as in hsv_public_key, T8 of
+// order 8, t odd: 2 * torsion + 1) and a signature over msg whose challenge
+// k = SHA-512(R || A' || msg) mod l satisfies k = 0 (mod 8) when accept != 0
+// -- then [s]B - [k]A' = R and verify_strict accepts (cofactorless) -- or
+// k != 0 (mod 8) when accept == 0, where only a cofactored verifier would
+// accept.  The nonce is RFC 8032's r = SHA-512(prefix || msg) for the first
+// try and SHA-512(prefix || msg || try) after it (deterministic).
+int hsv_sign_mixed_order(const uint8_t seed[32], const uint8_t *msg, size_t msg_len, int torsion, int accept,
+                         uint8_t pk_out[32], uint8_t sig_out[64]) {
+  if (!seed || (!msg && msg_len) || !pk_out || !sig_out || torsion < 0 || torsion > 3) return HSV_ERR_INVALID_ARG;
+  (void)fixed_base_table();
+  Expanded e;
+  expand(seed, e);
+  const ge_ext ap = ge_add_cached<true>(fixed_base_mul(e.a), ge_to_cached(torsion_multiple(2 * torsion + 1)));
+  uint32_t enc[8];
+  ge_compress(ap, enc);
+  uint8_t pk[32];
+  words_to_bytes(enc, pk, 8);
+  std::vector<uint8_t> buf(96 + msg_len + 4);
+  for (uint32_t attempt = 0; attempt < 4096; ++attempt) {
+    std::memcpy(buf.data(), e.prefix, 32);
+    if (msg_len) std::memcpy(buf.data() + 32, msg, msg_len);
+    size_t len = 32 + msg_len;
+    if (attempt) {
+      for (int b = 0; b < 4; ++b) buf[len + b] = (uint8_t)(attempt >> (8 * b));
+      len += 4;
+    }
+    uint8_t h[64];
+    sha512_bytes(buf.data(), len, h);
+    const sc r = reduce_bytes64(h);
+    uint32_t renc[8];
+    ge_compress(fixed_base_mul(r), renc);
+    uint8_t sig[64];
+    words_to_bytes(renc, sig, 8);
+    std::memcpy(buf.data(), sig, 32);
+    std::memcpy(buf.data() + 32, pk, 32);
+    if (msg_len) std::memcpy(buf.data() + 64, msg, msg_len);
+    sha512_bytes(buf.data(), 64 + msg_len, h);
+    const sc k = reduce_bytes64(h);
+    if (((k.v[0] & 7u) == 0) != (accept != 0)) continue;
+    const sc s = sc_muladd(k, e.a, r);
+    words_to_bytes(s.v, sig + 32, 8);
+    std::memcpy(pk_out, pk, 32);
+    std::memcpy(sig_out, sig, 64);
+    return HSV_OK;
+  }
+  return HSV_ERR_INVALID_ARG;  // unreachable in practice (2^-550 for accept)
+}
 
 int hsv_public_key(const uint8_t seed[32], uint8_t pk_out[32]) {
   if (!seed || !pk_out) return HSV_ERR_INVALID_ARG;

@@ -23,10 +23,11 @@ constexpr size_t kTxChunkBytes = size_t(1) << 29;  // transaction bytes staged p
 // records, verification and the short-transaction mask for m <= kChunk
 // transactions already in HBM (d_offsets relative to d_txs, or NULL = fixed size)
 int tx_enqueue(int v, const uint32_t *comb_b, const uint8_t *d_txs, const uint64_t *d_offsets, size_t tx_size,
-               size_t m, uint8_t *d_rec, uint8_t *d_flags, uint32_t *d_bits, hipStream_t s) {
+               size_t m, uint8_t *d_rec, uint8_t *d_flags, uint32_t *d_bits, uint32_t *d_fault, hipStream_t s) {
   hipError_t e = hsv_launch_tx_records(d_txs, d_offsets, tx_size, (uint32_t)m, d_rec, s);
   if (e != hipSuccess) return hip_fail("transaction record kernel launch", e);
-  e = hsv_launch_verify(v, d_rec, 128, d_rec + 32, 128, d_rec + 96, 128, (uint32_t)m, d_flags, d_bits, comb_b, s);
+  e = hsv_launch_verify(v, d_rec, 128, d_rec + 32, 128, d_rec + 96, 128, (uint32_t)m, d_flags, d_bits, comb_b,
+                        d_fault, s);
   if (e != hipSuccess) return hip_fail("verify kernel launch", e);
   e = hsv_launch_tx_mask(d_offsets, (uint32_t)m, d_flags, d_bits, s);
   if (e != hipSuccess) return hip_fail("transaction mask kernel launch", e);
@@ -57,13 +58,16 @@ int run_tx_on_device(DevCtx &c, const uint8_t *txs, const uint64_t *offsets, siz
     max_items = std::max(max_items, ch.second - ch.first);
     max_bytes = std::max(max_bytes, tx_bytes(offsets, tx_size, ch.first, ch.second));
   }
-  // device: tx bytes | offsets | records | flags;  host: tx bytes | offsets | flags
+  // device: tx bytes | offsets | records | flags | self-check words;
+  // host: tx bytes | offsets | flags | self-check words
   const size_t off_off = round_up(max_bytes, kAlign);
   const size_t rec_off = off_off + round_up((max_items + 1) * 8, kAlign);
   const size_t flag_off = rec_off + round_up(max_items * 128, kAlign);
-  const size_t d_total = flag_off + round_up(max_items, kAlign);
+  const size_t fault_off = flag_off + round_up(max_items, kAlign);
+  const size_t d_total = fault_off + kAlign;
   const size_t h_flag_off = rec_off;
-  const size_t h_total = h_flag_off + round_up(max_items, kAlign);
+  const size_t h_fault_off = h_flag_off + round_up(max_items, kAlign);
+  const size_t h_total = h_fault_off + kAlign;
   DeviceGuard guard(c.device);
   if (guard.status() != hipSuccess) return hip_fail("hipSetDevice", guard.status());
   const int v = variant();
@@ -87,14 +91,25 @@ int run_tx_on_device(DevCtx &c, const uint8_t *txs, const uint64_t *offsets, siz
       in_bytes = off_off + (m + 1) * 8;
     }
     hipError_t e = hipMemcpyAsync(s.d_buf, h, in_bytes, hipMemcpyHostToDevice, s.stream);
-    if (e != hipSuccess) return hip_fail("hipMemcpyAsync H2D", e);
+    // unwritten flags read as rejections; self-check words start at zero
+    if (e == hipSuccess) e = hipMemsetAsync(s.d_buf + flag_off, 0, fault_off + kFaultBytes - flag_off, s.stream);
+    if (e != hipSuccess) {
+      (void)hipStreamSynchronize(s.stream);
+      return hip_fail("hipMemcpyAsync H2D", e);
+    }
     rc = tx_enqueue(v, comb_b, s.d_buf, offsets ? reinterpret_cast<const uint64_t *>(s.d_buf + off_off) : nullptr,
-                    tx_size, m, s.d_buf + rec_off, s.d_buf + flag_off, nullptr, s.stream);
+                    tx_size, m, s.d_buf + rec_off, s.d_buf + flag_off, nullptr,
+                    reinterpret_cast<uint32_t *>(s.d_buf + fault_off), s.stream);
+    if (rc == HSV_OK) {
+      e = hipMemcpyAsync(h + h_flag_off, s.d_buf + flag_off, fault_off + kFaultBytes - flag_off,
+                         hipMemcpyDeviceToHost, s.stream);
+      if (e != hipSuccess) rc = hip_fail("hipMemcpyAsync D2H", e);
+    }
+    e = hipStreamSynchronize(s.stream);  // nothing of this call stays in flight
     if (rc != HSV_OK) return rc;
-    e = hipMemcpyAsync(h + h_flag_off, s.d_buf + flag_off, m, hipMemcpyDeviceToHost, s.stream);
-    if (e != hipSuccess) return hip_fail("hipMemcpyAsync D2H", e);
-    e = hipStreamSynchronize(s.stream);
     if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
+    rc = check_faults(h + h_fault_off, "transaction verify");
+    if (rc != HSV_OK) return rc;
     std::memcpy(flags_out + (a - lo), h + h_flag_off, m);
   }
   return HSV_OK;
@@ -164,6 +179,9 @@ int hsv_verify_transactions_device(const uint8_t *d_txs, const uint64_t *d_offse
   const uint32_t *comb_b = nullptr;
   rc = comb_table_for(ctx(dev), v, &comb_b);
   if (rc != HSV_OK) return rc;
+  uint32_t *fault = nullptr;
+  rc = device_fault_words(ctx(dev), &fault);
+  if (rc != HSV_OK) return rc;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const size_t per = std::min(n, kChunk);
   void *rec = nullptr;
@@ -173,7 +191,7 @@ int hsv_verify_transactions_device(const uint8_t *d_txs, const uint64_t *d_offse
     const size_t m = std::min(per, n - base);
     rc = tx_enqueue(v, comb_b, d_offsets ? d_txs : d_txs + base * tx_size, d_offsets ? d_offsets + base : nullptr,
                     tx_size, m, static_cast<uint8_t *>(rec), d_flags ? d_flags + base : nullptr,
-                    d_strict_bits ? d_strict_bits + base / 32 : nullptr, s);
+                    d_strict_bits ? d_strict_bits + base / 32 : nullptr, fault, s);
   }
   e = hipFreeAsync(rec, s);
   if (rc != HSV_OK) return rc;

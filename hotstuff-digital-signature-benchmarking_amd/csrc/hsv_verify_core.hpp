@@ -41,7 +41,26 @@ enum : uint32_t {
   kSOk = 0x20,
   kAOk = 0x40,
   kROk = 0x80,
+  // not a flag-byte bit: the device self-check failed for this item (see
+  // fault_bit); kernels turn it into the launch's fault word and the host
+  // into HSV_ERR_DEVICE_FAULT, never into a verdict
+  kFault = 0x200,
 };
+
+// Fault injection modes (hsv_test_inject_fault; tests only): what the kernels
+// read back in place of their table entries or workspace canary.
+enum : uint32_t {
+  kInjectNone = 0,
+  kInjectZeroTables = 1,  // table entries read back as zeros
+  kInjectCanary = 2,      // the lane's workspace canary is overwritten mid-batch
+  kInjectFlipTables = 3,  // one bit of table entries flipped
+};
+
+// kFault when both points decoded (the equation is then part of the verdict)
+// and the final accumulator q is not a curve point with Z != 0 (ge_is_sane).
+HSV_INL uint32_t fault_bit(uint32_t a_ok, uint32_t r_ok, const ge_ext &q) {
+  return (a_ok & r_ok & (ge_is_sane(q) ^ 1u)) ? (uint32_t)kFault : 0u;
+}
 
 // Shift a multi-limb value left by `sh` (0 < sh < 32) bits in place.
 template <int N>

@@ -168,7 +168,7 @@ HSV_INL uint32_t verify_one_full_comb(const uint32_t pk[8], const uint32_t sig[1
   fe rx, ry;
   const uint32_t r_ok = ge_decompress(sig, rx, ry);
   const uint32_t small_r = r_ok & y_is_small_order(ry);
-  return flags_byte(s_ok, a_ok, r_ok, small_a, small_r, ge_eq_affine(q, rx, ry));
+  return flags_byte(s_ok, a_ok, r_ok, small_a, small_r, ge_eq_affine(q, rx, ry)) | fault_bit(a_ok, r_ok, q);
 }
 
 template <int WA>
@@ -212,7 +212,7 @@ HSV_INL uint32_t verify_one_half_comb(const uint32_t pk[8], const uint32_t sig[1
   const sc b = sc_mul_small(lat.c1, sig + 8);
   q = comb_add_b<CB>(q, b.v, tb);
   const uint32_t same = ge_is_neutral(q);  // Q == O
-  return flags_byte(s_ok, a_ok, r_ok, small_a, small_r, same);
+  return flags_byte(s_ok, a_ok, r_ok, small_a, small_r, same) | fault_bit(a_ok, r_ok, q);
 }
 
 // ---- two-pass form: scalar prepass + point pass ---------------------------
@@ -298,7 +298,7 @@ HSV_INL uint32_t verify_one_prepped(const uint32_t pk[8], const uint32_t rb[8], 
   for (int i = 0; i < 8; ++i) b[i] = rec[(10 + i) * stride];
   q = comb_add_b<CB>(q, b, tb);
   const uint32_t same = ge_is_neutral(q);
-  return flags_byte(meta & kPrepSOk, a_ok, r_ok, small_a, small_r, same);
+  return flags_byte(meta & kPrepSOk, a_ok, r_ok, small_a, small_r, same) | fault_bit(a_ok, r_ok, q);
 }
 
 }  // namespace hsv

@@ -39,7 +39,9 @@ ERRORS = {
     -4: "HSV_ERR_ALLOC",
     -5: "HSV_ERR_ALIGN",
     -6: "HSV_ERR_PARSE",
+    -7: "HSV_ERR_DEVICE_FAULT",
 }
+HSV_ERR_DEVICE_FAULT = -7
 
 
 class HsvLibraryError(RuntimeError):
@@ -94,8 +96,15 @@ def _declare(lib):
         "hsv_get_variant": (ctypes.c_int, []),
         "hsv_set_lattice_bits": (ctypes.c_int, [ctypes.c_int]),
         "hsv_num_variants": (ctypes.c_int, []),
+        "hsv_device_faults": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+        "hsv_test_inject_fault": (ctypes.c_int, [ctypes.c_int]),
+        "hsv_host_call_stats": (None, [ctypes.POINTER(ctypes.c_double)] * 3),
+        "hsv_pack_threads": (ctypes.c_int, []),
+        "hsv_sign_mixed_order": (ctypes.c_int, [c_u8p, c_u8p, sz, ctypes.c_int, ctypes.c_int, c_u8p, c_u8p]),
     }
-    optional = {"hsv_set_lattice_bits"}  # test hooks absent from older A/B builds (tools/ab_probe.py)
+    # test / measurement hooks absent from older A/B builds (tools/ab_probe.py)
+    optional = {"hsv_set_lattice_bits", "hsv_test_inject_fault", "hsv_host_call_stats", "hsv_pack_threads",
+                "hsv_device_faults", "hsv_sign_mixed_order"}
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None) if name in optional else getattr(lib, name)
         if fn is None:

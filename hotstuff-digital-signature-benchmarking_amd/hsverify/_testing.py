@@ -1,0 +1,58 @@
+"""Test and measurement hooks of libhsv.so (not part of include/hsv.h).
+
+Kept out of the public modules: each changes process-wide behaviour of the
+library for every thread, so only tests, bench.py and tools/ use them.
+"""
+from __future__ import annotations
+
+import contextlib
+import ctypes
+
+from . import _lib
+
+# fault injection modes (csrc/hsv_verify_core.hpp kInject*)
+INJECT_NONE = 0
+INJECT_ZERO_TABLES = 1   # table entries read back as zeros
+INJECT_CANARY = 2        # a lane's workspace canary is overwritten mid-batch
+INJECT_FLIP_TABLES = 3   # one bit of table entries flipped
+
+
+def set_lattice_bits(bits: int) -> int:
+    """The lattice bound of the comb-path prepass (0 = default, 138; 133 sends
+    the tests/golden/lattice_fallback.bin challenges down the full-length
+    path).  Returns the previous bound."""
+    prev = _lib.load().hsv_set_lattice_bits(bits)
+    if prev < 0:
+        raise ValueError(f"lattice bound out of range: {bits}")
+    return prev
+
+
+def inject_fault(mode: int) -> int:
+    """Corrupt what the following launches read back (INJECT_*; 0 = off).
+    Returns the previous mode."""
+    prev = _lib.load().hsv_test_inject_fault(mode)
+    if prev < 0:
+        raise ValueError(f"unknown fault injection mode {mode}")
+    return prev
+
+
+@contextlib.contextmanager
+def injected_fault(mode: int):
+    prev = inject_fault(mode)
+    try:
+        yield
+    finally:
+        inject_fault(prev)
+
+
+def host_call_stats() -> dict:
+    """The calling thread's last host-buffer verification: pack time (host ms
+    spent copying into pinned staging), bytes copied host-to-device, wall ms."""
+    v = [ctypes.c_double() for _ in range(3)]
+    _lib.load().hsv_host_call_stats(*[ctypes.byref(x) for x in v])
+    return {"pack_ms": v[0].value, "h2d_bytes": v[1].value, "call_ms": v[2].value}
+
+
+def pack_threads() -> int:
+    """Helper threads of the library's staging-copy pool (HSV_PACK_THREADS)."""
+    return _lib.load().hsv_pack_threads()

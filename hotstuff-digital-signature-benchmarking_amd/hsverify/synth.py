@@ -10,8 +10,11 @@ Keys are derived from seeded 32-byte secrets; messages are 32-byte digests
 shaped like the reference's (QC digest = SHA-512(hash || round_le)[..32],
 consensus/src/messages.rs:201-207; TC vote digest = SHA-512(round_le ||
 high_qc_round_le)[..32], messages.rs:307-311).  Corruptions are spread evenly
-over the kinds SURVEY 8(d) lists for C3/C4 (mixed-order keys are exercised by
-the golden vectors instead, since building them needs point arithmetic).
+over the kinds SURVEY 8(d) lists for C3/C4, mixed-order keys included
+(A' = [a]B + T8 from hsv_sign_mixed_order, in both variants: k = 0 mod 8,
+which verify_strict ACCEPTS, and k != 0 mod 8, which it rejects).  The key of
+a mixed-order vote replaces the signer's key, i.e. it is that committee
+member's (malformed) key.  `accept` holds the expected verify_strict result.
 """
 from __future__ import annotations
 
@@ -44,7 +47,11 @@ SMALL_ORDER_ENCODINGS = [bytes.fromhex(h) for h in (
 UNDECODABLE = bytes.fromhex("0200000000000000000000000000000000000000000000000000000000000000")
 
 CORRUPTIONS = ("flip_R", "flip_s", "s_plus_l", "wrong_digest", "undecodable_R", "small_order_R",
-               "small_order_A", "s_bit255")
+               "small_order_A", "s_bit255", "mixed_order_A_ok", "mixed_order_A_bad")
+# kinds whose verify_strict result is still Ok (the cofactorless equation holds)
+ACCEPTED_KINDS = ("mixed_order_A_ok",)
+# kinds that replace the signer's key
+KEY_KINDS = ("small_order_A", "mixed_order_A_ok", "mixed_order_A_bad")
 
 
 @dataclass
@@ -54,10 +61,28 @@ class Workload:
     msg: np.ndarray       # (n, 32) uint8, or (32,) for one shared digest
     honest: np.ndarray    # (n,) bool: untouched honest signature
     kind: np.ndarray = field(default=None)  # (n,) int8: -1 honest, else CORRUPTIONS index
+    seeds: np.ndarray = field(default=None)  # (n, 32) uint8: the signers' secret seeds
+    accept: np.ndarray = field(default=None)  # (n,) bool: expected verify_strict Ok
+
+    def __post_init__(self):
+        if self.accept is None:
+            self.accept = self.honest.copy()
 
     @property
     def n(self) -> int:
         return self.pk.shape[0]
+
+
+def mixed_order_signature(seed: bytes, msg: bytes, torsion: int, accept: bool):
+    """(pk', sig) for the mixed-order key A' = [a]B + [2 torsion + 1]T8 of
+    `seed`, over msg, with k = 0 (mod 8) (accept) or not (hsv_sign_mixed_order)."""
+    import ctypes
+    from . import _lib
+    pk = ctypes.create_string_buffer(32)
+    sig = ctypes.create_string_buffer(64)
+    _lib.check(_lib.load().hsv_sign_mixed_order(bytes(seed), bytes(msg), len(msg), int(torsion), 1 if accept else 0,
+                                                pk, sig), "hsv_sign_mixed_order")
+    return np.frombuffer(pk.raw, np.uint8), np.frombuffer(sig.raw, np.uint8)
 
 
 def qc_digest(block_hash: bytes, round_: int) -> bytes:
@@ -83,7 +108,15 @@ def corrupt(w: Workload, frac: float, rng: np.random.Generator) -> None:
         name = CORRUPTIONS[kind]
         w.kind[i] = kind
         w.honest[i] = False
-        if name == "flip_R":
+        w.accept[i] = name in ACCEPTED_KINDS
+        if name.startswith("mixed_order_A"):
+            if w.seeds is None:
+                raise ValueError("mixed-order corruption needs the workload's signer seeds")
+            pk, sg = mixed_order_signature(bytes(w.seeds[i]), bytes(w.msg[i]), int(rng.integers(0, 4)),
+                                           name == "mixed_order_A_ok")
+            w.pk[i] = pk
+            w.sig[i] = sg
+        elif name == "flip_R":
             b = int(rng.integers(0, 255))
             w.sig[i, b // 8] ^= np.uint8(1 << (b % 8))
         elif name == "flip_s":
@@ -111,7 +144,7 @@ def independent_triples(n: int, seed: int, corrupt_frac: float = 0.05, nthreads:
     seeds = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
     msgs = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
     pk, sig = sign_many(seeds, msgs, nthreads)
-    w = Workload(pk, sig, msgs, np.ones(n, bool), np.full(n, -1, np.int8))
+    w = Workload(pk, sig, msgs, np.ones(n, bool), np.full(n, -1, np.int8), seeds=seeds)
     corrupt(w, corrupt_frac, rng)
     return w
 
@@ -129,7 +162,7 @@ def qc_votes(committee: int, seed: int = 0, corrupt_frac: float = 0.0, round_: i
     msgs = np.repeat(np.frombuffer(digest, np.uint8)[None, :], quorum, axis=0)
     pk, sig = sign_many(seeds, msgs)
     w = Workload(pk, sig, np.frombuffer(digest, np.uint8).copy(), np.ones(quorum, bool),
-                 np.full(quorum, -1, np.int8))
+                 np.full(quorum, -1, np.int8), seeds=seeds)
     corrupt(w, corrupt_frac, np.random.default_rng(seed + 17))
     return w
 
@@ -142,7 +175,7 @@ def tc_votes(committee: int, seed: int = 0, corrupt_frac: float = 0.0, round_: i
     hqc = rng.integers(round_ - 10, round_, size=quorum)
     msgs = np.stack([np.frombuffer(tc_vote_digest(round_, int(h)), np.uint8) for h in hqc])
     pk, sig = sign_many(seeds, msgs)
-    w = Workload(pk, sig, msgs, np.ones(quorum, bool), np.full(quorum, -1, np.int8))
+    w = Workload(pk, sig, msgs, np.ones(quorum, bool), np.full(quorum, -1, np.int8), seeds=seeds)
     corrupt(w, corrupt_frac, rng)
     return w
 
@@ -152,6 +185,7 @@ class TxWorkload:
     txs: np.ndarray       # (n, tx_size) uint8: message || pk || sig
     honest: np.ndarray    # (n,) bool
     kind: np.ndarray      # (n,) int8: -1 honest, else CORRUPTIONS index
+    accept: np.ndarray = field(default=None)  # (n,) bool: expected verify(..).is_ok()
 
     @property
     def n(self) -> int:
@@ -175,7 +209,7 @@ def transactions(n: int, tx_size: int = 512, seed: int = 0, corrupt_frac: float 
     for i in range(n):
         digests[i] = np.frombuffer(hashlib.sha512(msgs[i].tobytes()).digest()[:32], np.uint8)
     pk, sig = sign_many(seeds, digests, nthreads)
-    w = Workload(pk, sig, digests, np.ones(n, bool), np.full(n, -1, np.int8))
+    w = Workload(pk, sig, digests, np.ones(n, bool), np.full(n, -1, np.int8), seeds=seeds)
     corrupt(w, corrupt_frac, rng)
     bad_msg = np.nonzero(w.kind == CORRUPTIONS.index("wrong_digest"))[0]
     if mlen:
@@ -186,4 +220,4 @@ def transactions(n: int, tx_size: int = 512, seed: int = 0, corrupt_frac: float 
         for i in bad_msg:
             w.sig[i, 32] ^= np.uint8(1)
     txs = np.concatenate([msgs, w.pk, w.sig], axis=1)
-    return TxWorkload(np.ascontiguousarray(txs), w.honest, w.kind)
+    return TxWorkload(np.ascontiguousarray(txs), w.honest, w.kind, w.accept)

@@ -71,6 +71,22 @@ def verify_device(pk, sig, msg, flags=None, strict_bits=None, stream=None) -> No
     _lib.check(rc, "hsv_verify_device_bits")
 
 
+def device_faults(device: int = -1, clear: bool = True) -> int:
+    """Self-check results of the device-resident calls (hsv_device_faults):
+    0, or fault bits (1: a final point failed the curve check, 2: a workspace
+    canary changed).  Call after synchronising the streams the calls ran on."""
+    return _lib.check(_lib.load().hsv_device_faults(device, 1 if clear else 0), "hsv_device_faults")
+
+
+def check_device_faults(device: int = -1) -> None:
+    """Raise HsvLibraryError (HSV_ERR_DEVICE_FAULT) if the device-resident calls
+    since the last check tripped a self-check; clears the record."""
+    bits = device_faults(device, True)
+    if bits:
+        raise _lib.HsvLibraryError(f"HSV_ERR_DEVICE_FAULT: device self-check bits {bits:#x}: "
+                                   "the flags of those launches are not a verdict")
+
+
 def sign_many(seeds: np.ndarray, msgs: np.ndarray, nthreads: int = 0):
     """seeds (n,32), msgs (n,L) -> (pk (n,32), sig (n,64)) via host threads."""
     seeds = np.ascontiguousarray(seeds, dtype=np.uint8).reshape(-1, 32)
@@ -92,16 +108,6 @@ def measure_mad_peak() -> float:
 
 def set_variant(v: int) -> None:
     _lib.check(_lib.load().hsv_set_variant(v), "hsv_set_variant")
-
-
-def set_lattice_bits(bits: int) -> int:
-    """Test hook: the lattice bound of the comb-path prepass (0 = default, 138;
-    133 sends the tests/golden/lattice_fallback.bin challenges down the
-    full-length path).  Returns the previous bound."""
-    prev = _lib.load().hsv_set_lattice_bits(bits)
-    if prev < 0:
-        raise ValueError(f"lattice bound out of range: {bits}")
-    return prev
 
 
 def get_variant() -> int:

@@ -55,6 +55,11 @@ extern "C" {
 #define HSV_ERR_ALLOC (-4)
 #define HSV_ERR_ALIGN (-5)
 #define HSV_ERR_PARSE (-6) /* malformed wire bytes (hsv_*_bincode) */
+/* The device self-checks failed: an item's final point was not a curve point
+ * (corrupted table memory, workspace or HBM) or a workspace canary changed.
+ * The launch's flags are not a verdict; callers treat it like any other
+ * infrastructure error (a GPU failure is never a silent reject). */
+#define HSV_ERR_DEVICE_FAULT (-7)
 
 /* ---- lifecycle and device binding -------------------------------------- */
 /* Optional: contexts are created lazily on first use.
@@ -144,6 +149,15 @@ int hsv_verify_device_bits(const uint8_t *d_pk, size_t pk_stride, const uint8_t 
                            size_t sig_stride, const uint8_t *d_msg, size_t msg_stride, size_t n,
                            uint8_t *d_flags, uint32_t *d_strict_bits, void *stream);
 
+/* Device self-check results of the device-resident calls on `device` (-1:
+ * every device) since the last clear.  The stream-ordered calls cannot return
+ * a kernel's outcome, so their kernels record it in a per-device word; read it
+ * after synchronising the stream the calls ran on.  Returns 0 (no fault), the
+ * fault bits (1: a final point failed the curve check, 2: a workspace canary
+ * changed), or < 0 on error.  clear != 0 resets the word(s).  Host-buffer
+ * calls report their own launches' faults as HSV_ERR_DEVICE_FAULT instead. */
+int hsv_device_faults(int device, int clear);
+
 /* ---- committee key cache --------------------------- */
 /* Consensus keys are fixed per epoch (consensus/src/config.rs Committee).  A
  * committee holds, in HBM of the device bound at creation (hsv_init), a 384 KiB
@@ -229,6 +243,15 @@ int hsv_sign(const uint8_t seed[32], const uint8_t *msg, size_t msg_len, uint8_t
  * keys and n signatures.  nthreads <= 0 picks min(hardware concurrency, 16). */
 int hsv_sign_many(const uint8_t *seeds, const uint8_t *msgs, size_t msg_len, size_t n,
                   uint8_t *pk_out, uint8_t *sig_out, int nthreads);
+
+/* Synthesis helper for the corrupted-input mixes (SURVEY 8(d) C3/C4 "mixed-
+ * order A"; Appendix A.3 rows 7-8): the key A' = [a]B + [2*torsion+1]T8 (a
+ * from seed as in hsv_public_key, T8 a point of order 8, torsion in 0..3) and
+ * a signature over msg whose challenge k is = 0 (mod 8) when accept != 0
+ * (verify_strict accepts: cofactorless equation holds) or != 0 (mod 8) when
+ * accept == 0 (rejected; a cofactored verifier would accept). */
+int hsv_sign_mixed_order(const uint8_t seed[32], const uint8_t *msg, size_t msg_len, int torsion, int accept,
+                         uint8_t pk_out[32], uint8_t sig_out[64]);
 
 /* ---- measurement helpers ------------------------------------------------ */
 /* Measured issue rate of v_mad_u64_u32 on the current device, in

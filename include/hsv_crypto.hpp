@@ -75,6 +75,33 @@ inline std::atomic<uint64_t> &infrastructure_fallback_uses() {
 }
 inline void set_infrastructure_fallback(InfrastructureFallback f) { infrastructure_fallback() = std::move(f); }
 
+// Latency routing of the caller.
+// One signature on the GPU costs a launch plus one dependent root chain
+// (~0.08 ms for a cached committee key), one host core ~0.04 ms; a QC of
+// three votes is level; from a handful of votes on the GPU wins.  A
+// deployment installs a host verifier with the same semantics (dalek in the
+// Rust shim) and a size limit: verify calls and verify_batch calls of at most
+// max_batch votes go to it, everything larger to libhsv.  Unlike the
+// infrastructure fallback this is a routing choice made before the call --
+// libhsv's verdicts are never second-guessed.  Every routed call is counted.
+struct HostRoute {
+  size_t max_batch = 0;  // verify_batch calls of at most this many votes go to the host
+  bool single = false;   // Signature::verify goes to the host
+  std::function<bool(const uint8_t *digest, const uint8_t *pk, const uint8_t *sig)> verify_strict;
+  std::function<bool(const uint8_t *digest, const uint8_t *votes, size_t n)> verify_batch;
+};
+
+inline HostRoute &host_route() {
+  static HostRoute r;
+  return r;
+}
+inline std::atomic<uint64_t> &host_route_uses() {
+  static std::atomic<uint64_t> n{0};
+  return n;
+}
+// Install once at startup, before verify calls run on other threads.
+inline void set_host_route(HostRoute r) { host_route() = std::move(r); }
+
 // ed25519::Error: opaque.
 struct CryptoError {
   std::string message = "signature error";
@@ -228,6 +255,12 @@ class Signature {
   // Signature::verify (lib.rs:204-208): ed25519-dalek verify_strict semantics.
   Result verify(const Digest &digest, const PublicKey &public_key) const {
     const std::array<uint8_t, 64> f = flatten();
+    const HostRoute &route = host_route();
+    if (route.single && route.verify_strict) {
+      ++host_route_uses();
+      return route.verify_strict(digest.bytes.data(), public_key.bytes.data(), f.data()) ? Result::ok()
+                                                                                         : Result::err();
+    }
     int rc = hsv_verify_strict(digest.bytes.data(), public_key.bytes.data(), f.data());
     if (rc < 0 && infrastructure_fallback().verify_strict) {
       ++infrastructure_fallback_uses();
@@ -244,6 +277,11 @@ class Signature {
       std::memcpy(packed.data() + 96 * i, votes[i].first.bytes.data(), 32);
       std::memcpy(packed.data() + 96 * i + 32, votes[i].second.part1.data(), 32);
       std::memcpy(packed.data() + 96 * i + 64, votes[i].second.part2.data(), 32);
+    }
+    const HostRoute &route = host_route();
+    if (votes.size() <= route.max_batch && route.verify_batch) {
+      ++host_route_uses();
+      return route.verify_batch(digest.bytes.data(), packed.data(), votes.size()) ? Result::ok() : Result::err();
     }
     int rc = hsv_verify_batch_packed(digest.bytes.data(), packed.data(), votes.size());
     if (rc < 0 && infrastructure_fallback().verify_batch) {

@@ -10,6 +10,7 @@
 // a machine without a GPU every verify goes to it and the tests still pass;
 // on a GPU it must never be used.
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -200,8 +201,36 @@ static void install_oracle_fallback() {
   set_infrastructure_fallback(std::move(f));
 }
 
+// --route: single verifies and QCs of at most 2 votes on the host verifier
+// (the C oracle stands in for dalek), larger QCs on libhsv
+static void install_host_route() {
+  HostRoute r;
+  r.single = true;
+  r.max_batch = 2;
+  r.verify_strict = [](const uint8_t *digest, const uint8_t *pk, const uint8_t *sig) {
+    return (oracle_verify_flags(pk, sig, digest, 32) & HSV_STRICT_OK) != 0;
+  };
+  r.verify_batch = [](const uint8_t *digest, const uint8_t *votes, size_t n) {
+    for (size_t i = 0; i < n; ++i) {
+      const uint8_t fl = oracle_verify_flags(votes + 96 * i, votes + 96 * i + 32, digest, 32);
+      if ((fl & (HSV_PARSE_OK | HSV_EQ_OK)) != (HSV_PARSE_OK | HSV_EQ_OK)) return false;
+    }
+    return true;
+  };
+  set_host_route(std::move(r));
+}
+
+// libhsv's fault injection hook (test only, not in hsv.h)
+extern "C" int hsv_test_inject_fault(int mode);
+
 int main(int argc, char **argv) {
-  const bool fallback = argc > 1 && std::strcmp(argv[1], "--fallback") == 0;
+  bool fallback = false;
+  for (int i = 1; i < argc; ++i) {
+    if (std::strcmp(argv[i], "--fallback") == 0) fallback = true;
+    if (std::strcmp(argv[i], "--route") == 0) install_host_route();
+    // --inject MODE: every launch reads corrupted tables (csrc/hsv_verify_core.hpp kInject*)
+    if (std::strcmp(argv[i], "--inject") == 0 && i + 1 < argc) hsv_test_inject_fault(std::atoi(argv[++i]));
+  }
   if (fallback) install_oracle_fallback();
   import_export_public_key();
   import_export_secret_key();
@@ -216,6 +245,7 @@ int main(int argc, char **argv) {
     return 1;
   }
   if (fallback) std::printf("infrastructure fallbacks: %llu\n", (unsigned long long)infrastructure_fallback_uses());
+  std::printf("host-routed calls: %llu\n", (unsigned long long)host_route_uses());
   std::printf("crypto_tests: all passed\n");
   return 0;
 }

@@ -70,7 +70,7 @@ def test_two_chunks_ragged_tail_with_bits(mods, oracle_lib):
     assert (f[idx] == exp).all()
     # copy 0 keeps its digests: its honest items verify and its corrupted ones do
     # not (a perturbed copy can undo a wrong_digest corruption, so only copy 0)
-    h0 = base.honest
+    h0 = base.accept
     assert (f[:base.n][h0] & o.STRICT_OK).all() and not (f[:base.n][~h0] & o.STRICT_OK).any()
 
 
@@ -95,12 +95,17 @@ def test_c5_2p24_properties(mods, oracle_lib):
     exp = oracle_flags(oracle_lib, base.pk, base.sig, base.msg)
     assert (per_copy[0] == exp).all()
     assert (_unpack(bits.cpu().numpy(), n) == (f & o.STRICT_OK)).all()
-    honest = np.tile(base.honest, reps)
+    honest = np.tile(base.accept, reps)
     assert (f[honest] & o.STRICT_OK).all() and not (f[~honest] & o.STRICT_OK).any()
     kinds = {name: per_copy[0][base.kind == k] for k, name in enumerate(synth.CORRUPTIONS)}
     assert not (kinds["s_plus_l"] & o.S_OK).any() and not (kinds["s_bit255"] & o.S_OK).any()
     assert not (kinds["undecodable_R"] & o.R_OK).any()
     assert (kinds["small_order_R"] & o.SMALL_R).all() and (kinds["small_order_A"] & o.SMALL_A).all()
+    # mixed-order keys: the cofactorless equation decides (Appendix A.3 rows 7-8)
+    assert kinds["mixed_order_A_ok"].size and (kinds["mixed_order_A_ok"] & o.STRICT_OK).all()
+    assert not (kinds["mixed_order_A_ok"] & o.SMALL_A).any()
+    assert kinds["mixed_order_A_bad"].size and (kinds["mixed_order_A_bad"] & o.PARSE_OK).all()
+    assert not (kinds["mixed_order_A_bad"] & o.EQ_OK).any()
     # idempotent
     flags2 = torch.zeros_like(flags)
     verifier.verify_device(t_pk, t_sig, t_msg, flags2)

@@ -102,3 +102,42 @@ def test_synth_workload_shapes(lib):
     assert q.n == 67 and q.msg.shape == (32,)
     t = synth.tc_votes(1000)
     assert t.n == 667 and t.msg.shape == (667, 32)
+
+
+def test_mixed_order_signer_matches_oracle(lib):
+    """hsv_sign_mixed_order (the C3/C4 mixed-order-A corruption): the key is
+    [a]B plus an order-8 torsion point, and the oracle decides as SURVEY A.3
+    rows 7-8 say -- k = 0 (mod 8): verify_strict Ok (cofactorless equation
+    holds, A is not small-order); k != 0 (mod 8): parses but the equation fails."""
+    from hsverify import synth
+    rnd = np.random.default_rng(9)
+    for t in range(4):
+        for accept in (True, False):
+            seed = bytes(rnd.integers(0, 256, 32, dtype=np.uint8))
+            msg = bytes(rnd.integers(0, 256, 32, dtype=np.uint8))
+            pk, sig = synth.mixed_order_signature(seed, msg, t, accept)
+            pk, sig = bytes(pk), bytes(sig)
+            pt = o.decompress(pk)
+            assert pt is not None and not o.is_small_order(o.to_ext(pt))
+            assert not o.is_identity(o.scalar_mult(o.L, o.to_ext(pt)))       # not in the prime-order subgroup
+            assert o.is_identity(o.scalar_mult(8 * o.L, o.to_ext(pt)))
+            k = o.scalar_from_hash(o.sha512(sig[:32] + pk + msg))
+            assert (k % 8 == 0) == accept
+            f = o.verify_flags(pk, sig, msg)
+            assert f & o.PARSE_OK and not f & o.SMALL_A
+            assert bool(f & o.STRICT_OK) == accept and bool(f & o.EQ_OK) == accept
+
+
+def test_synth_corruption_mix_has_every_kind(lib):
+    """bit-flip in R / s, s + l, wrong digest, undecodable R,
+    small-order R / A, mixed-order A -- all present in the 5 % of a C3 quorum,
+    and `accept` marks exactly the honest votes and the k = 0 (mod 8)
+    mixed-order ones (checked against the Python oracle)."""
+    from hsverify import synth
+    for make in (synth.qc_votes, synth.tc_votes):
+        w = make(1000, seed=5, corrupt_frac=0.05)
+        assert set(np.unique(w.kind[w.kind >= 0])) == set(range(len(synth.CORRUPTIONS)))
+        msg = w.msg if w.msg.ndim == 2 else np.repeat(w.msg[None], w.n, 0)
+        for i in np.nonzero(w.kind >= 0)[0]:
+            f = o.verify_flags(bytes(w.pk[i]), bytes(w.sig[i]), bytes(msg[i]))
+            assert bool(f & o.STRICT_OK) == bool(w.accept[i]), synth.CORRUPTIONS[w.kind[i]]

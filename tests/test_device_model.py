@@ -62,7 +62,7 @@ def test_virtual_shards_gather_matches_unsharded_and_oracle(mods, oracle_lib, sh
     finally:
         verifier.set_virtual_shards(0)
     assert (sharded == whole).all()
-    assert (whole[w.honest] & o.STRICT_OK).all() and not (whole[~w.honest] & o.STRICT_OK).any()
+    assert (whole[w.accept] & o.STRICT_OK).all() and not (whole[~w.accept] & o.STRICT_OK).any()
     # oracle sample around every shard boundary
     cuts = [n * d // shards for d in range(1, shards)]
     idx = np.unique(np.concatenate([np.arange(max(0, c - 40), min(n, c + 40)) for c in cuts] + [np.arange(64)]))
@@ -81,7 +81,7 @@ def test_virtual_shards_transactions(mods, oracle_lib):
     finally:
         verifier.set_virtual_shards(0)
     assert (sharded == whole).all()
-    assert (whole[w.honest] & o.STRICT_OK).all() and not (whole[~w.honest] & o.STRICT_OK).any()
+    assert (whole[w.accept] & o.STRICT_OK).all() and not (whole[~w.accept] & o.STRICT_OK).any()
 
 
 def test_many_concurrent_small_calls(mods, golden):
@@ -138,7 +138,7 @@ def test_device_batches_on_concurrent_streams(mods, golden):
         assert torch.equal(outs[i], ref), i
         assert (gouts[i].cpu().numpy() == g["flags"]).all(), i
     f = ref.cpu().numpy()
-    assert (f[w.honest] & o.STRICT_OK).all() and not (f[~w.honest] & o.STRICT_OK).any()
+    assert (f[w.accept] & o.STRICT_OK).all() and not (f[~w.accept] & o.STRICT_OK).any()
 
 
 def test_committee_survives_shutdown(mods, hsv, golden):

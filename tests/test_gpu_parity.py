@@ -46,11 +46,11 @@ def test_lattice_fallback_records_every_variant(api, fallback_records, bits):
     match the oracle's flags either way.  The automatic committee cache is off
     so the generic kernels run."""
     _, verifier, _ = api
-    from hsverify import _lib
+    from hsverify import _lib, _testing
     lib = _lib.load()
     fb = fallback_records
     default = verifier.get_variant()
-    prev = verifier.set_lattice_bits(bits)
+    prev = _testing.set_lattice_bits(bits)
     lib.hsv_set_auto_committee(0)
     try:
         for v in verifier.variants():
@@ -67,7 +67,7 @@ def test_lattice_fallback_records_every_variant(api, fallback_records, bits):
             assert (got == fb["flags"][idx]).all(), v
     finally:
         verifier.set_variant(default)
-        verifier.set_lattice_bits(prev)
+        _testing.set_lattice_bits(prev)
         lib.hsv_set_auto_committee(1)
 
 
@@ -165,6 +165,14 @@ def test_qc_configs(api, oracle_lib, committee):
     s[40] ^= 4
     bad[i] = (bad[i][0], crypto.Signature(bytes(s[:32]), bytes(s[32:])))
     assert crypto.Signature.verify_batch(d, bad).is_err()
+    # per-vote flags, not only the verdict: clean and corrupted quorums (for C1
+    # one vote in three), all 8 bits against the C oracle
+    for frac in (0.0, 0.34 if committee == 4 else 0.05):
+        wc = synth.qc_votes(committee, seed=committee + 1, corrupt_frac=frac)
+        msg = wc.msg if wc.msg.ndim == 2 else np.repeat(wc.msg[None], wc.n, 0)
+        got = verifier.verify_flags(wc.pk, wc.sig, msg)
+        assert (got == oracle_flags(oracle_lib, wc.pk, wc.sig, msg)).all()
+        assert (got[wc.accept] & o.STRICT_OK).all() and not (got[~wc.accept] & o.STRICT_OK).any()
 
 
 def test_c3_committee_1000_qc_and_tc_bit_exact(api, oracle_lib):
@@ -175,8 +183,11 @@ def test_c3_committee_1000_qc_and_tc_bit_exact(api, oracle_lib):
         got = verifier.verify_flags(w.pk, w.sig, msg)
         exp = oracle_flags(oracle_lib, w.pk, w.sig, msg)
         assert (got == exp).all()
-        assert (got[w.honest] & o.STRICT_OK).all()
-        assert not (got[~w.honest] & o.STRICT_OK).any()
+        assert (got[w.accept] & o.STRICT_OK).all()
+        assert not (got[~w.accept] & o.STRICT_OK).any()
+        # every corruption kind SURVEY 8(d) lists is in the vector, mixed-order keys included
+        assert set(np.unique(w.kind[w.kind >= 0])) == set(range(len(synth.CORRUPTIONS)))
+        assert (got[w.kind == synth.CORRUPTIONS.index("mixed_order_A_ok")] & o.STRICT_OK).all()
 
 
 def test_random_batch_vs_c_oracle(api, oracle_lib):
@@ -285,13 +296,19 @@ def test_c4_full_size_properties(api, oracle_lib):
     verifier.verify_device(pk, sig, msg, flags)
     torch.cuda.synchronize()
     f = flags.cpu().numpy()
-    # honest signatures are all accepted; every corruption kind is rejected
-    assert (f[w.honest] & o.STRICT_OK).all()
-    assert not (f[~w.honest] & o.STRICT_OK).any()
+    # honest signatures are all accepted; every corruption kind but the
+    # accepted mixed-order one (k = 0 mod 8) is rejected
+    assert (f[w.accept] & o.STRICT_OK).all()
+    assert not (f[~w.accept] & o.STRICT_OK).any()
     kinds = {name: f[w.kind == k] for k, name in enumerate(synth.CORRUPTIONS)}
     assert not (kinds["s_plus_l"] & o.S_OK).any() and not (kinds["s_bit255"] & o.S_OK).any()
     assert not (kinds["undecodable_R"] & o.R_OK).any()
     assert (kinds["small_order_R"] & o.SMALL_R).all() and (kinds["small_order_A"] & o.SMALL_A).all()
+    # mixed-order keys: the cofactorless equation decides (Appendix A.3 rows 7-8)
+    assert kinds["mixed_order_A_ok"].size and (kinds["mixed_order_A_ok"] & o.STRICT_OK).all()
+    assert not (kinds["mixed_order_A_ok"] & o.SMALL_A).any()
+    assert kinds["mixed_order_A_bad"].size and (kinds["mixed_order_A_bad"] & o.PARSE_OK).all()
+    assert not (kinds["mixed_order_A_bad"] & o.EQ_OK).any()
     # idempotent: a second launch gives identical bytes
     flags2 = torch.zeros_like(flags)
     verifier.verify_device(pk, sig, msg, flags2)
@@ -319,6 +336,6 @@ def test_host_api_pipelined_chunks_match_device_api(api, oracle_lib):
     verifier.verify_device(pk, sig, msg, flags)
     torch.cuda.synchronize()
     assert (got == flags.cpu().numpy()).all()
-    assert (got[w.honest] & o.STRICT_OK).all() and not (got[~w.honest] & o.STRICT_OK).any()
+    assert (got[w.accept] & o.STRICT_OK).all() and not (got[~w.accept] & o.STRICT_OK).any()
     sample = np.sort(np.random.default_rng(3).choice(n, 4096, replace=False))
     assert (got[sample] == oracle_flags(oracle_lib, w.pk[sample], w.sig[sample], w.msg[sample])).all()

@@ -242,3 +242,48 @@ def test_degenerate_accumulator_fails_closed(core_host):
     final checks (ge_is_neutral, ge_eq_affine) also require Z != 0, so it is
     rejected, while the neutral point itself still compares equal."""
     assert _run(core_host, ["--degenerate"], []) == ["0", "0", "1", "1"]
+
+
+def test_sanity_check_separates_points_from_corruption(core_host):
+    """ge_is_sane, the device self-check on every final accumulator: curve
+    points with Z != 0 pass (identity, B, [2^10]B); (0 : 0 : 0 : 0), an
+    off-curve X and Z = 0 fail."""
+    assert _run(core_host, ["--sanity"], []) == ["1", "0", "1", "0", "1", "0"]
+
+
+@pytest.mark.parametrize("mode", [1, 3])
+def test_injected_table_corruption_is_a_fault_not_a_verdict(core_host, golden, mode):
+    """The kernel's fault injection (zeroed / bit-flipped table entries between
+    the table build and the window loop) replayed on the host-built two-pass
+    path: every record whose points decode reports the fault (the host turns
+    it into HSV_ERR_DEVICE_FAULT); records whose A or R does not decode keep
+    their flags (their verdict never depends on the equation)."""
+    idx = list(range(golden["n_edge"])) + list(range(golden["n_edge"], len(golden["flags"]), 5))
+    lines = [f"{bytes(golden['pk'][i]).hex()} {bytes(golden['sig'][i]).hex()} {bytes(golden['msg'][i]).hex()}"
+             for i in idx]
+    got = _run(core_host, ["--inject", str(mode)], lines)
+    for i, g in zip(idx, got):
+        f = int(golden["flags"][i])
+        decoded = (f & o.A_OK) and (f & o.R_OK)
+        if decoded:
+            assert g == "fault", golden["cases"][i]
+        else:
+            assert int(g, 16) == f, golden["cases"][i]
+
+
+@pytest.mark.parametrize("mode", [1, 3])
+def test_injected_committee_table_corruption_is_a_fault(core_host, golden, mode):
+    """Same for the committee kernels' key tables (verify_one_comb)."""
+    idx = list(range(golden["n_edge"]))
+    keys = sorted({bytes(golden["pk"][i]).hex() for i in idx})
+    kidx = {k: n for n, k in enumerate(keys)}
+    lines = [str(len(keys))] + keys + [
+        f"{kidx[bytes(golden['pk'][i]).hex()]} {bytes(golden['sig'][i]).hex()} {bytes(golden['msg'][i]).hex()}"
+        for i in idx]
+    got = _run(core_host, ["--comb", str(mode)], lines)
+    for i, g in zip(idx, got):
+        f = int(golden["flags"][i])
+        if (f & o.A_OK) and (f & o.R_OK):
+            assert g == "fault", golden["cases"][i]
+        else:
+            assert int(g, 16) == f, golden["cases"][i]

@@ -114,7 +114,7 @@ def test_tx_fixed_size_vs_oracle(hsv, oracle_lib, size):
     got = mempool.verify_transactions_fixed(w.txs)
     exp = oracle_tx_flags(oracle_lib, w.txs.reshape(-1), tx_size=size, n=w.n)
     assert (got == exp).all(), np.nonzero(got != exp)[0][:8]
-    assert (got[w.honest] & o.STRICT_OK).all() and not (got[~w.honest] & o.STRICT_OK).any()
+    assert (got[w.accept] & o.STRICT_OK).all() and not (got[~w.accept] & o.STRICT_OK).any()
 
 
 @pytest.mark.gpu
