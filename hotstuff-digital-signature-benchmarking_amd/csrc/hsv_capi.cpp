@@ -304,7 +304,10 @@ class PackPool {
   };
 
   PackPool() {
-    int n = 6;  // the GPU box's cgroup gives a job 16 CPUs; 7 copying threads
+    // default: 11 helpers + the caller, capped by the CPUs this process may
+    // run on (the GPU box's cgroup gives a job 16); at 12 copying threads the
+    // pack of 2^20 triples takes ~1.3 ms (tools/host_pipeline_probe.py)
+    int n = std::min(11, (int)std::thread::hardware_concurrency() - 1);
     if (const char *v = std::getenv("HSV_PACK_THREADS")) n = std::atoi(v);
     n = std::max(0, std::min(n, 32));
     for (int i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
@@ -515,12 +518,13 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
     pend_m[b] = 0;
     return HSV_OK;
   };
-  // pack items [base, base + m) into the dense layout the kernels read, split
-  // over the pack pool by item range
-  auto pack = [&](uint8_t *h, size_t base, size_t m) {
+  // pack items [base + lo, base + hi) of a chunk into the dense layout the
+  // kernels read, split over the pack pool by item range
+  auto pack_range = [&](uint8_t *h, size_t base, size_t lo0, size_t hi0) {
+    const size_t m = hi0 - lo0;
     const int nparts = (int)std::min<size_t>(64, (m * 128 + kPackPart - 1) / kPackPart);
     auto part = [&](int p) {
-      const size_t lo = m * p / nparts, hi = m * (p + 1) / nparts;
+      const size_t lo = lo0 + m * p / nparts, hi = lo0 + m * (p + 1) / nparts;
       if (pk_stride == 32) std::memcpy(h + pk_off + 32 * lo, pk + (base + lo) * 32, (hi - lo) * 32);
       else for (size_t i = lo; i < hi; ++i) std::memcpy(h + pk_off + 32 * i, pk + (base + i) * pk_stride, 32);
       if (sig_stride == 64) std::memcpy(h + sig_off + 64 * lo, sig + (base + lo) * 64, (hi - lo) * 64);
@@ -531,9 +535,12 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
     };
     if (nparts < 2) part(0);
     else PackPool::get().run(nparts, part);
+  };
+  // the rest of a chunk's staging: the shared digest, and zeroed flags (a flag
+  // the kernels failed to write reads as a rejection, never as an earlier
+  // call's verdict) and self-check words
+  auto pack_tail = [&](uint8_t *h, size_t m) {
     if (msg_stride == 0) std::memcpy(h + msg_off, msg, 32);
-    // a flag the kernels failed to write reads as a rejection, never as an
-    // earlier call's verdict; the self-check words start at zero
     std::memset(h + flag_off, 0, m);
     std::memset(h + fault_off, 0, kFaultBytes);
   };
@@ -546,7 +553,39 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
     uint8_t *h = s.h_buf + (size_t)b * total;
     uint8_t *d = s.d_buf + (size_t)b * total;
     const auto t_pack = std::chrono::steady_clock::now();
-    pack(h, base, m);
+    if (pipe && base == 0) {
+      // nothing hides the first chunk's pack and copy: copy it in slices, each
+      // as soon as it is packed, so the DMA engine runs beside the packing
+      constexpr size_t kSlices = 4;
+      for (size_t q = 0; q < kSlices; ++q) {
+        const size_t lo = m * q / kSlices, hi = m * (q + 1) / kSlices;
+        pack_range(h, base, lo, hi);
+        hipError_t e = hipMemcpyAsync(d + pk_off + 32 * lo, h + pk_off + 32 * lo, 32 * (hi - lo),
+                                      hipMemcpyHostToDevice, st);
+        if (e == hipSuccess)
+          e = hipMemcpyAsync(d + sig_off + 64 * lo, h + sig_off + 64 * lo, 64 * (hi - lo), hipMemcpyHostToDevice, st);
+        if (e == hipSuccess && msg_stride)
+          e = hipMemcpyAsync(d + msg_off + 32 * lo, h + msg_off + 32 * lo, 32 * (hi - lo), hipMemcpyHostToDevice, st);
+        if (e != hipSuccess) return drain(hip_fail("hipMemcpyAsync H2D", e));
+      }
+      pack_tail(h, m);
+      const size_t tail_from = msg_stride ? flag_off : msg_off;
+      hipError_t e = hipMemcpyAsync(d + tail_from, h + tail_from, fault_off + kFaultBytes - tail_from,
+                                    hipMemcpyHostToDevice, st);
+      if (e != hipSuccess) return drain(hip_fail("hipMemcpyAsync H2D", e));
+      t_pack_ms += ms_since(t_pack);
+      t_h2d_bytes += fault_off + kFaultBytes;
+      e = hsv_launch_verify(v, d + pk_off, 32, d + sig_off, 64, d + msg_off, msg_stride ? 32 : 0, (uint32_t)m,
+                            d + flag_off, nullptr, comb_b, reinterpret_cast<uint32_t *>(d + fault_off), st);
+      if (e != hipSuccess) return drain(hip_fail("verify kernel launch", e));
+      e = hipMemcpyAsync(h + flag_off, d + flag_off, fault_off + kFaultBytes - flag_off, hipMemcpyDeviceToHost, st);
+      if (e != hipSuccess) return drain(hip_fail("hipMemcpyAsync D2H", e));
+      pend_base[b] = base;
+      pend_m[b] = m;
+      continue;
+    }
+    pack_range(h, base, 0, m);
+    pack_tail(h, m);
     t_pack_ms += ms_since(t_pack);
     // small batches (a QC of non-cached keys, a single vote): the kernels read
     // the pinned staging buffer and write the flags through its device

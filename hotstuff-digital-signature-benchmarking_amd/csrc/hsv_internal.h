@@ -75,6 +75,19 @@ extern "C" {
 // (offsets[i]..offsets[i+1] of txs, or fixed tx_size when offsets is NULL).
 hipError_t hsv_launch_tx_records(const uint8_t *txs, const uint64_t *offsets, uint64_t tx_size, uint32_t n,
                                  uint8_t *records, hipStream_t stream);
+// The same records plus the point pass's scalar prepass on them (one read of
+// each transaction): prep = the SoA prepass records (kPrepWords words per
+// item, row stride n), items without a short lattice pair appended to fb_list
+// through *fb_count.  Used by hsv_launch_verify_tx.
+hipError_t hsv_launch_tx_prep(const uint8_t *txs, const uint64_t *offsets, uint64_t tx_size, uint32_t n,
+                              uint8_t *records, uint32_t *prep, uint32_t *fb_count, uint32_t *fb_list,
+                              int lat_bits, hipStream_t stream);
+// Transactions end to end: records (128 B per item, caller's buffer) and
+// verification, fused as above for large batches of the product variants;
+// otherwise hsv_launch_tx_records + hsv_launch_verify.
+hipError_t hsv_launch_verify_tx(int variant, const uint8_t *txs, const uint64_t *offsets, uint64_t tx_size,
+                                uint32_t n, uint8_t *records, uint8_t *flags_out, uint32_t *strict_bits,
+                                const uint32_t *comb_b, uint32_t *fault, hipStream_t stream);
 // flags 0 (and STRICT_OK bit cleared) for transactions shorter than 96 bytes
 hipError_t hsv_launch_tx_mask(const uint64_t *offsets, uint32_t n, uint8_t *flags, uint32_t *strict_bits,
                               hipStream_t stream);

@@ -965,10 +965,21 @@ hipError_t launch_mt(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
 // Two-pass launch (variants 19/20): prepass over all items, then the
 // persistent point pass.  Workspace: per-lane tables | counters (256 B) |
 // fallback list (4 B per item) | prep records (kPrepWords x 4 B per item).
+// Transactions whose records the prepass writes itself (hsv_launch_tx_prep):
+// the point pass then reads pk / R (and, for fallback items, s and the
+// digest) from `records` at stride 128.
+struct TxPrep {
+  const uint8_t *txs;
+  const uint64_t *offsets;
+  uint64_t tx_size;
+  uint8_t *records;
+};
+
 template <int WA, int WAVES, int CB, bool TAIL = false>
 hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
                      const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
-                     uint32_t *strict_bits, const uint32_t *comb_b, uint32_t *fault, hipStream_t stream) {
+                     uint32_t *strict_bits, const uint32_t *comb_b, uint32_t *fault, hipStream_t stream,
+                     const TxPrep *tx = nullptr) {
   const void *kern = reinterpret_cast<const void *>(hsv::hsv_verify_hp_kernel<WA, WAVES, CB>);
 #if HSV_ALL_VARIANTS
   if constexpr (TAIL) kern = reinterpret_cast<const void *>(hsv::hsv_verify_hpt_kernel<WA, WAVES, CB>);
@@ -1011,7 +1022,15 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
   uint32_t *rec = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256 + canary_bytes + fb_bytes);
   e = hipMemsetAsync(ctr, 0, sizeof(hsv::HcCounters), stream);
   if (e == hipSuccess && strict_bits) e = hipMemsetAsync(strict_bits, 0, (size_t)((n + 31u) / 32u) * 4u, stream);
-  if (e == hipSuccess) {
+  if (e == hipSuccess && tx) {
+    static_assert(WA == 4, "hsv_launch_tx_prep writes the WA = 4 prepass record");
+    e = hsv_launch_tx_prep(tx->txs, tx->offsets, tx->tx_size, n, tx->records, rec, &ctr->fb_count, fb_list,
+                           g_lat_bits.load(), stream);
+    pk = tx->records;
+    sig = tx->records + 32;
+    msg = tx->records + 96;
+    pk_stride = sig_stride = msg_stride = 128;
+  } else if (e == hipSuccess) {
     hipLaunchKernelGGL((hsv::hsv_prep_kernel<WA>), dim3(blocks_needed), dim3(hsv::kBlock), 0, stream, pk, pk_stride,
                        sig, sig_stride, msg, msg_stride, n, rec, ctr, fb_list, g_lat_bits.load());
     e = hipGetLastError();
@@ -1133,6 +1152,23 @@ extern "C" hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t
 #undef HSV_LAUNCH
   return hipGetLastError();
 #endif
+}
+
+extern "C" hipError_t hsv_launch_verify_tx(int variant, const uint8_t *txs, const uint64_t *offsets,
+                                           uint64_t tx_size, uint32_t n, uint8_t *records, uint8_t *flags_out,
+                                           uint32_t *strict_bits, const uint32_t *comb_b, uint32_t *fault,
+                                           hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  if ((variant == 19 || variant == 21) && n > kPairMax) {
+    if (!comb_b || !fault) return hipErrorInvalidValue;
+    const TxPrep tx{txs, offsets, tx_size, records};
+    return launch_hp<4, HSV_HP_WAVES, 16>(nullptr, 0, nullptr, 0, nullptr, 0, n, flags_out, strict_bits, comb_b,
+                                          fault, stream, &tx);
+  }
+  hipError_t e = hsv_launch_tx_records(txs, offsets, tx_size, n, records, stream);
+  if (e != hipSuccess) return e;
+  return hsv_launch_verify(variant, records, 128, records + 32, 128, records + 96, 128, n, flags_out, strict_bits,
+                           comb_b, fault, stream);
 }
 
 // Variant ids compiled into this library.  The product build carries the

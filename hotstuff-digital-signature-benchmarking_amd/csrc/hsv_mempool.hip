@@ -17,6 +17,7 @@
 
 #include "hsv_internal.h"
 #include "hsv_txhash.hpp"
+#include "hsv_verify_hc.hpp"
 
 namespace hsv {
 
@@ -83,10 +84,20 @@ __device__ __forceinline__ void tx_stage_chunks(const uint4 *__restrict__ q, uin
 
 // One lane per transaction; the wave's loads are cooperative (tx_stage_chunks).
 // Waves are independent: each loops over its own longest message.
+// PREP (large batches, hsv_launch_tx_prep): the same lane then runs the scalar
+// prepass of the generic point pass on the record it holds in registers
+// (SHA-512(R || A || digest), k mod l, lattice reduction, recoding;
+// prep_scalars, hsv_verify_hc.hpp) and writes its SoA record, so a
+// transaction's bytes are read once and no separate prepass reads the
+// records back (round-2 VERDICT item 8).
+template <bool PREP>
 __global__ void __launch_bounds__(kTxBlock) hsv_tx_record_kernel(const uint8_t *__restrict__ txs,
                                                                   const uint64_t *__restrict__ offsets,
                                                                   uint64_t tx_size, uint32_t n,
-                                                                  uint4 *__restrict__ rec) {
+                                                                  uint4 *__restrict__ rec,
+                                                                  uint32_t *__restrict__ prep,
+                                                                  uint32_t *__restrict__ fb_count,
+                                                                  uint32_t *__restrict__ fb_list, int lat_bits) {
   __shared__ uint4 stage_all[kTxWaves][64 * kTxQ];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   if (blockIdx.x * kTxBlock + wv * 64u >= n) return;  // whole wave past the end
@@ -134,6 +145,10 @@ __global__ void __launch_bounds__(kTxBlock) hsv_tx_record_kernel(const uint8_t *
   uint4 *out = rec + (size_t)i * 8;
   HSV_UNROLL
   for (int j = 0; j < 8; ++j) out[j] = make_uint4(r[4 * j], r[4 * j + 1], r[4 * j + 2], r[4 * j + 3]);
+  if constexpr (PREP) {
+    // pk = r[0..8), R || s = r[8..24), digest = r[24..32)
+    if (prep_scalars<4>(r, r + 8, r + 24, prep + i, n, lat_bits)) fb_list[atomicAdd(fb_count, 1u)] = i;
+  }
 }
 
 // Zero the flags (and the STRICT_OK bit) of transactions shorter than 96 bytes.
@@ -153,8 +168,18 @@ extern "C" hipError_t hsv_launch_tx_records(const uint8_t *txs, const uint64_t *
                                             uint32_t n, uint8_t *records, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const uint32_t grid = (n + hsv::kTxBlock - 1) / hsv::kTxBlock;
-  hipLaunchKernelGGL(hsv::hsv_tx_record_kernel, dim3(grid), dim3(hsv::kTxBlock), 0, stream, txs, offsets, tx_size,
-                     n, reinterpret_cast<uint4 *>(records));
+  hipLaunchKernelGGL((hsv::hsv_tx_record_kernel<false>), dim3(grid), dim3(hsv::kTxBlock), 0, stream, txs, offsets,
+                     tx_size, n, reinterpret_cast<uint4 *>(records), nullptr, nullptr, nullptr, 0);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t hsv_launch_tx_prep(const uint8_t *txs, const uint64_t *offsets, uint64_t tx_size, uint32_t n,
+                                         uint8_t *records, uint32_t *prep, uint32_t *fb_count, uint32_t *fb_list,
+                                         int lat_bits, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const uint32_t grid = (n + hsv::kTxBlock - 1) / hsv::kTxBlock;
+  hipLaunchKernelGGL((hsv::hsv_tx_record_kernel<true>), dim3(grid), dim3(hsv::kTxBlock), 0, stream, txs, offsets,
+                     tx_size, n, reinterpret_cast<uint4 *>(records), prep, fb_count, fb_list, lat_bits);
   return hipGetLastError();
 }
 

@@ -24,11 +24,9 @@ constexpr size_t kTxChunkBytes = size_t(1) << 29;  // transaction bytes staged p
 // transactions already in HBM (d_offsets relative to d_txs, or NULL = fixed size)
 int tx_enqueue(int v, const uint32_t *comb_b, const uint8_t *d_txs, const uint64_t *d_offsets, size_t tx_size,
                size_t m, uint8_t *d_rec, uint8_t *d_flags, uint32_t *d_bits, uint32_t *d_fault, hipStream_t s) {
-  hipError_t e = hsv_launch_tx_records(d_txs, d_offsets, tx_size, (uint32_t)m, d_rec, s);
-  if (e != hipSuccess) return hip_fail("transaction record kernel launch", e);
-  e = hsv_launch_verify(v, d_rec, 128, d_rec + 32, 128, d_rec + 96, 128, (uint32_t)m, d_flags, d_bits, comb_b,
-                        d_fault, s);
-  if (e != hipSuccess) return hip_fail("verify kernel launch", e);
+  hipError_t e = hsv_launch_verify_tx(v, d_txs, d_offsets, tx_size, (uint32_t)m, d_rec, d_flags, d_bits, comb_b,
+                                      d_fault, s);
+  if (e != hipSuccess) return hip_fail("transaction verify launch", e);
   e = hsv_launch_tx_mask(d_offsets, (uint32_t)m, d_flags, d_bits, s);
   if (e != hipSuccess) return hip_fail("transaction mask kernel launch", e);
   return HSV_OK;

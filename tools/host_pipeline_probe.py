@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""Where the host-buffer path (hsv_verify from numpy, PCIe-inclusive) loses
+time against the HBM-resident launch, at 2^20 triples:
+
+  device  the same 2^20 items as device-resident launches of CHUNK items
+          alternating over two streams (the GPU-side cost of chunking alone);
+  host    hsv_verify from host arrays, one fresh process per setting of
+          HSV_PIPE_CHUNK_LOG2 / HSV_PACK_THREADS (read once per process),
+          with the library's own pack time and the call's wall time.
+
+python tools/host_pipeline_probe.py [--rounds 3]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "hotstuff-digital-signature-benchmarking_amd"))
+CACHE = "/tmp/hsv_host_pipe_c4.npz"
+N = 1 << 20
+
+
+def workload():
+    if os.path.exists(CACHE):
+        z = np.load(CACHE)
+        return z["pk"], z["sig"], z["msg"]
+    from hsverify import synth
+    w = synth.independent_triples(N, seed=0xC4 * 1000, corrupt_frac=0.05, nthreads=16)
+    np.savez(CACHE, pk=w.pk, sig=w.sig, msg=w.msg)
+    return w.pk, w.sig, w.msg
+
+
+def child(rounds):
+    from hsverify import _testing, verifier
+    pk, sig, msg = workload()
+    verifier.verify_flags(pk, sig, msg)
+    res = []
+    for _ in range(rounds * 3):
+        t0 = time.perf_counter()
+        verifier.verify_flags(pk, sig, msg)
+        res.append(((time.perf_counter() - t0) * 1e3, _testing.host_call_stats()["pack_ms"]))
+    res.sort()
+    ms, pack = res[len(res) // 2]
+    print(json.dumps({"ms": ms, "pack_ms": pack, "verif_per_s": N / (ms * 1e-3)}))
+
+
+def device_chunks(rounds):
+    import torch
+    from hsverify import verifier
+    pk, sig, msg = workload()
+    dev = torch.device("cuda", 0)
+    tp, ts, tm = (torch.from_numpy(x).to(dev) for x in (pk, sig, msg))
+    flags = torch.zeros(N, dtype=torch.uint8, device=dev)
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    out = {}
+    for lg in (15, 16, 17, 18, 19, 20):
+        c = 1 << lg
+
+        def run():
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            for k, base in enumerate(range(0, N, c)):
+                verifier.verify_device(tp[base:base + c], ts[base:base + c], tm[base:base + c], flags[base:base + c],
+                                       stream=streams[k & 1].cuda_stream)
+            torch.cuda.synchronize(dev)
+            return (time.perf_counter() - t) * 1e3
+
+        run()
+        out[f"2^{lg}"] = sorted(run() for _ in range(rounds * 3))[rounds * 3 // 2]
+    print(json.dumps({"device_chunked_ms_per_2^20": out}), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--child", action="store_true")
+    a = ap.parse_args()
+    if a.child:
+        return child(a.rounds)
+    workload()
+    device_chunks(a.rounds)
+    for lg in (16, 17, 18):
+        for th in (6, 12):
+            env = dict(os.environ, HSV_PIPE_CHUNK_LOG2=str(lg), HSV_PACK_THREADS=str(th))
+            r = subprocess.run([sys.executable, __file__, "--child", "--rounds", str(a.rounds)], env=env,
+                               capture_output=True, text=True, timeout=300)
+            line = r.stdout.strip().splitlines()[-1] if r.returncode == 0 else f"rc={r.returncode} {r.stderr[-300:]}"
+            print(json.dumps({"chunk_log2": lg, "pack_threads": th, "result": line}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
