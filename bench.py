@@ -171,6 +171,13 @@ def cpu_baseline(w, gpu_flags, sample):
     fb = lib.oracle_verify_many_batch64(pk.ctypes.data, sig.ctypes.data, msg.ctypes.data, m, out64.ctypes.data,
                                         threads)
     dt64 = time.perf_counter() - t0
+    # dalek's verify_batch draws random z_i: a chunk whose only failures are
+    # pure torsion terms (a mixed-order key with k != 0 mod 8) is accepted with
+    # some probability, so its items then read as accepted.  Any
+    # other disagreement would be a bug; report which kinds disagree.
+    miss = np.nonzero((out64 & 1) != (gpu_flags[:m] & 1))[0]
+    from hsverify import synth
+    miss_kinds = sorted({synth.CORRUPTIONS[k] if k >= 0 else "honest" for k in w.kind[miss]})
     return {
         "value": m / dt, "unit": "verif/s", "cores": threads, "kind": "port",
         "sample": f"first {m} triples of the same C4 workload (5 % corrupted); oracle/ed25519_oracle.c "
@@ -183,7 +190,11 @@ def cpu_baseline(w, gpu_flags, sample):
                     "algorithm": "dalek verify_batch (random linear combination, Straus MSM) over chunks of 64, "
                                  "verify_strict per item for the chunks that fail",
                     "failed_chunks": int(fb), "chunks": (m + 63) // 64,
-                    "strict_ok_parity_vs_gpu": bool(((out64 & 1) == (gpu_flags[:m] & 1)).all())},
+                    "strict_ok_parity_vs_gpu": bool(miss.size == 0),
+                    "strict_ok_mismatches": int(miss.size), "mismatch_kinds": miss_kinds,
+                    "mismatch_note": "dalek verify_batch is randomised when a chunk's only failures are pure "
+                                     "torsion (mixed-order key, k != 0 mod 8): such chunks may pass; the "
+                                     "per-signature vector is verify_strict's (SURVEY A.2)"},
     }
 
 
