@@ -189,6 +189,16 @@ int slot_stream2(Slot &s) {
   return e == hipSuccess ? HSV_OK : hip_fail("hipStreamCreate", e);
 }
 
+int slot_pipeline(Slot &s) {
+  int rc = slot_stream2(s);
+  if (rc != HSV_OK) return rc;
+  hipError_t e = hipSuccess;
+  if (!s.copy) e = hipStreamCreateWithFlags(&s.copy, hipStreamNonBlocking);
+  for (int i = 0; i < 4 && e == hipSuccess; ++i)
+    if (!s.ev[i]) e = hipEventCreateWithFlags(&s.ev[i], hipEventDisableTiming);
+  return e == hipSuccess ? HSV_OK : hip_fail("creating the pipeline streams and events", e);
+}
+
 namespace {
 
 const uint8_t kBasepointEncoding[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
@@ -463,9 +473,140 @@ size_t pipe_chunk() {  // HSV_PIPE_CHUNK_LOG2 (14..22): measurement switch
 // copied host-to-device, and the call's wall time.
 thread_local double t_pack_ms = 0, t_call_ms = 0;
 thread_local uint64_t t_h2d_bytes = 0;
+// per-chunk host timestamps of the last pipelined call (ms from its start):
+// waited for the staging buffer, packed, copies enqueued, launch enqueued
+thread_local std::vector<double> t_chunk_marks;
 
 double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// Large host batches (n >= 2 pipe_chunk(), n <= kChunk): the inputs stream
+// to HBM chunk by chunk while earlier chunks verify.
+//   * HBM holds the whole batch (pk | sig | msg | flags | self-check words):
+//     a device region is never reused within the call, so a chunk's launch
+//     depends only on its own copy;
+//   * two pinned staging buffers alternate on the host: chunk c is packed
+//     while chunk c-1 copies, and a staging buffer is reused as soon as its
+//     copy is done (event), not when its chunk's kernels are;
+//   * copies run on the slot's copy stream, launches alternate over two
+//     compute streams (a chunk's launch starts in the previous one's grid
+//     end), each waiting for its chunk's copy by event;
+//   * chunk sizes ramp up (p/4, p/2, then p = pipe_chunk()): the first launch
+//     waits for a quarter chunk's pack and copy, not a whole one;
+//   * one copy back of all flags and the self-check words at the end.
+// The host's work (pack + enqueue) runs ahead of the GPU: the call takes the
+// GPU's time for the batch plus the first small chunk and the final copy back
+// (profiles/r03c_timeline.txt shows the two-buffer form it replaces, where
+// each chunk's pack waited for the chunk two back to finish verifying).
+int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, size_t pk_stride, const uint8_t *sig,
+                  size_t sig_stride, const uint8_t *msg, size_t msg_stride, size_t n, uint8_t *flags_out) {
+  const size_t pchunk = pipe_chunk();
+  // HBM: pk n*32 | sig n*64 | msg n*32 (or 32) | flags n | self-check words
+  const size_t d_sig = round_up(n * 32, kAlign);
+  const size_t d_msg = d_sig + round_up(n * 64, kAlign);
+  const size_t d_flag = d_msg + round_up(msg_stride ? n * 32 : 32, kAlign);
+  const size_t d_fault = d_flag + round_up(n, kAlign);
+  const size_t d_total = d_fault + kAlign;
+  // host: two staging buffers of one chunk (pk | sig | msg) | flags n | self-check words
+  const size_t h_stage = round_up(pchunk * 128, kAlign);
+  const size_t h_flag = 2 * h_stage;
+  const size_t h_fault = h_flag + round_up(n, kAlign);
+  const size_t h_total = h_fault + kAlign;
+  int rc = slot_prepare(s, d_total, h_total);
+  if (rc == HSV_OK) rc = slot_pipeline(s);
+  if (rc != HSV_OK) return rc;
+  // one launch workspace per compute stream, kept by the slot: no allocation
+  // inside the loop (a pool allocation per launch made the enqueue of each
+  // chunk wait ~1 ms for an earlier chunk, tools/host_api_probe.py marks)
+  const size_t ws_need = hsv_launch_ws_bytes(v, (uint32_t)pchunk);
+  if (ws_need > s.ws_cap) {
+    for (uint8_t *&w : s.d_ws) {
+      if (w) (void)hipFree(w);
+      w = nullptr;
+    }
+    s.ws_cap = 0;
+    for (uint8_t *&w : s.d_ws) {
+      const hipError_t ea = hipMalloc(&w, ws_need);
+      if (ea != hipSuccess) return hip_fail("allocating the pipeline workspaces", ea);
+    }
+    s.ws_cap = ws_need;
+  }
+  hipStream_t comp[2] = {s.stream, s.stream2};
+  hipEvent_t staged[2] = {s.ev[0], s.ev[1]};
+  auto drain = [&](int code) -> int {
+    (void)hipStreamSynchronize(s.copy);
+    (void)hipStreamSynchronize(s.stream);
+    (void)hipStreamSynchronize(s.stream2);
+    return code;
+  };
+  uint8_t *d = s.d_buf;
+  // flags and self-check words start at zero (unwritten flags read as
+  // rejections); ordered before every launch through the staged events
+  hipError_t e = hipMemsetAsync(d + d_flag, 0, d_total - d_flag, s.copy);
+  if (e == hipSuccess && msg_stride == 0) e = hipMemcpyAsync(d + d_msg, msg, 32, hipMemcpyHostToDevice, s.copy);
+  if (e != hipSuccess) return drain(hip_fail("hipMemsetAsync", e));
+  bool used[2] = {false, false};
+  size_t base = 0;
+  const auto t_start = std::chrono::steady_clock::now();
+  t_chunk_marks.clear();
+  for (int k = 0; base < n; ++k) {
+    const size_t want = k == 0 ? pchunk / 4 : k == 1 ? pchunk / 2 : pchunk;
+    const size_t m = std::min(want, n - base);
+    const int b = k & 1;
+    uint8_t *h = s.h_buf + (size_t)b * h_stage;
+    if (used[b]) {  // the copy that last read this staging buffer has finished
+      e = hipEventSynchronize(staged[b]);
+      if (e != hipSuccess) return drain(hip_fail("hipEventSynchronize", e));
+    }
+    t_chunk_marks.push_back(ms_since(t_start));
+    const auto t_pack = std::chrono::steady_clock::now();
+    uint8_t *hpk = h, *hsig = h + m * 32, *hmsg = h + m * 96;
+    const int nparts = (int)std::min<size_t>(64, (m * 128 + kPackPart - 1) / kPackPart);
+    auto part = [&](int p) {
+      const size_t lo = m * p / nparts, hi = m * (p + 1) / nparts;
+      if (pk_stride == 32) std::memcpy(hpk + 32 * lo, pk + (base + lo) * 32, (hi - lo) * 32);
+      else for (size_t i = lo; i < hi; ++i) std::memcpy(hpk + 32 * i, pk + (base + i) * pk_stride, 32);
+      if (sig_stride == 64) std::memcpy(hsig + 64 * lo, sig + (base + lo) * 64, (hi - lo) * 64);
+      else for (size_t i = lo; i < hi; ++i) std::memcpy(hsig + 64 * i, sig + (base + i) * sig_stride, 64);
+      if (msg_stride == 32) std::memcpy(hmsg + 32 * lo, msg + (base + lo) * 32, (hi - lo) * 32);
+      else if (msg_stride != 0)
+        for (size_t i = lo; i < hi; ++i) std::memcpy(hmsg + 32 * i, msg + (base + i) * msg_stride, 32);
+    };
+    if (nparts < 2) part(0);
+    else PackPool::get().run(nparts, part);
+    t_pack_ms += ms_since(t_pack);
+    t_chunk_marks.push_back(ms_since(t_start));
+    e = hipMemcpyAsync(d + base * 32, hpk, m * 32, hipMemcpyHostToDevice, s.copy);
+    if (e == hipSuccess) e = hipMemcpyAsync(d + d_sig + base * 64, hsig, m * 64, hipMemcpyHostToDevice, s.copy);
+    if (e == hipSuccess && msg_stride)
+      e = hipMemcpyAsync(d + d_msg + base * 32, hmsg, m * 32, hipMemcpyHostToDevice, s.copy);
+    if (e == hipSuccess) e = hipEventRecord(staged[b], s.copy);
+    if (e == hipSuccess) e = hipStreamWaitEvent(comp[b], staged[b], 0);
+    if (e != hipSuccess) return drain(hip_fail("staging a chunk", e));
+    used[b] = true;
+    t_chunk_marks.push_back(ms_since(t_start));
+    t_h2d_bytes += m * (msg_stride ? 128 : 96);
+    e = hsv_launch_verify_ws(v, d + base * 32, 32, d + d_sig + base * 64, 64,
+                             d + d_msg + (msg_stride ? base * 32 : 0), msg_stride ? 32 : 0, (uint32_t)m,
+                             d + d_flag + base, nullptr, comb_b, reinterpret_cast<uint32_t *>(d + d_fault),
+                             s.d_ws[b], s.ws_cap, comp[b]);
+    if (e != hipSuccess) return drain(hip_fail("verify kernel launch", e));
+    t_chunk_marks.push_back(ms_since(t_start));
+    base += m;
+  }
+  // join: the flags come back once both compute streams are done
+  e = hipEventRecord(s.ev[3], s.stream2);
+  if (e == hipSuccess) e = hipStreamWaitEvent(s.stream, s.ev[3], 0);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(s.h_buf + h_flag, d + d_flag, d_total - d_flag, hipMemcpyDeviceToHost, s.stream);
+  if (e != hipSuccess) return drain(hip_fail("hipMemcpyAsync D2H", e));
+  e = hipStreamSynchronize(s.stream);
+  if (e != hipSuccess) return drain(hip_fail("hipStreamSynchronize", e));
+  const int frc = check_faults(s.h_buf + h_fault, "verify");
+  if (frc != HSV_OK) return drain(frc);
+  std::memcpy(flags_out, s.h_buf + h_flag, n);
+  return HSV_OK;
 }
 
 int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t *sig, size_t sig_stride,
@@ -484,11 +625,20 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
   SlotLease lease(c);
   Slot &s = lease.slot();
   const size_t pchunk = pipe_chunk();
-  const bool pipe = !no_pipe && n >= 2 * pchunk;
-  const size_t chunk = pipe ? pchunk : std::min(n, kChunk);
-  const int nbuf = pipe ? 2 : 1;
-  // staging layout of one buffer: pk 32 | sig 64 | msg 32 (or one shared
-  // digest) | flags 1 | self-check words (kFaultBytes); the same in HBM
+  if (!no_pipe && n >= 2 * pchunk) {
+    for (size_t base = 0; base < n; base += kChunk) {
+      const size_t m = std::min(kChunk, n - base);
+      rc = run_pipelined(s, v, comb_b, pk + base * pk_stride, pk_stride, sig + base * sig_stride, sig_stride,
+                         msg + base * msg_stride, msg_stride, m, flags_out + base);
+      if (rc != HSV_OK) return rc;
+    }
+    t_call_ms = ms_since(t_call);
+    return HSV_OK;
+  }
+  // below the pipeline's size (or with HSV_NO_PIPELINE): one staging buffer,
+  // chunk by chunk -- pk 32 | sig 64 | msg 32 (or one shared digest) | flags 1
+  // | self-check words (kFaultBytes); the same layout in HBM
+  const size_t chunk = std::min(n, kChunk);
   const size_t pk_off = 0;
   const size_t sig_off = round_up(chunk * 32, kAlign);
   const size_t msg_off = sig_off + round_up(chunk * 64, kAlign);
@@ -496,35 +646,16 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
   const size_t flag_off = msg_off + round_up(msg_bytes, kAlign);
   const size_t fault_off = flag_off + round_up(chunk, kAlign);
   const size_t total = fault_off + kAlign;
-  rc = slot_prepare(s, total * nbuf, total * nbuf);
-  if (rc == HSV_OK && pipe) rc = slot_stream2(s);
+  rc = slot_prepare(s, total, total);
   if (rc != HSV_OK) return rc;
-  size_t pend_base[2] = {0, 0}, pend_m[2] = {0, 0};
-  // an error leaves no copy or kernel of this call in flight on the slot
-  auto drain = [&](int code) -> int {
-    if (s.stream) (void)hipStreamSynchronize(s.stream);
-    if (s.stream2) (void)hipStreamSynchronize(s.stream2);
-    return code;
-  };
-  // wait for buffer b's chunk, check its self-check words, hand its flags over
-  auto retire = [&](int b) -> int {
-    if (pend_m[b] == 0) return HSV_OK;
-    const hipError_t e = hipStreamSynchronize(b ? s.stream2 : s.stream);
-    if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
-    const uint8_t *h = s.h_buf + (size_t)b * total;
-    const int frc = check_faults(h + fault_off, "verify");
-    if (frc != HSV_OK) return frc;
-    std::memcpy(flags_out + pend_base[b], h + flag_off, pend_m[b]);
-    pend_m[b] = 0;
-    return HSV_OK;
-  };
-  // pack items [base + lo, base + hi) of a chunk into the dense layout the
-  // kernels read, split over the pack pool by item range
-  auto pack_range = [&](uint8_t *h, size_t base, size_t lo0, size_t hi0) {
-    const size_t m = hi0 - lo0;
+  uint8_t *h = s.h_buf, *d = s.d_buf;
+  hipStream_t st = s.stream;
+  for (size_t base = 0; base < n; base += chunk) {
+    const size_t m = std::min(chunk, n - base);
+    const auto t_pack = std::chrono::steady_clock::now();
     const int nparts = (int)std::min<size_t>(64, (m * 128 + kPackPart - 1) / kPackPart);
     auto part = [&](int p) {
-      const size_t lo = lo0 + m * p / nparts, hi = lo0 + m * (p + 1) / nparts;
+      const size_t lo = m * p / nparts, hi = m * (p + 1) / nparts;
       if (pk_stride == 32) std::memcpy(h + pk_off + 32 * lo, pk + (base + lo) * 32, (hi - lo) * 32);
       else for (size_t i = lo; i < hi; ++i) std::memcpy(h + pk_off + 32 * i, pk + (base + i) * pk_stride, 32);
       if (sig_stride == 64) std::memcpy(h + sig_off + 64 * lo, sig + (base + lo) * 64, (hi - lo) * 64);
@@ -535,88 +666,39 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
     };
     if (nparts < 2) part(0);
     else PackPool::get().run(nparts, part);
-  };
-  // the rest of a chunk's staging: the shared digest, and zeroed flags (a flag
-  // the kernels failed to write reads as a rejection, never as an earlier
-  // call's verdict) and self-check words
-  auto pack_tail = [&](uint8_t *h, size_t m) {
     if (msg_stride == 0) std::memcpy(h + msg_off, msg, 32);
+    // a flag the kernels failed to write reads as a rejection, never as an
+    // earlier call's verdict; the self-check words start at zero
     std::memset(h + flag_off, 0, m);
     std::memset(h + fault_off, 0, kFaultBytes);
-  };
-  int b = 0;
-  for (size_t base = 0; base < n; base += chunk, b = (b + 1) % nbuf) {
-    const size_t m = std::min(chunk, n - base);
-    rc = retire(b);
-    if (rc != HSV_OK) return drain(rc);
-    hipStream_t st = b ? s.stream2 : s.stream;
-    uint8_t *h = s.h_buf + (size_t)b * total;
-    uint8_t *d = s.d_buf + (size_t)b * total;
-    const auto t_pack = std::chrono::steady_clock::now();
-    if (pipe && base == 0) {
-      // nothing hides the first chunk's pack and copy: copy it in slices, each
-      // as soon as it is packed, so the DMA engine runs beside the packing
-      constexpr size_t kSlices = 4;
-      for (size_t q = 0; q < kSlices; ++q) {
-        const size_t lo = m * q / kSlices, hi = m * (q + 1) / kSlices;
-        pack_range(h, base, lo, hi);
-        hipError_t e = hipMemcpyAsync(d + pk_off + 32 * lo, h + pk_off + 32 * lo, 32 * (hi - lo),
-                                      hipMemcpyHostToDevice, st);
-        if (e == hipSuccess)
-          e = hipMemcpyAsync(d + sig_off + 64 * lo, h + sig_off + 64 * lo, 64 * (hi - lo), hipMemcpyHostToDevice, st);
-        if (e == hipSuccess && msg_stride)
-          e = hipMemcpyAsync(d + msg_off + 32 * lo, h + msg_off + 32 * lo, 32 * (hi - lo), hipMemcpyHostToDevice, st);
-        if (e != hipSuccess) return drain(hip_fail("hipMemcpyAsync H2D", e));
-      }
-      pack_tail(h, m);
-      const size_t tail_from = msg_stride ? flag_off : msg_off;
-      hipError_t e = hipMemcpyAsync(d + tail_from, h + tail_from, fault_off + kFaultBytes - tail_from,
-                                    hipMemcpyHostToDevice, st);
-      if (e != hipSuccess) return drain(hip_fail("hipMemcpyAsync H2D", e));
-      t_pack_ms += ms_since(t_pack);
-      t_h2d_bytes += fault_off + kFaultBytes;
-      e = hsv_launch_verify(v, d + pk_off, 32, d + sig_off, 64, d + msg_off, msg_stride ? 32 : 0, (uint32_t)m,
-                            d + flag_off, nullptr, comb_b, reinterpret_cast<uint32_t *>(d + fault_off), st);
-      if (e != hipSuccess) return drain(hip_fail("verify kernel launch", e));
-      e = hipMemcpyAsync(h + flag_off, d + flag_off, fault_off + kFaultBytes - flag_off, hipMemcpyDeviceToHost, st);
-      if (e != hipSuccess) return drain(hip_fail("hipMemcpyAsync D2H", e));
-      pend_base[b] = base;
-      pend_m[b] = m;
-      continue;
-    }
-    pack_range(h, base, 0, m);
-    pack_tail(h, m);
     t_pack_ms += ms_since(t_pack);
-    // small batches (a QC of non-cached keys, a single vote): the kernels read
-    // the pinned staging buffer and write the flags through its device
-    // mapping, so no copy launches sit on the latency path
+    hipError_t e;
     void *hd = nullptr;
     if (!no_zero_copy && n <= kZeroCopyMax && hipHostGetDevicePointer(&hd, h, 0) == hipSuccess && hd) {
+      // small batches (a QC of non-cached keys, a single vote): the kernels read
+      // the pinned staging buffer and write the flags through its device
+      // mapping, so no copy launches sit on the latency path
       uint8_t *dh = static_cast<uint8_t *>(hd);
-      hipError_t e = hsv_launch_verify(v, dh + pk_off, 32, dh + sig_off, 64, dh + msg_off, msg_stride ? 32 : 0,
-                                       (uint32_t)m, dh + flag_off, nullptr, comb_b,
-                                       reinterpret_cast<uint32_t *>(dh + fault_off), st);
-      if (e != hipSuccess) return drain(hip_fail("verify kernel launch", e));
-      pend_base[b] = base;
-      pend_m[b] = m;
-      continue;
+      e = hsv_launch_verify(v, dh + pk_off, 32, dh + sig_off, 64, dh + msg_off, msg_stride ? 32 : 0, (uint32_t)m,
+                            dh + flag_off, nullptr, comb_b, reinterpret_cast<uint32_t *>(dh + fault_off), st);
+    } else {
+      // inputs, the zeroed flags and the zeroed self-check words in one copy
+      const size_t in_bytes = fault_off + kFaultBytes;
+      e = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, st);
+      t_h2d_bytes += in_bytes;
+      if (e == hipSuccess)
+        e = hsv_launch_verify(v, d + pk_off, 32, d + sig_off, 64, d + msg_off, msg_stride ? 32 : 0, (uint32_t)m,
+                              d + flag_off, nullptr, comb_b, reinterpret_cast<uint32_t *>(d + fault_off), st);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(h + flag_off, d + flag_off, fault_off + kFaultBytes - flag_off, hipMemcpyDeviceToHost,
+                           st);
     }
-    // inputs, the zeroed flags and the zeroed self-check words in one copy
-    const size_t in_bytes = fault_off + kFaultBytes;
-    hipError_t e = hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, st);
-    if (e != hipSuccess) return drain(hip_fail("hipMemcpyAsync H2D", e));
-    t_h2d_bytes += in_bytes;
-    e = hsv_launch_verify(v, d + pk_off, 32, d + sig_off, 64, d + msg_off, msg_stride ? 32 : 0, (uint32_t)m,
-                          d + flag_off, nullptr, comb_b, reinterpret_cast<uint32_t *>(d + fault_off), st);
-    if (e != hipSuccess) return drain(hip_fail("verify kernel launch", e));
-    e = hipMemcpyAsync(h + flag_off, d + flag_off, fault_off + kFaultBytes - flag_off, hipMemcpyDeviceToHost, st);
-    if (e != hipSuccess) return drain(hip_fail("hipMemcpyAsync D2H", e));
-    pend_base[b] = base;
-    pend_m[b] = m;
-  }
-  for (int k = 0; k < nbuf; ++k) {
-    rc = retire(k);
-    if (rc != HSV_OK) return drain(rc);
+    const hipError_t es = hipStreamSynchronize(st);  // nothing of this call stays in flight
+    if (e != hipSuccess) return hip_fail("verify launch", e);
+    if (es != hipSuccess) return hip_fail("hipStreamSynchronize", es);
+    rc = check_faults(h + fault_off, "verify");
+    if (rc != HSV_OK) return rc;
+    std::memcpy(flags_out + base, h + flag_off, m);
   }
   t_call_ms = ms_since(t_call);
   return HSV_OK;
@@ -705,6 +787,7 @@ void hsv_shutdown(void) {
     for (auto &sp : c->slots) {
       if (sp->stream) (void)hipStreamSynchronize(sp->stream);
       if (sp->stream2) (void)hipStreamSynchronize(sp->stream2);
+      if (sp->copy) (void)hipStreamSynchronize(sp->copy);
     }
     for (hipStream_t st : c->side_all) (void)hipStreamSynchronize(st);
     (void)hipDeviceSynchronize();
@@ -721,6 +804,17 @@ void hsv_shutdown(void) {
       Slot &s = *sp;
       if (s.stream) (void)hipStreamDestroy(s.stream);
       if (s.stream2) (void)hipStreamDestroy(s.stream2);
+      if (s.copy) (void)hipStreamDestroy(s.copy);
+      for (hipEvent_t &ev : s.ev) {
+        if (ev) (void)hipEventDestroy(ev);
+        ev = nullptr;
+      }
+      s.copy = nullptr;
+      for (uint8_t *&w : s.d_ws) {
+        if (w) (void)hipFree(w);
+        w = nullptr;
+      }
+      s.ws_cap = 0;
       if (s.d_buf) (void)hipFree(s.d_buf);
       if (s.h_buf) (void)hipHostFree(s.h_buf);
       s.stream = s.stream2 = nullptr;
@@ -886,6 +980,14 @@ void hsv_host_call_stats(double *pack_ms, double *h2d_bytes, double *call_ms) {
 }
 
 int hsv_pack_threads(void) { return PackPool::get().threads(); }
+
+// Measurement hook (not in hsv.h): the per-chunk host marks of the calling
+// thread's last pipelined call (4 per chunk, see t_chunk_marks); returns the count.
+int hsv_host_call_marks(double *out, int cap) {
+  const int n = (int)t_chunk_marks.size();
+  for (int i = 0; out && i < n && i < cap; ++i) out[i] = t_chunk_marks[i];
+  return n;
+}
 
 double hsv_measure_mad_peak(void) {
   if (ensure_init() != HSV_OK) return -1.0;

@@ -32,6 +32,15 @@ hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t pk_stride,
                              uint64_t sig_stride, const uint8_t *msg, uint64_t msg_stride,
                              uint32_t n, uint8_t *flags_out, uint32_t *strict_bits,
                              const uint32_t *comb_b, uint32_t *fault, hipStream_t stream);
+// The same launch with a caller-provided workspace (ws, ws_cap bytes; the
+// library pool is used when it is NULL or too small): a pipeline keeps one per
+// stream instead of allocating per launch.  hsv_launch_ws_bytes(variant, n):
+// the workspace a launch of n items needs (0 for variants without one).
+hipError_t hsv_launch_verify_ws(int variant, const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig,
+                                uint64_t sig_stride, const uint8_t *msg, uint64_t msg_stride, uint32_t n,
+                                uint8_t *flags_out, uint32_t *strict_bits, const uint32_t *comb_b, uint32_t *fault,
+                                void *ws, size_t ws_cap, hipStream_t stream);
+size_t hsv_launch_ws_bytes(int variant, uint32_t n);
 // fault injection mode of the next launches (tests only; hsv_kernels.hip)
 int hsv_test_inject_mode(void);
 // digit width of the B comb table a variant reads: 8 (hsv_comb_table_bytes),

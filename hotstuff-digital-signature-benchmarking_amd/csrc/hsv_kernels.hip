@@ -376,6 +376,11 @@ hsv_prep_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const uint8_
                 uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
                 uint32_t *__restrict__ rec, HcCounters *__restrict__ ctr, uint32_t *__restrict__ fb_list,
                 int lat_bits) {
+  // The prepass usually runs beside the previous batch's point pass (another
+  // stream, or the previous chunk of a host pipeline), whose waves keep every
+  // SIMD's VALU busy; this batch's point pass cannot start before the prepass
+  // ends.  Highest wave priority: the SIMD issues the prepass's waves first.
+  __builtin_amdgcn_s_setprio(3);
   const uint32_t idx = blockIdx.x * kBlock + threadIdx.x;
   if (idx >= n) return;
   uint32_t pkw[8], sigw[16], msgw[8];
@@ -871,6 +876,13 @@ extern "C" hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream) 
       uint64_t keep = UINT64_MAX;
       e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
       if (e != hipSuccess) return e;
+      // A block freed by a launch still running on another stream is never
+      // handed out by making the new launch wait for that stream: launches on
+      // different streams (consecutive batches, pipelined chunks) must be
+      // free to overlap.  Blocks whose free has completed are reused.
+      int no = 0;
+      e = hipMemPoolSetAttribute(pool, hipMemPoolReuseAllowInternalDependencies, &no);
+      if (e != hipSuccess) return e;
       it = pools.emplace(dev, pool).first;
     }
     pool = it->second;
@@ -979,7 +991,8 @@ template <int WA, int WAVES, int CB, bool TAIL = false>
 hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
                      const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
                      uint32_t *strict_bits, const uint32_t *comb_b, uint32_t *fault, hipStream_t stream,
-                     const TxPrep *tx = nullptr) {
+                     const TxPrep *tx = nullptr, void *ws_in = nullptr, size_t ws_cap = 0,
+                     size_t *ws_need = nullptr) {
   const void *kern = reinterpret_cast<const void *>(hsv::hsv_verify_hp_kernel<WA, WAVES, CB>);
 #if HSV_ALL_VARIANTS
   if constexpr (TAIL) kern = reinterpret_cast<const void *>(hsv::hsv_verify_hpt_kernel<WA, WAVES, CB>);
@@ -1011,8 +1024,16 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
   const size_t canary_bytes = ((size_t)grid * hsv::kBlock * sizeof(uint32_t) + 255) & ~(size_t)255;
   const size_t fb_bytes = (size_t)n * sizeof(uint32_t);
   const size_t rec_bytes = (size_t)n * hsv::kPrepWords * sizeof(uint32_t);
-  void *ws = nullptr;
-  e = hsv_ws_malloc(&ws, ws_bytes + 256 + canary_bytes + fb_bytes + rec_bytes, stream);
+  const size_t need = ws_bytes + 256 + canary_bytes + fb_bytes + rec_bytes;
+  if (ws_need) {  // size query only
+    *ws_need = need;
+    return hipSuccess;
+  }
+  // the caller's workspace when it is large enough (a pipeline that keeps one
+  // per stream), else one from the library pool, freed on the stream
+  void *ws = ws_in && ws_cap >= need ? ws_in : nullptr;
+  const bool own = ws == nullptr;
+  if (own) e = hsv_ws_malloc(&ws, need, stream);
   if (e != hipSuccess) return e;
   uint8_t *ws8 = static_cast<uint8_t *>(ws);
   uint4 *vt_ws = reinterpret_cast<uint4 *>(ws);
@@ -1053,7 +1074,7 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
     }
     e = hipGetLastError();
   }
-  const hipError_t ef = hipFreeAsync(ws, stream);
+  const hipError_t ef = own ? hipFreeAsync(ws, stream) : hipSuccess;
   return e != hipSuccess ? e : ef;
 }
 
@@ -1067,12 +1088,19 @@ constexpr uint32_t kPairMax = 1u << 13;
 template <int WA, int CB>
 hipError_t launch_pair(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
                        const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
-                       uint32_t *strict_bits, const uint32_t *comb_b, uint32_t *fault, hipStream_t stream) {
+                       uint32_t *strict_bits, const uint32_t *comb_b, uint32_t *fault, hipStream_t stream,
+                       void *ws_in = nullptr, size_t ws_cap = 0, size_t *ws_need = nullptr) {
   const uint32_t grid = (n + hsv::kFusedItems - 1) / hsv::kFusedItems;
   const size_t slots = (size_t)grid * 2u * hsv::kFusedItems;
   const size_t ws_bytes = slots * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
-  void *ws = nullptr;
-  hipError_t e = hsv_ws_malloc(&ws, ws_bytes + slots * sizeof(uint32_t), stream);
+  const size_t need = ws_bytes + slots * sizeof(uint32_t);
+  if (ws_need) {
+    *ws_need = need;
+    return hipSuccess;
+  }
+  void *ws = ws_in && ws_cap >= need ? ws_in : nullptr;
+  const bool own = ws == nullptr;
+  hipError_t e = own ? hsv_ws_malloc(&ws, need, stream) : hipSuccess;
   if (e != hipSuccess) return e;
   if (strict_bits) e = hipMemsetAsync(strict_bits, 0, (size_t)((n + 31u) / 32u) * 4u, stream);
   if (e == hipSuccess) {
@@ -1083,11 +1111,38 @@ hipError_t launch_pair(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig
                        g_inject.load(), fault);
     e = hipGetLastError();
   }
-  const hipError_t ef = hipFreeAsync(ws, stream);
+  const hipError_t ef = own ? hipFreeAsync(ws, stream) : hipSuccess;
   return e != hipSuccess ? e : ef;
 }
 
 }  // namespace
+
+extern "C" hipError_t hsv_launch_verify_ws(int variant, const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig,
+                                           uint64_t sig_stride, const uint8_t *msg, uint64_t msg_stride, uint32_t n,
+                                           uint8_t *flags_out, uint32_t *strict_bits, const uint32_t *comb_b,
+                                           uint32_t *fault, void *ws, size_t ws_cap, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  if (variant != 19 && variant != 21)
+    return hsv_launch_verify(variant, pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits,
+                             comb_b, fault, stream);
+  if (!comb_b || !fault) return hipErrorInvalidValue;
+  if (variant == 21 && n <= kPairMax)
+    return launch_pair<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b,
+                              fault, stream, ws, ws_cap);
+  return launch_hp<4, HSV_HP_WAVES, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits,
+                                        comb_b, fault, stream, nullptr, ws, ws_cap);
+}
+
+extern "C" size_t hsv_launch_ws_bytes(int variant, uint32_t n) {
+  size_t need = 0;
+  if (variant == 21 && n <= kPairMax)
+    (void)launch_pair<4, 16>(nullptr, 0, nullptr, 0, nullptr, 0, n, nullptr, nullptr, nullptr, nullptr, nullptr,
+                             nullptr, 0, &need);
+  else if (variant == 19 || variant == 21)
+    (void)launch_hp<4, HSV_HP_WAVES, 16>(nullptr, 0, nullptr, 0, nullptr, 0, n, nullptr, nullptr, nullptr, nullptr,
+                                         nullptr, nullptr, nullptr, 0, &need);
+  return need;
+}
 
 extern "C" hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t pk_stride,
                                         const uint8_t *sig, uint64_t sig_stride,

@@ -339,3 +339,38 @@ def test_host_api_pipelined_chunks_match_device_api(api, oracle_lib):
     assert (got[w.accept] & o.STRICT_OK).all() and not (got[~w.accept] & o.STRICT_OK).any()
     sample = np.sort(np.random.default_rng(3).choice(n, 4096, replace=False))
     assert (got[sample] == oracle_flags(oracle_lib, w.pk[sample], w.sig[sample], w.msg[sample])).all()
+
+
+def test_host_api_pipeline_shared_digest_and_packed_votes(api, oracle_lib):
+    """The streamed host pipeline (hsv_capi.cpp run_pipelined: ramped chunks,
+    whole batch in HBM, two compute streams) with one shared digest (a huge
+    QC) and with packed 96-byte votes (hsv_verify_batch_packed's strided
+    records): flags equal the device-resident launch and an oracle sample."""
+    import torch
+    _, verifier, synth = api
+    from hsverify import _lib
+    lib = _lib.load()
+    n = (1 << 18) + 777
+    seeds = synth.committee_seeds(n, 3)
+    digest = np.frombuffer(synth.qc_digest(bytes(32), 9), np.uint8).copy()
+    pk, sig = verifier.sign_many(seeds, np.repeat(digest[None], n, 0))
+    sig[5, 40] ^= 1                                   # one forged vote
+    got = verifier.verify_flags(pk, sig, digest)       # msg_stride 0, pipelined
+    dev = torch.device("cuda:0")
+    flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+    verifier.verify_device(torch.from_numpy(pk).to(dev), torch.from_numpy(sig).to(dev),
+                           torch.from_numpy(digest).to(dev), flags)
+    torch.cuda.synchronize()
+    assert (got == flags.cpu().numpy()).all()
+    assert not got[5] & o.STRICT_OK and (np.delete(got, 5) & o.STRICT_OK).all()
+    sample = np.unique(np.concatenate([[5], np.random.default_rng(4).choice(n, 2048, replace=False)]))
+    exp = oracle_flags(oracle_lib, pk[sample], sig[sample], np.repeat(digest[None], sample.size, 0))
+    assert (got[sample] == exp).all()
+    packed = np.concatenate([pk, sig], axis=1)
+    lib.hsv_set_auto_committee(0)
+    try:
+        assert lib.hsv_verify_batch_packed(digest.tobytes(), packed.tobytes(), n) == 0
+        packed[5, 32 + 40] ^= 1
+        assert lib.hsv_verify_batch_packed(digest.tobytes(), packed.tobytes(), n) == 1
+    finally:
+        lib.hsv_set_auto_committee(1)

@@ -26,5 +26,13 @@ for _ in range(5):
     f = verifier.verify_flags(w.pk, w.sig, w.msg)
     ts.append(time.perf_counter() - t0)
 ms = float(np.median(ts) * 1e3)
+import ctypes  # noqa: E402
+from hsverify import _lib  # noqa: E402
+lib = _lib.load()
+marks = (ctypes.c_double * 256)()
+cnt = lib.hsv_host_call_marks(marks, 256)
+print("per-chunk host marks (ms: staged-wait done, packed, copies enqueued, launch enqueued):")
+for k in range(0, cnt, 4):
+    print("  chunk %d: %s" % (k // 4, " ".join("%.3f" % marks[k + j] for j in range(4) if k + j < cnt)))
 print(json.dumps({"pipeline": "HSV_NO_PIPELINE" not in os.environ, "items": n, "ms": ms,
                   "verif_per_s": n / (ms * 1e-3), "ok": bool((f[w.accept] & 1).all())}))
