@@ -483,42 +483,42 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
 
 // Large host batches (n >= 2 pipe_chunk(), n <= kChunk): the inputs stream
 // to HBM chunk by chunk while earlier chunks verify.
-//   * HBM holds the whole batch (pk | sig | msg | flags | self-check words):
-//     a device region is never reused within the call, so a chunk's launch
-//     depends only on its own copy;
-//   * two pinned staging buffers alternate on the host: chunk c is packed
-//     while chunk c-1 copies, and a staging buffer is reused as soon as its
+//   * HBM holds the whole batch as records pk | R || s | digest (96 B with a
+//     shared digest, staged once), then all flags and the self-check words.
+//     A device region is never reused within the call, so a chunk's launch
+//     depends only on its own copy -- one copy per chunk, the first chunk
+//     half-size;
+//   * two pinned staging buffers alternate on the host: chunk k is packed
+//     while chunk k-1 copies, and a staging buffer is reused as soon as its
 //     copy is done (event), not when its chunk's kernels are;
-//   * copies run on the slot's copy stream, launches alternate over two
+//   * copies run on the slot's copy stream; launches alternate over two
 //     compute streams (a chunk's launch starts in the previous one's grid
-//     end), each waiting for its chunk's copy by event;
-//   * chunk sizes ramp up (p/4, p/2, then p = pipe_chunk()): the first launch
-//     waits for a quarter chunk's pack and copy, not a whole one;
+//     end), each waiting for its chunk's copy by event, each with a launch
+//     workspace the slot keeps (no allocation in the loop);
 //   * one copy back of all flags and the self-check words at the end.
-// The host's work (pack + enqueue) runs ahead of the GPU: the call takes the
-// GPU's time for the batch plus the first small chunk and the final copy back
-// (profiles/r03c_timeline.txt shows the two-buffer form it replaces, where
-// each chunk's pack waited for the chunk two back to finish verifying).
+// The host's part (pack + enqueue) runs ahead of the GPU; the call costs the
+// GPU's time for the chunks plus the first chunk's pack and copy and the copy
+// back ("host buffers").
 int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, size_t pk_stride, const uint8_t *sig,
                   size_t sig_stride, const uint8_t *msg, size_t msg_stride, size_t n, uint8_t *flags_out) {
   const size_t pchunk = pipe_chunk();
-  // HBM: pk n*32 | sig n*64 | msg n*32 (or 32) | flags n | self-check words
-  const size_t d_sig = round_up(n * 32, kAlign);
-  const size_t d_msg = d_sig + round_up(n * 64, kAlign);
-  const size_t d_flag = d_msg + round_up(msg_stride ? n * 32 : 32, kAlign);
+  const size_t rec = msg_stride ? 128 : 96;  // record bytes per item (a shared digest is staged once)
+  // HBM: records n*rec | shared digest | flags n | self-check words
+  const size_t d_dig = round_up(n * rec, kAlign);
+  const size_t d_flag = d_dig + kAlign;
   const size_t d_fault = d_flag + round_up(n, kAlign);
   const size_t d_total = d_fault + kAlign;
-  // host: two staging buffers of one chunk (pk | sig | msg) | flags n | self-check words
-  const size_t h_stage = round_up(pchunk * 128, kAlign);
+  // host: two staging buffers of one chunk | flags n | self-check words
+  const size_t h_stage = round_up(pchunk * rec, kAlign);
   const size_t h_flag = 2 * h_stage;
   const size_t h_fault = h_flag + round_up(n, kAlign);
   const size_t h_total = h_fault + kAlign;
   int rc = slot_prepare(s, d_total, h_total);
   if (rc == HSV_OK) rc = slot_pipeline(s);
   if (rc != HSV_OK) return rc;
-  // one launch workspace per compute stream, kept by the slot: no allocation
-  // inside the loop (a pool allocation per launch made the enqueue of each
-  // chunk wait ~1 ms for an earlier chunk, tools/host_api_probe.py marks)
+  // one launch workspace per compute stream, kept by the slot: a pool
+  // allocation per launch made the enqueue of each chunk wait ~1 ms for an
+  // earlier chunk (tools/host_api_probe.py marks)
   const size_t ws_need = hsv_launch_ws_bytes(v, (uint32_t)pchunk);
   if (ws_need > s.ws_cap) {
     for (uint8_t *&w : s.d_ws) {
@@ -544,56 +544,66 @@ int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, siz
   // flags and self-check words start at zero (unwritten flags read as
   // rejections); ordered before every launch through the staged events
   hipError_t e = hipMemsetAsync(d + d_flag, 0, d_total - d_flag, s.copy);
-  if (e == hipSuccess && msg_stride == 0) e = hipMemcpyAsync(d + d_msg, msg, 32, hipMemcpyHostToDevice, s.copy);
+  if (e == hipSuccess && msg_stride == 0) e = hipMemcpyAsync(d + d_dig, msg, 32, hipMemcpyHostToDevice, s.copy);
   if (e != hipSuccess) return drain(hip_fail("hipMemsetAsync", e));
   bool used[2] = {false, false};
-  size_t base = 0;
   const auto t_start = std::chrono::steady_clock::now();
   t_chunk_marks.clear();
-  for (int k = 0; base < n; ++k) {
-    const size_t want = k == 0 ? pchunk / 4 : k == 1 ? pchunk / 2 : pchunk;
-    const size_t m = std::min(want, n - base);
-    const int b = k & 1;
+  // Nothing hides the first chunk's pack and copy, so it is half a chunk
+  // (2^16 items: 10.73 ms per 2^20 against 10.99 for a full first chunk sent
+  // in four pieces and 11.01 for 2^15, profiles/r03m_host_pipeline_probe.txt).
+  // HSV_PIPE_FIRST_LOG2 overrides it (measurement switch).
+  static const size_t first_env = [] {
+    const char *v = std::getenv("HSV_PIPE_FIRST_LOG2");
+    const int l = v ? std::atoi(v) : 0;
+    return (l >= 12 && l <= 22) ? (size_t(1) << l) : size_t(0);
+  }();
+  const size_t first = std::min(pchunk, first_env ? first_env : pchunk / 2);
+  for (size_t base = 0, k = 0, m = 0; base < n; base += m, ++k) {
+    m = std::min(k == 0 ? first : pchunk, n - base);
+    const int b = (int)(k & 1);
     uint8_t *h = s.h_buf + (size_t)b * h_stage;
     if (used[b]) {  // the copy that last read this staging buffer has finished
       e = hipEventSynchronize(staged[b]);
       if (e != hipSuccess) return drain(hip_fail("hipEventSynchronize", e));
     }
     t_chunk_marks.push_back(ms_since(t_start));
-    const auto t_pack = std::chrono::steady_clock::now();
-    uint8_t *hpk = h, *hsig = h + m * 32, *hmsg = h + m * 96;
-    const int nparts = (int)std::min<size_t>(64, (m * 128 + kPackPart - 1) / kPackPart);
-    auto part = [&](int p) {
-      const size_t lo = m * p / nparts, hi = m * (p + 1) / nparts;
-      if (pk_stride == 32) std::memcpy(hpk + 32 * lo, pk + (base + lo) * 32, (hi - lo) * 32);
-      else for (size_t i = lo; i < hi; ++i) std::memcpy(hpk + 32 * i, pk + (base + i) * pk_stride, 32);
-      if (sig_stride == 64) std::memcpy(hsig + 64 * lo, sig + (base + lo) * 64, (hi - lo) * 64);
-      else for (size_t i = lo; i < hi; ++i) std::memcpy(hsig + 64 * i, sig + (base + i) * sig_stride, 64);
-      if (msg_stride == 32) std::memcpy(hmsg + 32 * lo, msg + (base + lo) * 32, (hi - lo) * 32);
-      else if (msg_stride != 0)
-        for (size_t i = lo; i < hi; ++i) std::memcpy(hmsg + 32 * i, msg + (base + i) * msg_stride, 32);
-    };
-    if (nparts < 2) part(0);
-    else PackPool::get().run(nparts, part);
-    t_pack_ms += ms_since(t_pack);
+    uint8_t *dc = d + base * rec;  // chunk k's records in HBM
+    // Items as records pk | R || s (| digest), so any item range is one
+    // contiguous copy.  A full-size first chunk (HSV_PIPE_FIRST_LOG2) goes in
+    // four pieces, each copied as soon as it is packed.
+    const size_t pieces = k == 0 && m == pchunk ? 4 : 1;
+    for (size_t q = 0; q < pieces; ++q) {
+      const size_t lo0 = m * q / pieces, hi0 = m * (q + 1) / pieces;
+      const auto t_pack = std::chrono::steady_clock::now();
+      const int nparts = (int)std::min<size_t>(64, ((hi0 - lo0) * rec + kPackPart - 1) / kPackPart);
+      auto part = [&](int p) {
+        const size_t lo = lo0 + (hi0 - lo0) * p / nparts, hi = lo0 + (hi0 - lo0) * (p + 1) / nparts;
+        for (size_t i = lo; i < hi; ++i) {
+          uint8_t *r = h + rec * i;
+          std::memcpy(r, pk + (base + i) * pk_stride, 32);
+          std::memcpy(r + 32, sig + (base + i) * sig_stride, 64);
+          if (msg_stride) std::memcpy(r + 96, msg + (base + i) * msg_stride, 32);
+        }
+      };
+      if (nparts < 2) part(0);
+      else PackPool::get().run(nparts, part);
+      t_pack_ms += ms_since(t_pack);
+      e = hipMemcpyAsync(dc + lo0 * rec, h + lo0 * rec, (hi0 - lo0) * rec, hipMemcpyHostToDevice, s.copy);
+      if (e != hipSuccess) return drain(hip_fail("hipMemcpyAsync H2D", e));
+    }
     t_chunk_marks.push_back(ms_since(t_start));
-    e = hipMemcpyAsync(d + base * 32, hpk, m * 32, hipMemcpyHostToDevice, s.copy);
-    if (e == hipSuccess) e = hipMemcpyAsync(d + d_sig + base * 64, hsig, m * 64, hipMemcpyHostToDevice, s.copy);
-    if (e == hipSuccess && msg_stride)
-      e = hipMemcpyAsync(d + d_msg + base * 32, hmsg, m * 32, hipMemcpyHostToDevice, s.copy);
-    if (e == hipSuccess) e = hipEventRecord(staged[b], s.copy);
+    e = hipEventRecord(staged[b], s.copy);
     if (e == hipSuccess) e = hipStreamWaitEvent(comp[b], staged[b], 0);
     if (e != hipSuccess) return drain(hip_fail("staging a chunk", e));
     used[b] = true;
     t_chunk_marks.push_back(ms_since(t_start));
-    t_h2d_bytes += m * (msg_stride ? 128 : 96);
-    e = hsv_launch_verify_ws(v, d + base * 32, 32, d + d_sig + base * 64, 64,
-                             d + d_msg + (msg_stride ? base * 32 : 0), msg_stride ? 32 : 0, (uint32_t)m,
-                             d + d_flag + base, nullptr, comb_b, reinterpret_cast<uint32_t *>(d + d_fault),
-                             s.d_ws[b], s.ws_cap, comp[b]);
+    t_h2d_bytes += m * rec;
+    e = hsv_launch_verify_ws(v, dc, rec, dc + 32, rec, msg_stride ? dc + 96 : d + d_dig, msg_stride ? rec : 0,
+                             (uint32_t)m, d + d_flag + base, nullptr, comb_b,
+                             reinterpret_cast<uint32_t *>(d + d_fault), s.d_ws[b], s.ws_cap, comp[b]);
     if (e != hipSuccess) return drain(hip_fail("verify kernel launch", e));
     t_chunk_marks.push_back(ms_since(t_start));
-    base += m;
   }
   // join: the flags come back once both compute streams are done
   e = hipEventRecord(s.ev[3], s.stream2);

@@ -73,24 +73,47 @@ def device_chunks(rounds):
         run()
         out[f"2^{lg}"] = sorted(run() for _ in range(rounds * 3))[rounds * 3 // 2]
     print(json.dumps({"device_chunked_ms_per_2^20": out}), flush=True)
+    # the same 2^17-item launches while another stream copies 16 MiB pinned
+    # buffers host-to-device back to back (as the host pipeline's copies do)
+    src = torch.empty(16 << 20, dtype=torch.uint8).pin_memory()
+    dst = torch.empty(16 << 20, dtype=torch.uint8, device=dev)
+    cs = torch.cuda.Stream(dev)
+    c = 1 << 17
+    res = []
+    for _ in range(rounds * 3):
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        with torch.cuda.stream(cs):
+            for _ in range(8):
+                dst.copy_(src, non_blocking=True)
+        for k, base in enumerate(range(0, N, c)):
+            verifier.verify_device(tp[base:base + c], ts[base:base + c], tm[base:base + c], flags[base:base + c],
+                                   stream=streams[k & 1].cuda_stream)
+        torch.cuda.synchronize(dev)
+        res.append((time.perf_counter() - t) * 1e3)
+    print(json.dumps({"device_chunked_2^17_with_concurrent_h2d_ms": sorted(res)[len(res) // 2]}), flush=True)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--child", action="store_true")
+    ap.add_argument("--device-only", action="store_true", help="only the device-chunked runs (for a trace)")
     a = ap.parse_args()
     if a.child:
         return child(a.rounds)
     workload()
     device_chunks(a.rounds)
-    for lg in (16, 17, 18):
-        for th in (6, 12):
-            env = dict(os.environ, HSV_PIPE_CHUNK_LOG2=str(lg), HSV_PACK_THREADS=str(th))
-            r = subprocess.run([sys.executable, __file__, "--child", "--rounds", str(a.rounds)], env=env,
-                               capture_output=True, text=True, timeout=300)
-            line = r.stdout.strip().splitlines()[-1] if r.returncode == 0 else f"rc={r.returncode} {r.stderr[-300:]}"
-            print(json.dumps({"chunk_log2": lg, "pack_threads": th, "result": line}), flush=True)
+    if a.device_only:
+        return
+    for lg, first in ((17, 0), (17, 15), (17, 16), (18, 16), (18, 0)):
+        env = dict(os.environ, HSV_PIPE_CHUNK_LOG2=str(lg))
+        if first:
+            env["HSV_PIPE_FIRST_LOG2"] = str(first)
+        r = subprocess.run([sys.executable, __file__, "--child", "--rounds", str(a.rounds)], env=env,
+                           capture_output=True, text=True, timeout=300)
+        line = r.stdout.strip().splitlines()[-1] if r.returncode == 0 else f"rc={r.returncode} {r.stderr[-300:]}"
+        print(json.dumps({"chunk_log2": lg, "first_log2": first or lg, "result": line}), flush=True)
 
 
 if __name__ == "__main__":
