@@ -4,9 +4,11 @@ time against the HBM-resident launch, at 2^20 triples:
 
   device  the same 2^20 items as device-resident launches of CHUNK items
           alternating over two streams (the GPU-side cost of chunking alone);
-  host    hsv_verify from host arrays, one fresh process per setting of
-          HSV_PIPE_CHUNK_LOG2 / HSV_PACK_THREADS (read once per process),
-          with the library's own pack time and the call's wall time.
+  host    hsv_verify from host arrays, one fresh process per setting of the
+          pipeline's measurement switches (HSV_PIPE_CHUNK_LOG2,
+          HSV_PIPE_FIRST_LOG2; read once per process; r03r also tried a
+          third compute stream, since removed), with
+          the library's own pack time and the call's wall time.
 
 python tools/host_pipeline_probe.py [--rounds 3]
 """
@@ -106,15 +108,13 @@ def main():
     device_chunks(a.rounds)
     if a.device_only:
         return
-    for lg, first in ((17, 0), (17, 15), (17, 16), (18, 16), (18, 0)):
-        env = dict(os.environ, HSV_PIPE_CHUNK_LOG2=str(lg))
-        if first:
-            env["HSV_PIPE_FIRST_LOG2"] = str(first)
+    cases = [{}, {"HSV_PIPE_FIRST_LOG2": "17"}, {"HSV_PIPE_FIRST_LOG2": "15"}, {"HSV_PIPE_CHUNK_LOG2": "18"}, {}]
+    for case in cases:
+        env = dict(os.environ, **case)
         r = subprocess.run([sys.executable, __file__, "--child", "--rounds", str(a.rounds)], env=env,
                            capture_output=True, text=True, timeout=300)
         line = r.stdout.strip().splitlines()[-1] if r.returncode == 0 else f"rc={r.returncode} {r.stderr[-300:]}"
-        print(json.dumps({"chunk_log2": lg, "first_log2": first or lg, "result": line}), flush=True)
-
+        print(json.dumps({"env": case, "result": line}), flush=True)
 
 if __name__ == "__main__":
     main()
