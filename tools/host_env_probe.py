@@ -6,7 +6,9 @@ fresh child per case --
   npz        inputs loaded from a cached .npz by the main thread;
   synth      inputs generated in-process by synth (16 threads, as bench.py);
   synth_copy the synth arrays copied once by the main thread;
-  after_c4   npz inputs, after ten HBM-resident 2^20 launches on three streams.
+  after_c4   npz inputs, after ten HBM-resident 2^20 launches on three streams;
+  after_load npz inputs, right after 2 s of back-to-back resident launches;
+  after_rest the same, then 2 s idle before the host calls.
 
 python tools/host_env_probe.py [--reps 9]
 """
@@ -23,7 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "hotstuff-digital-signature-benchmarking_amd"))
 CACHE = "/tmp/hsv_host_pipe_c4.npz"
 N = 1 << 20
-CASES = ("npz", "synth", "synth_copy", "after_c4")
+CASES = ("npz", "synth", "synth_copy", "after_c4", "after_load", "after_rest")
 
 
 def arrays(case):
@@ -42,15 +44,22 @@ def arrays(case):
 def child(case, reps):
     from hsverify import _testing, verifier
     pk, sig, msg = arrays(case)
-    if case == "after_c4":
+    if case.startswith("after"):
         import torch
         dev = torch.device("cuda", 0)
         tp, ts, tm = (torch.from_numpy(x).to(dev) for x in (pk, sig, msg))
         streams = [torch.cuda.Stream(dev) for _ in range(3)]
         flags = [torch.zeros(N, dtype=torch.uint8, device=dev) for _ in range(3)]
-        for k in range(10):
+        t_end = time.perf_counter() + (2.0 if case != "after_c4" else 0.0)
+        k = 0
+        while k < 10 or time.perf_counter() < t_end:
             verifier.verify_device(tp, ts, tm, flags[k % 3], stream=streams[k % 3].cuda_stream)
+            k += 1
+            if k % 30 == 0:
+                torch.cuda.synchronize(dev)
         torch.cuda.synchronize(dev)
+        if case == "after_rest":
+            time.sleep(2.0)
     verifier.verify_flags(pk, sig, msg)
     res = []
     for _ in range(reps):
@@ -71,7 +80,7 @@ def main():
     if a.child:
         return child(a.child, a.reps)
     arrays("npz")
-    for case in CASES + ("npz",):
+    for case in ("npz", "after_c4", "after_load", "after_rest", "npz", "after_load"):
         r = subprocess.run([sys.executable, __file__, "--child", case, "--reps", str(a.reps)],
                            capture_output=True, text=True, timeout=300)
         print(r.stdout.strip().splitlines()[-1] if r.returncode == 0 else f"{case}: rc={r.returncode} {r.stderr[-300:]}",
