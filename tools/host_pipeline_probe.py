@@ -101,14 +101,18 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--device-only", action="store_true", help="only the device-chunked runs (for a trace)")
+    ap.add_argument("--host-only", action="store_true", help="skip the device-chunked runs")
+    ap.add_argument("--cases", default=None, help="JSON list of env dicts, one child process each")
     a = ap.parse_args()
     if a.child:
         return child(a.rounds)
     workload()
-    device_chunks(a.rounds)
+    if not a.host_only:
+        device_chunks(a.rounds)
     if a.device_only:
         return
-    cases = [{}, {"HSV_PIPE_FIRST_LOG2": "17"}, {"HSV_PIPE_FIRST_LOG2": "15"}, {"HSV_PIPE_CHUNK_LOG2": "18"}, {}]
+    cases = (json.loads(a.cases) if a.cases else
+             [{}, {"HSV_PIPE_FIRST_LOG2": "17"}, {"HSV_PIPE_FIRST_LOG2": "15"}, {"HSV_PIPE_CHUNK_LOG2": "18"}, {}])
     for case in cases:
         env = dict(os.environ, **case)
         r = subprocess.run([sys.executable, __file__, "--child", "--rounds", str(a.rounds)], env=env,
