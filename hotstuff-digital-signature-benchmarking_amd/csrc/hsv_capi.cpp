@@ -508,6 +508,41 @@ size_t pipe_chunk() {  // HSV_PIPE_CHUNK_LOG2 (14..22): measurement switch
   return c;
 }
 
+// Chunk sizes of a pipelined call over n items (n >= 2 pipe_chunk()).
+// Nothing hides the first chunk's pack and copy, so it is half a chunk
+// (2^16 items: 10.73 ms per 2^20 against 10.99 for a full first chunk sent
+// in four pieces and 11.01 for 2^15, profiles/r03m_host_pipeline_probe.txt).
+// Measurement switches: HSV_PIPE_FIRST_LOG2 sets the first chunk;
+// HSV_PIPE_SIZES="a,b,..." gives the sizes in units of 2^14 items (the last
+// one repeats until the n items are covered).
+std::vector<size_t> pipe_schedule(size_t n) {
+  const size_t pchunk = pipe_chunk();
+  static const size_t first_env = [] {
+    const int l = env_int("HSV_PIPE_FIRST_LOG2", 0);
+    return (l >= 12 && l <= 22) ? (size_t(1) << l) : size_t(0);
+  }();
+  static const std::vector<size_t> sizes_env = [] {
+    std::vector<size_t> v;
+    if (const char *e = std::getenv("HSV_PIPE_SIZES"))
+      for (const char *c = e; *c;) {
+        const long u = std::strtol(c, const_cast<char **>(&c), 10);
+        if (u > 0 && u <= 256) v.push_back(size_t(u) << 14);
+        while (*c == ',' || *c == ' ') ++c;
+        if (*c && (*c < '0' || *c > '9')) break;
+      }
+    return v;
+  }();
+  std::vector<size_t> sizes;
+  for (size_t base = 0, k = 0; base < n; ++k) {
+    size_t want;
+    if (!sizes_env.empty()) want = sizes_env[std::min(k, sizes_env.size() - 1)];
+    else want = k == 0 ? std::min(pchunk, first_env ? first_env : pchunk / 2) : pchunk;
+    sizes.push_back(std::min(want, n - base));
+    base += sizes.back();
+  }
+  return sizes;
+}
+
 // Stats of the calling thread's last host-buffer call (hsv_host_call_stats,
 // a measurement hook): host time spent packing into pinned staging, bytes
 // copied host-to-device, and the call's wall time.
@@ -541,15 +576,16 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
 // back ("host buffers").
 int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, size_t pk_stride, const uint8_t *sig,
                   size_t sig_stride, const uint8_t *msg, size_t msg_stride, size_t n, uint8_t *flags_out) {
-  const size_t pchunk = pipe_chunk();
+  const std::vector<size_t> sizes = pipe_schedule(n);
+  const size_t maxm = *std::max_element(sizes.begin(), sizes.end());
   const size_t rec = msg_stride ? 128 : 96;  // record bytes per item (a shared digest is staged once)
   // HBM: records n*rec | shared digest | flags n | self-check words
   const size_t d_dig = round_up(n * rec, kAlign);
   const size_t d_flag = d_dig + kAlign;
   const size_t d_fault = d_flag + round_up(n, kAlign);
   const size_t d_total = d_fault + kAlign;
-  // host: two staging buffers of one chunk | flags n | self-check words
-  const size_t h_stage = round_up(pchunk * rec, kAlign);
+  // host: two staging buffers of the largest chunk | flags n | self-check words
+  const size_t h_stage = round_up(maxm * rec, kAlign);
   const size_t h_flag = 2 * h_stage;
   const size_t h_fault = h_flag + round_up(n, kAlign);
   const size_t h_total = h_fault + kAlign;
@@ -559,7 +595,7 @@ int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, siz
   // one launch workspace per compute stream, kept by the slot: a pool
   // allocation per launch made the enqueue of each chunk wait ~1 ms for an
   // earlier chunk (tools/host_api_probe.py marks)
-  const size_t ws_need = hsv_launch_ws_bytes(v, (uint32_t)pchunk);
+  const size_t ws_need = hsv_launch_ws_bytes(v, (uint32_t)maxm);
   if (ws_need > s.ws_cap) {
     for (uint8_t *&w : s.d_ws) {
       if (w) (void)hipFree(w);
@@ -589,31 +625,6 @@ int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, siz
   bool used[2] = {false, false};
   const auto t_start = std::chrono::steady_clock::now();
   t_chunk_marks.clear();
-  // Nothing hides the first chunk's pack and copy, so it is half a chunk
-  // (2^16 items: 10.73 ms per 2^20 against 10.99 for a full first chunk sent
-  // in four pieces and 11.01 for 2^15, profiles/r03m_host_pipeline_probe.txt).
-  // HSV_PIPE_FIRST_LOG2 overrides it (measurement switch).
-  static const size_t first_env = [] {
-    const char *v = std::getenv("HSV_PIPE_FIRST_LOG2");
-    const int l = v ? std::atoi(v) : 0;
-    return (l >= 12 && l <= 22) ? (size_t(1) << l) : size_t(0);
-  }();
-  const size_t first = std::min(pchunk, first_env ? first_env : pchunk / 2);
-  // measurement switches: HSV_PIPE_RAMP=1 doubles the chunks from the first
-  // up to pchunk; HSV_PIPE_TAIL_LOG2 ends the call with a chunk of that size
-  static const bool ramp = env_int("HSV_PIPE_RAMP", 0) != 0;
-  static const size_t tail_env = [] {
-    const int l = env_int("HSV_PIPE_TAIL_LOG2", 0);
-    return (l >= 12 && l <= 22) ? (size_t(1) << l) : size_t(0);
-  }();
-  const size_t tail = tail_env && n > 4 * tail_env ? std::min(tail_env, pchunk) : 0;
-  std::vector<size_t> sizes;
-  for (size_t base = 0, k = 0; base < n - tail; ++k) {
-    const size_t want = k == 0 ? first : ramp ? std::min(pchunk, first << std::min<size_t>(k, 20)) : pchunk;
-    sizes.push_back(std::min(want, n - tail - base));
-    base += sizes.back();
-  }
-  if (tail) sizes.push_back(tail);
   for (size_t base = 0, k = 0, m = 0; k < sizes.size(); base += m, ++k) {
     m = sizes[k];
     const int b = (int)(k & 1);
@@ -627,7 +638,7 @@ int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, siz
     // Items as records pk | R || s (| digest), so any item range is one
     // contiguous copy.  A full-size first chunk (HSV_PIPE_FIRST_LOG2) goes in
     // four pieces, each copied as soon as it is packed.
-    const size_t pieces = k == 0 && m == pchunk ? 4 : 1;
+    const size_t pieces = k == 0 && m >= pipe_chunk() ? 4 : 1;
     for (size_t q = 0; q < pieces; ++q) {
       const size_t lo0 = m * q / pieces, hi0 = m * (q + 1) / pieces;
       const auto t_pack = std::chrono::steady_clock::now();
