@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include "hsv_comb.hpp"
+#include "hsv_fe16x16.hpp"
 #include "hsv_internal.h"
 
 namespace hsv {
@@ -75,18 +76,22 @@ hsv_comb_verify_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__re
 }
 
 // Latency form of hsv_comb_verify_kernel for small batches (a QC is 67 or
-// 667 votes): L lanes per vote (HSV_COMB_LANES, default 4).  Lane g of a
+// 667 votes): L lanes per vote (HSV_COMB_LANES, default 16).  Lane g of a
 // vote's group adds the comb entries of positions [g P, (g+1) P), P = 32 / L,
 // for both k (the key's table) and s (the B table): 2P mixed additions on the
 // critical lane instead of 64; the group's partial sums meet through log2(L)
 // lane-swap + addition rounds (16 lanes: 4 + 4 additions in sequence, 4 lanes:
 // 16 + 2).  Every lane of the group hashes the vote (same instruction stream,
 // no extra latency); flags come out of lane 0 exactly as verify_one_comb
-// computes them.  The vote's critical path is R's root chain on wave 1 (below),
-// not the additions: 16 lanes per vote measured 4-7 % slower than 4 (more
-// waves, same chain; profiles/r02w_qc_ab.txt).
+// computes them.  With R decompressed on one lane (round 2) its root chain was
+// the critical path and 16 lanes measured 4-7 % slower than 4
+// (profiles/r02w_qc_ab.txt).  With the lane-split R waves the additions are
+// the longer piece at 4 lanes per vote, and a block of 4 lanes per vote needs
+// 5 waves, which then share SIMDs: C1 / C3 p50 0.099 / 0.105 ms at 4 lanes,
+// 0.057 / 0.062 at 8 (3 waves), 0.055 / 0.062 at 16 (2 waves), against
+// 0.082 / 0.088 ms for round 2's form (profiles/r03z_qc_ab.txt).
 #ifndef HSV_COMB_LANES
-#define HSV_COMB_LANES 4
+#define HSV_COMB_LANES 16
 #endif
 constexpr int kCombLanes = HSV_COMB_LANES;
 static_assert(kCombLanes == 4 || kCombLanes == 8 || kCombLanes == 16, "lanes per vote");
@@ -104,16 +109,26 @@ __device__ __forceinline__ ge_ext ge_swap_xor(const ge_ext &p, int m) {
   return r;
 }
 
-// The latency form in two specialised waves (at <= kCombQuadMax votes): a
-// block of 128 threads takes 64 / L votes.  Wave 0 computes each vote's
-// combined sum Q = [s]B - [k]A over L lanes; wave 1 decompresses the votes' R
-// (one lane each) at the same time on another SIMD and leaves (x, y, flags)
-// in LDS.  R's root chain, the longest single piece, runs beside the hash and
-// the comb additions: the vote costs max(hash + comb, root chain) + the final
-// comparison.
+// The latency form in specialised waves (at <= kCombQuadMax votes): a block
+// takes 64 / L votes.  Wave 0 computes each vote's combined sum
+// Q = [s]B - [k]A over L lanes; the R waves decompress the votes' R at the
+// same time on other SIMDs and leave (x, y, flags) in LDS.  R's root chain,
+// the longest single piece, runs beside the hash and the comb additions: the
+// vote costs max(hash + comb, root chain) + the final comparison.  The R
+// waves hold one vote per 16-lane row with the products spread over the row
+// (ge_decompress_row, hsv_fe16x16.hpp: 32 us for the root chain on a lone
+// wave against 57 us on one lane, profiles/r03z_ubench_lanesplit.txt), four
+// votes per wave.  HSV_COMB_R_ONELANE (measurement builds only) keeps round
+// 2's single R wave with one vote per lane.
 constexpr int kFusedVotes = 64 / kCombLanes;
+#ifdef HSV_COMB_R_ONELANE
+constexpr int kFusedRWaves = 1;
+#else
+constexpr int kFusedRWaves = (kFusedVotes + 3) / 4;
+#endif
+constexpr int kFusedThreads = 64 * (1 + kFusedRWaves);
 
-__global__ void __launch_bounds__(128)
+__global__ void __launch_bounds__(kFusedThreads)
 hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__restrict__ sig,
                                   uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride,
                                   uint32_t m, const uint8_t *__restrict__ pks, const uint8_t *__restrict__ key_flags,
@@ -123,7 +138,28 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
   __shared__ uint32_t r_x[kFusedVotes][kFeLimbs], r_y[kFusedVotes][kFeLimbs], r_fl[kFusedVotes];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint32_t base = blockIdx.x * kFusedVotes;
-  if (wave == 1) {
+  if (wave >= 1) {
+#ifndef HSV_COMB_R_ONELANE
+    const RowLane L;
+    const uint32_t vr = (wave - 1u) * 4u + (lane >> 4);  // this row's vote in the block
+    if (vr < (uint32_t)kFusedVotes) {
+      const uint32_t i = base + vr < m ? base + vr : m - 1u;
+      const uint4 *sp = reinterpret_cast<const uint4 *>(sig + (uint64_t)i * sig_stride);
+      const uint4 s0 = sp[0], s1 = sp[1];
+      const uint32_t rw[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      fe rx, ry;
+      const uint32_t r_ok = ge_decompress_row(rw, rx, ry, L);
+      const uint32_t small_r = r_ok & y_is_small_order(ry);
+      if (L.k == 0u) {
+        HSV_UNROLL
+        for (int l = 0; l < kFeLimbs; ++l) {
+          r_x[vr][l] = rx.v[l];
+          r_y[vr][l] = ry.v[l];
+        }
+        r_fl[vr] = r_ok | (small_r << 1);
+      }
+    }
+#else
     if (lane < (uint32_t)kFusedVotes) {
       const uint32_t i = base + lane < m ? base + lane : m - 1u;
       const uint4 *sp = reinterpret_cast<const uint4 *>(sig + (uint64_t)i * sig_stride);
@@ -139,6 +175,7 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
       }
       r_fl[lane] = r_ok | (small_r << 1);
     }
+#endif
     __syncthreads();
     return;
   }
@@ -226,6 +263,33 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
   if (valid && g == 0u) flags_out[i0] = kvalid ? (uint8_t)f : (uint8_t)0;
 }
 
+// Test hook (tests/test_lanesplit.py): the row form of hsv_fe16x16.hpp
+// against the one-lane form, one 16-lane row per input of 16 words (a | b,
+// 8 little-endian words each).  out[row] bit 0: a * b differs, bit 1:
+// a^((p-5)/8) differs, bit 2: ge_decompress_row(a) differs from
+// ge_decompress(a) in its flag or, for a decodable a, in (x, y).
+__global__ void __launch_bounds__(64) hsv_lanesplit_check_kernel(const uint32_t *__restrict__ in, uint32_t rows,
+                                                                 uint32_t *__restrict__ out) {
+  const RowLane L;
+  const uint32_t r = blockIdx.x * 4u + (threadIdx.x >> 4);
+  const uint32_t rr = r < rows ? r : rows - 1u;
+  uint32_t aw[8], bw[8];
+  HSV_UNROLL
+  for (int i = 0; i < 8; ++i) {
+    aw[i] = in[16u * rr + i];
+    bw[i] = in[16u * rr + 8u + i];
+  }
+  const fe a = fe_from_words_masked(aw), b = fe_from_words_masked(bw);
+  uint32_t bad = 0;
+  bad |= fe_eq(fe_mul(a, b), fl_to_fe(fl_mul(fl_from_fe(a, L), fl_from_fe(b, L), L), L)) ? 0u : 1u;
+  bad |= fe_eq(fe_pow22523(a), fl_to_fe(fl_pow22523(fl_from_fe(a, L), L), L)) ? 0u : 2u;
+  fe x0, y0, x1, y1;
+  const uint32_t ok0 = ge_decompress(aw, x0, y0);
+  const uint32_t ok1 = ge_decompress_row(aw, x1, y1, L);
+  bad |= (ok0 == ok1 && (!ok0 || (fe_eq(x0, x1) && fe_eq(y0, y1)))) ? 0u : 4u;
+  if (r < rows && L.k == 0u) out[r] = bad;
+}
+
 // one lane per (position j, chunk c) of the wide B table; j is wave-uniform
 // (256 chunks per position)
 __global__ void __launch_bounds__(256) hsv_comb16_build_kernel(uint32_t *__restrict__ table,
@@ -246,6 +310,25 @@ extern "C" hipError_t hsv_launch_comb16_build(uint32_t *table, uint32_t *tmp, hi
   const uint32_t lanes = (uint32_t)(hsv::kComb16Pos * hsv::kComb16ChunksPerPos);
   hipLaunchKernelGGL(hsv::hsv_comb16_build_kernel, dim3(lanes / 256u), dim3(256), 0, stream, table, tmp);
   return hipGetLastError();
+}
+
+// Test hook, not in hsv.h: runs hsv_lanesplit_check_kernel on the current
+// device over `rows` host inputs of 16 words; 0 or a hipError_t.
+extern "C" int hsv_test_lanesplit_check(const uint32_t *in, uint32_t rows, uint32_t *out) {
+  if (rows == 0) return 0;
+  uint32_t *d_in = nullptr, *d_out = nullptr;
+  hipError_t e = hipMalloc(&d_in, (size_t)rows * 64);
+  if (e == hipSuccess) e = hipMalloc(&d_out, (size_t)rows * 4);
+  if (e == hipSuccess) e = hipMemcpy(d_in, in, (size_t)rows * 64, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(hsv::hsv_lanesplit_check_kernel, dim3((rows + 3) / 4), dim3(64), 0, 0, d_in, rows, d_out);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(out, d_out, (size_t)rows * 4, hipMemcpyDeviceToHost);
+  if (d_in) (void)hipFree(d_in);
+  if (d_out) (void)hipFree(d_out);
+  return (int)e;
 }
 
 extern "C" uint64_t hsv_comb16_table_bytes(void) { return hsv::kComb16TableWords * 4ull; }
@@ -275,9 +358,9 @@ extern "C" hipError_t hsv_launch_comb_verify(const uint32_t *key_idx, const uint
   if (m == 0) return hipSuccess;
   if (!fault) return hipErrorInvalidValue;
   const uint32_t inject = (uint32_t)hsv_test_inject_mode();
-  if (m <= kCombQuadMax) {  // latency form: four lanes per vote, R decompressed by a second wave
+  if (m <= kCombQuadMax) {  // latency form: four lanes per vote, R decompressed by the R waves
     hipLaunchKernelGGL(hsv::hsv_comb_verify_quad_fused_kernel, dim3((m + hsv::kFusedVotes - 1) / hsv::kFusedVotes),
-                       dim3(128), 0, stream, key_idx, sig, sig_stride, msg, msg_stride, m, pks, key_flags, nkeys,
+                       dim3(hsv::kFusedThreads), 0, stream, key_idx, sig, sig_stride, msg, msg_stride, m, pks, key_flags, nkeys,
                        key_tables, btable, flags_out, inject, fault);
     return hipGetLastError();
   }

@@ -1,0 +1,191 @@
+// GF(2^255 - 19) spread over a row of 16 lanes (device only): the latency
+// form of a field element for a lone wave.
+//
+// A lone wave issues one VALU instruction per 4 clocks (8 for v_mad_u64_u32)
+// however many of its lanes are active, so a product on one lane costs its
+// whole instruction count: ~97 instructions and ~620 clocks for a squaring in
+// radix 2^25.5 (hsv_fe26x10.hpp, profiles/r02w_ubench_fe_lone_wave.txt).
+// Here lane k of a 16-lane DPP row holds limb k of a radix-2^16 element
+// (2^256 = 38 mod p), and a product runs the 16 columns side by side:
+//
+//   step i = 0..15:  acc_k += f_i * g'_k,   g'_k = g_{(k-i) mod 16}, times 38
+//                    once the limb has wrapped past lane 15 (2^256 = 38)
+//   f_i  reaches every lane of the row by DPP row_newbcast:i,
+//   g'   moves one lane up per step by DPP row_ror:1 folded into the
+//        v_mul_u32_u24 that scales the wrapped limb (38 on lane 0, 1 elsewhere);
+//   two carry passes (lane k's carry to lane k + 1, lane 15's times 38 to
+//   lane 0) leave limbs <= 2^16.05 (the bound is a fixed point of the
+//   passes; operands may also be unreduced sums with limbs < 2^18, whose
+//   product comes out <= 2^16.1: tools/lanesplit_model.py checks every
+//   instruction's bound over worst-case inputs, tests/test_lanesplit.py).
+//
+// 16 v_mad_u64_u32 + 16 broadcasts + 15 rotations + 8 carry instructions:
+// ~55 instructions and ~290 clocks per product or squaring on a lone wave.
+// Four rows of a wave hold four independent elements.
+//
+// Bounds (limbs <= M = 2^16.05 in, out):
+//   g' <= 38 M < 2^21.3 (the u24 multiply needs < 2^24);
+//   acc_0 <= M^2 (15 * 38 + 1) < 2^41.3;
+//   pass 1 carry <= 2^25.3 (lane 15's: <= 16 M^2 / 2^16, times 38 < 2^25.4);
+//   pass 2 carry <= 2^9.3, lane 15's times 38 <= 2^11.1.
+#pragma once
+#include "hsv_point.hpp"
+
+#if defined(__HIPCC__)
+namespace hsv {
+
+// lane constants of the row form, computed once per kernel
+struct RowLane {
+  uint32_t k;     // limb index = lane & 15
+  uint32_t win;   // 38 on lane 0 (a limb arriving from lane 15 wraps), else 1
+  uint32_t wout;  // 38 on lane 15 (its carry wraps to lane 0), else 1
+  __device__ __forceinline__ RowLane() {
+    k = __lane_id() & 15u;
+    win = k == 0u ? 38u : 1u;
+    wout = k == 15u ? 38u : 1u;
+  }
+};
+
+// DPP within a row of 16 lanes
+template <int I>
+__device__ __forceinline__ uint32_t row_bcast(uint32_t x) {  // lane I of the row, to every lane of it
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x150 + I, 0xf, 0xf, true);
+}
+__device__ __forceinline__ uint32_t row_ror1(uint32_t x) {  // lane k <- lane (k - 1) mod 16
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x121, 0xf, 0xf, true);
+}
+__device__ __forceinline__ uint32_t row_shl1(uint32_t x) {  // lane k <- lane k + 1 (lane 15 <- 0)
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x101, 0xf, 0xf, true);
+}
+
+template <int I>
+__device__ __forceinline__ void fl_mul_step(uint64_t &acc, uint32_t &gr, uint32_t f, const RowLane &L) {
+  if constexpr (I > 0) gr = __umul24(row_ror1(gr), L.win);
+  acc += (uint64_t)row_bcast<I>(f) * gr;
+  if constexpr (I < 15) fl_mul_step<I + 1>(acc, gr, f, L);
+}
+
+// f * g, limbs <= 2^16.05 in and out
+__device__ __forceinline__ uint32_t fl_mul(uint32_t f, uint32_t g, const RowLane &L) {
+  HSV_SCHED_FENCE();
+  uint64_t acc = 0;
+  uint32_t gr = g;
+  fl_mul_step<0>(acc, gr, f, L);
+  // pass 1: the carry may exceed 2^24, so lane 15's factor 38 is a full multiply
+  uint32_t lo = (uint32_t)acc & 0xffffu;
+  uint32_t t = __builtin_amdgcn_alignbit((uint32_t)(acc >> 32), (uint32_t)acc, 16);
+  uint32_t x = lo + row_ror1(t * L.wout);
+  // pass 2
+  lo = x & 0xffffu;
+  t = x >> 16;
+  x = lo + row_ror1(__umul24(t, L.wout));
+  HSV_SCHED_FENCE();
+  return x;
+}
+
+__device__ __forceinline__ uint32_t fl_sq(uint32_t f, const RowLane &L) { return fl_mul(f, f, L); }
+
+__device__ __forceinline__ uint32_t fl_sqn(uint32_t f, int n, const RowLane &L) {
+  HSV_NOUNROLL
+  for (int i = 0; i < n; ++i) f = fl_sq(f, L);
+  return f;
+}
+
+// z^((p-5)/8) = z^(2^252 - 3), the chain of fe_pow22523 (hsv_field.hpp)
+__device__ __forceinline__ uint32_t fl_pow22523(uint32_t z, const RowLane &L) {
+  uint32_t t0 = fl_sq(z, L);                 // 2
+  uint32_t t1 = fl_sq(fl_sq(t0, L), L);      // 8
+  t1 = fl_mul(z, t1, L);                     // 9
+  t0 = fl_mul(t0, t1, L);                    // 11
+  t0 = fl_sq(t0, L);                         // 22
+  t0 = fl_mul(t1, t0, L);                    // 31 = 2^5 - 1
+  t1 = fl_sqn(t0, 5, L);
+  t0 = fl_mul(t1, t0, L);                    // 2^10 - 1
+  t1 = fl_sqn(t0, 10, L);
+  t1 = fl_mul(t1, t0, L);                    // 2^20 - 1
+  uint32_t t2 = fl_sqn(t1, 20, L);
+  t1 = fl_mul(t2, t1, L);                    // 2^40 - 1
+  t1 = fl_sqn(t1, 10, L);
+  t0 = fl_mul(t1, t0, L);                    // 2^50 - 1
+  t1 = fl_sqn(t0, 50, L);
+  t1 = fl_mul(t1, t0, L);                    // 2^100 - 1
+  t2 = fl_sqn(t1, 100, L);
+  t1 = fl_mul(t2, t1, L);                    // 2^200 - 1
+  t1 = fl_sqn(t1, 50, L);
+  t0 = fl_mul(t1, t0, L);                    // 2^250 - 1
+  t0 = fl_sqn(t0, 2, L);                     // 2^252 - 4
+  return fl_mul(t0, z, L);                   // 2^252 - 3
+}
+
+// Limb k of 8 little-endian words held identically by every lane of the row:
+// word k/2 by selects on lane masks (the row pattern repeats every 16 lanes),
+// no indexed register access.
+__device__ __forceinline__ uint32_t row_limb_of_words(const uint32_t w[8], const RowLane &L) {
+  uint32_t x = w[0];
+  HSV_UNROLL
+  for (int j = 1; j < 8; ++j) {
+    const uint64_t m = 0x0003000300030003ull << (2 * j);
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(x) : "v"(x), "v"(w[j]), "s"(m));
+  }
+  return (L.k & 1u) ? x >> 16 : x & 0xffffu;
+}
+
+// The element held identically by every lane of the row (class R, ten
+// limbs) -> this lane's radix-2^16 limb of its canonical value.
+__device__ __forceinline__ uint32_t fl_from_fe(const fe &a, const RowLane &L) {
+  uint32_t w[8];
+  fe_pack(a, w);
+  return row_limb_of_words(w, L);
+}
+
+// this row's element (limbs <= 2^16.05) -> ten limbs (class R, value < 2^255,
+// possibly >= p) in every lane of the row
+__device__ __forceinline__ fe fl_to_fe(uint32_t x, const RowLane &L) {
+  // exact limbs: 16 bits each, 15 for limb 15, whose carry (weight 2^255)
+  // wraps to lane 0 times 19; repeated until no lane of the wave carries
+  const uint32_t sh = L.k == 15u ? 15u : 16u;
+  const uint32_t mask = (1u << sh) - 1u;
+  const uint32_t w19 = L.k == 15u ? 19u : 1u;
+  for (;;) {
+    const uint32_t t = x >> sh;
+    x = (x & mask) + row_ror1(__umul24(t, w19));
+    if (!__ballot(t != 0u)) break;
+  }
+  // words: lane 2j holds limbs 2j | 2j+1, then each word to every lane
+  const uint32_t pair = x | (row_shl1(x) << 16);
+  uint32_t w[8];
+  w[0] = row_bcast<0>(pair);
+  w[1] = row_bcast<2>(pair);
+  w[2] = row_bcast<4>(pair);
+  w[3] = row_bcast<6>(pair);
+  w[4] = row_bcast<8>(pair);
+  w[5] = row_bcast<10>(pair);
+  w[6] = row_bcast<12>(pair);
+  w[7] = row_bcast<14>(pair);
+  return fe_from_words_masked(w);
+}
+
+// CompressedEdwardsY::decompress (ge_decompress, hsv_point.hpp) for one
+// encoding per row, every lane of the row holding it: the products of
+// sqrt_ratio_i -- y^2, d y^2, v^3, v^7, u v^7, the root chain, u v^3 (.)
+// and v r^2 -- in the row form, the sign rules on ten limbs.  Every lane of
+// the row returns the same (x, y) and flag as ge_decompress.
+__device__ __forceinline__ uint32_t ge_decompress_row(const uint32_t enc[8], fe &x, fe &y, const RowLane &L) {
+  y = fe_from_words_masked(enc);
+  uint32_t yl = row_limb_of_words(enc, L);
+  if (L.k == 15u) yl &= 0x7fffu;  // bit 255 is the sign of x
+  const uint32_t yy = fl_sq(yl, L);
+  // u = y^2 - 1 as y^2 + (p - 1), limbs < 2^17.1 (a product operand may be < 2^18)
+  const uint32_t u = yy + (L.k == 0u ? 0xffecu : L.k == 15u ? 0x7fffu : 0xffffu);
+  const uint32_t v = fl_mul(yy, fl_from_fe(fe_d(), L), L) + (L.k == 0u ? 1u : 0u);
+  const uint32_t v3 = fl_mul(fl_sq(v, L), v, L);
+  const uint32_t v7 = fl_mul(fl_sq(v3, L), v, L);
+  const uint32_t r = fl_mul(fl_mul(u, v3, L), fl_pow22523(fl_mul(u, v7, L), L), L);
+  const uint32_t check = fl_mul(v, fl_sq(r, L), L);
+  const uint32_t ok = fe_sqrt_ratio_fix_chk(fl_to_fe(u, L), fl_to_fe(check, L), fl_to_fe(r, L), x);
+  x = fe_canon(fe_select(x, fe_neg(x), enc[7] >> 31));  // -0 == 0 is accepted (no rejection)
+  return ok;
+}
+
+}  // namespace hsv
+#endif

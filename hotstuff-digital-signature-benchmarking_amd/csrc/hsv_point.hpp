@@ -145,8 +145,9 @@ HSV_INL ge_niels ge_niels_cneg(const ge_niels &q, uint32_t neg) {
 
 // Tail of sqrt_ratio_i once the candidate root r = u v^3 (u v^7)^((p-5)/8)
 // is known: fix up by sqrt(-1), pick the non-negative root.
-HSV_INL uint32_t fe_sqrt_ratio_fix(const fe &u, const fe &v, fe r, fe &r_out) {
-  fe check = fe_mul(v, fe_sq(r));
+// check = v r^2, computed by the caller (the lane-split R decompression has it
+// from its own products)
+HSV_INL uint32_t fe_sqrt_ratio_fix_chk(const fe &u, const fe &check, fe r, fe &r_out) {
   fe neg_u = fe_neg(u);
   uint32_t correct = fe_eq(check, u);
   uint32_t flipped = fe_eq(check, neg_u);
@@ -156,6 +157,10 @@ HSV_INL uint32_t fe_sqrt_ratio_fix(const fe &u, const fe &v, fe r, fe &r_out) {
   const uint32_t neg = fe_is_negative(r);
   r_out = fe_canon(fe_select(r, fe_neg(r), neg));
   return correct | flipped;
+}
+
+HSV_INL uint32_t fe_sqrt_ratio_fix(const fe &u, const fe &v, fe r, fe &r_out) {
+  return fe_sqrt_ratio_fix_chk(u, fe_mul(v, fe_sq(r)), r, r_out);
 }
 
 // curve25519-dalek FieldElement::sqrt_ratio_i: returns was_nonzero_square

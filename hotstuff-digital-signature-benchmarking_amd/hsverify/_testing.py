@@ -56,3 +56,19 @@ def host_call_stats() -> dict:
 def pack_threads() -> int:
     """Helper threads of the library's staging-copy pool (HSV_PACK_THREADS)."""
     return _lib.load().hsv_pack_threads()
+
+
+def lanesplit_check(words):
+    """Row-form field arithmetic against the one-lane form on the GPU
+    (hsv_test_lanesplit_check): words is an (n, 16) uint32 array of element
+    pairs a | b; returns per-row mismatch bits (1 product, 2 root chain,
+    4 decompression of a as an encoding)."""
+    import numpy as np
+    w = np.ascontiguousarray(words, dtype=np.uint32)
+    out = np.zeros(len(w), np.uint32)
+    lib = _lib.load()
+    rc = lib.hsv_test_lanesplit_check(ctypes.c_void_p(w.ctypes.data), ctypes.c_uint32(len(w)),
+                                      ctypes.c_void_p(out.ctypes.data))
+    if rc != 0:
+        raise RuntimeError(f"hsv_test_lanesplit_check failed: hipError {rc}")
+    return out
