@@ -148,7 +148,13 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
       const uint4 s0 = sp[0], s1 = sp[1];
       const uint32_t rw[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
       fe rx, ry;
+#ifdef HSV_TIMING_STUB_RWAVE  // tools/qc_phase_probe.py only: wrong flags, the quad path's time alone
+      rx = fe_small(0);
+      ry = fe_from_words_masked(rw);
+      const uint32_t r_ok = 1u;
+#else
       const uint32_t r_ok = ge_decompress_row(rw, rx, ry, L);
+#endif
       const uint32_t small_r = r_ok & y_is_small_order(ry);
       if (L.k == 0u) {
         HSV_UNROLL
@@ -204,6 +210,11 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
     msgw[4] = m1.x; msgw[5] = m1.y; msgw[6] = m1.z; msgw[7] = m1.w;
   }
   const uint32_t s_ok = sc_is_canonical(sigw + 8);
+#ifdef HSV_TIMING_STUB_QUADPATH  // tools/qc_phase_probe.py only: wrong flags, the R waves' time alone
+  ge_ext q = ge_identity();
+  const uint32_t *ta = key_tables[kk];
+  (void)ta;
+#else
   uint32_t h[16];
   sha512_96(sigw, pkw, msgw, h);
   const sc k = sc_reduce512(h);
@@ -240,6 +251,7 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
   HSV_UNROLL
   for (int mask = 1; mask < kCombLanes; mask <<= 1)
     q = ge_add_cached_rt(q, ge_to_cached(ge_swap_xor(q, mask)), mask < kCombLanes / 2);
+#endif
   __syncthreads();
   fe rx, ry;
   HSV_UNROLL
