@@ -97,6 +97,35 @@ constexpr int kCombLanes = HSV_COMB_LANES;
 static_assert(kCombLanes == 4 || kCombLanes == 8 || kCombLanes == 16, "lanes per vote");
 constexpr int kCombPosPerLane = kCombPos / kCombLanes;
 
+// ---- checks of a vote's final sum spread over its 16-lane row (L = 16) ----
+#ifdef HSV_COMB_SEQ_CHECKS  // measurement builds only: the one-lane checks of round 2
+constexpr bool kRowChecks = false;
+#else
+constexpr bool kRowChecks = kCombLanes == 16;
+#endif
+// After the swap rounds every lane of the vote's row holds Q, and the row is a
+// DPP row, so the final checks run as rounds of one field operation per lane.
+// ge_is_sane (hsv_point.hpp) in three rounds instead of seven operations:
+// X^2 | Y^2 | Z^2, then (Y^2 - X^2) Z^2 | X^2 Y^2 | Z^4, then d X^2 Y^2.
+// Z != 0 comes back separately for the equation check.
+__device__ __forceinline__ uint32_t ge_is_sane_row(const ge_ext &p, uint32_t &z_nonzero) {
+  const fe s1 = fe_sq(fe_row_pick3(p.X, p.Y, p.Z));
+  const fe xx = fe_row_bcast<0>(s1), yy = fe_row_bcast<1>(s1), zz = fe_row_bcast<2>(s1);
+  const fe s2 = fe_mul(fe_row_pick3(fe_sub(yy, xx), xx, zz), fe_row_pick3(zz, yy, zz));
+  const fe lhs = fe_row_bcast<0>(s2), xy = fe_row_bcast<1>(s2), z4 = fe_row_bcast<2>(s2);
+  const fe dxy = fe_mul(xy, fe_d());
+  z_nonzero = fe_is_zero(p.Z) ^ 1u;
+  return fe_eq(lhs, fe_add(z4, dxy)) & z_nonzero;
+}
+
+// ge_eq_affine (Q == (x, y), Z != 0 known): x Z == X on row lane 0 and
+// y Z == Y on lane 1, one product each
+__device__ __forceinline__ uint32_t ge_eq_affine_row(const ge_ext &p, const fe &x, const fe &y, uint32_t z_nonzero) {
+  const fe t = fe_mul(fe_row_pick3(x, y, y), p.Z);
+  const uint32_t e = fe_eq(t, fe_row_pick3(p.X, p.Y, p.Y));
+  return row_bcast<0>(e) & row_bcast<1>(e) & z_nonzero;
+}
+
 __device__ __forceinline__ ge_ext ge_swap_xor(const ge_ext &p, int m) {
   ge_ext r;
   HSV_UNROLL
@@ -151,11 +180,12 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
 #ifdef HSV_TIMING_STUB_RWAVE  // tools/qc_phase_probe.py only: wrong flags, the quad path's time alone
       rx = fe_small(0);
       ry = fe_from_words_masked(rw);
-      const uint32_t r_ok = 1u;
+      const uint32_t r_ok = 1u, small = 0u;
 #else
-      const uint32_t r_ok = ge_decompress_row(rw, rx, ry, L);
+      uint32_t small;
+      const uint32_t r_ok = ge_decompress_row(rw, rx, ry, small, L);
 #endif
-      const uint32_t small_r = r_ok & y_is_small_order(ry);
+      const uint32_t small_r = r_ok & small;
       if (L.k == 0u) {
         HSV_UNROLL
         for (int l = 0; l < kFeLimbs; ++l) {
@@ -252,6 +282,9 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
   for (int mask = 1; mask < kCombLanes; mask <<= 1)
     q = ge_add_cached_rt(q, ge_to_cached(ge_swap_xor(q, mask)), mask < kCombLanes / 2);
 #endif
+  // the self-check of Q needs nothing from the R waves: before the barrier
+  uint32_t z_nonzero = 0, sane = 0;
+  if constexpr (kRowChecks) sane = ge_is_sane_row(q, z_nonzero);
   __syncthreads();
   fe rx, ry;
   HSV_UNROLL
@@ -261,7 +294,9 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
   }
   const uint32_t rf = r_fl[vl];
   const uint32_t r_ok = rf & 1u, small_r = (rf >> 1) & 1u;
-  const uint32_t same = ge_eq_affine(q, rx, ry);
+  uint32_t same;
+  if constexpr (kRowChecks) same = ge_eq_affine_row(q, rx, ry, z_nonzero);
+  else same = ge_eq_affine(q, rx, ry);
   const uint32_t kf = key_flags[kk];
   const uint32_t a_ok = (kf & kKeyAOk) ? 1u : 0u;
   const uint32_t small_a = a_ok & ((kf & kKeySmallA) ? 1u : 0u);
@@ -271,7 +306,10 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
   const uint32_t f = (strict_ok ? kStrictOk : 0u) | (eq_ok ? kEqOk : 0u) | (parse_ok ? kParseOk : 0u) |
                      (small_a ? kSmallA : 0u) | (small_r ? kSmallR : 0u) | (s_ok ? kSOk : 0u) |
                      (a_ok ? kAOk : 0u) | (r_ok ? kROk : 0u);
-  if (fault_bit(a_ok, r_ok, q)) fault[0] = 1u;  // device self-check (hsv_kernels.hip report_faults)
+  uint32_t fb;
+  if constexpr (kRowChecks) fb = a_ok & r_ok & (sane ^ 1u);
+  else fb = fault_bit(a_ok, r_ok, q) ? 1u : 0u;
+  if (fb) fault[0] = 1u;  // device self-check (hsv_kernels.hip report_faults)
   if (valid && g == 0u) flags_out[i0] = kvalid ? (uint8_t)f : (uint8_t)0;
 }
 
@@ -296,9 +334,10 @@ __global__ void __launch_bounds__(64) hsv_lanesplit_check_kernel(const uint32_t 
   bad |= fe_eq(fe_mul(a, b), fl_to_fe(fl_mul(fl_from_fe(a, L), fl_from_fe(b, L), L), L)) ? 0u : 1u;
   bad |= fe_eq(fe_pow22523(a), fl_to_fe(fl_pow22523(fl_from_fe(a, L), L), L)) ? 0u : 2u;
   fe x0, y0, x1, y1;
+  uint32_t small1;
   const uint32_t ok0 = ge_decompress(aw, x0, y0);
-  const uint32_t ok1 = ge_decompress_row(aw, x1, y1, L);
-  bad |= (ok0 == ok1 && (!ok0 || (fe_eq(x0, x1) && fe_eq(y0, y1)))) ? 0u : 4u;
+  const uint32_t ok1 = ge_decompress_row(aw, x1, y1, small1, L);
+  bad |= (ok0 == ok1 && (!ok0 || (fe_eq(x0, x1) && fe_eq(y0, y1) && y_is_small_order(y0) == small1))) ? 0u : 4u;
   if (r < rows && L.k == 0u) out[r] = bad;
 }
 

@@ -59,6 +59,27 @@ __device__ __forceinline__ uint32_t row_shl1(uint32_t x) {  // lane k <- lane k 
 }
 
 template <int I>
+__device__ __forceinline__ fe fe_row_bcast(const fe &a) {
+  fe r;
+  HSV_UNROLL
+  for (int l = 0; l < kFeLimbs; ++l) r.v[l] = row_bcast<I>(a.v[l]);
+  return r;
+}
+
+// a on row lane 0 (and 3..15), b on lane 1, c on lane 2
+__device__ __forceinline__ fe fe_row_pick3(const fe &a, const fe &b, const fe &c) {
+  fe r;
+  const uint64_t m1 = 0x0002000200020002ull, m2 = 0x0004000400040004ull;
+  HSV_UNROLL
+  for (int l = 0; l < kFeLimbs; ++l) {
+    uint32_t x;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(x) : "v"(a.v[l]), "v"(b.v[l]), "s"(m1));
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r.v[l]) : "v"(x), "v"(c.v[l]), "s"(m2));
+  }
+  return r;
+}
+
+template <int I>
 __device__ __forceinline__ void fl_mul_step(uint64_t &acc, uint32_t &gr, uint32_t f, const RowLane &L) {
   if constexpr (I > 0) gr = __umul24(row_ror1(gr), L.win);
   acc += (uint64_t)row_bcast<I>(f) * gr;
@@ -168,23 +189,38 @@ __device__ __forceinline__ fe fl_to_fe(uint32_t x, const RowLane &L) {
 // CompressedEdwardsY::decompress (ge_decompress, hsv_point.hpp) for one
 // encoding per row, every lane of the row holding it: the products of
 // sqrt_ratio_i -- y^2, d y^2, v^3, v^7, u v^7, the root chain, u v^3 (.)
-// and v r^2 -- in the row form, the sign rules on ten limbs.  Every lane of
-// the row returns the same (x, y) and flag as ge_decompress.
-__device__ __forceinline__ uint32_t ge_decompress_row(const uint32_t enc[8], fe &x, fe &y, const RowLane &L) {
+// and v r^2 -- in the row form; the sign rules on ten limbs with their
+// independent operations on separate lanes of the row (one product, then one
+// comparison per lane).  Every lane of the row returns the same (x, y),
+// flag and small-order bit as ge_decompress and y_is_small_order.
+__device__ __forceinline__ uint32_t ge_decompress_row(const uint32_t enc[8], fe &x, fe &y, uint32_t &small,
+                                                      const RowLane &L) {
   y = fe_from_words_masked(enc);
   uint32_t yl = row_limb_of_words(enc, L);
   if (L.k == 15u) yl &= 0x7fffu;  // bit 255 is the sign of x
   const uint32_t yy = fl_sq(yl, L);
   // u = y^2 - 1 as y^2 + (p - 1), limbs < 2^17.1 (a product operand may be < 2^18)
-  const uint32_t u = yy + (L.k == 0u ? 0xffecu : L.k == 15u ? 0x7fffu : 0xffffu);
+  const uint32_t ul = yy + (L.k == 0u ? 0xffecu : L.k == 15u ? 0x7fffu : 0xffffu);
   const uint32_t v = fl_mul(yy, fl_from_fe(fe_d(), L), L) + (L.k == 0u ? 1u : 0u);
   const uint32_t v3 = fl_mul(fl_sq(v, L), v, L);
   const uint32_t v7 = fl_mul(fl_sq(v3, L), v, L);
-  const uint32_t r = fl_mul(fl_mul(u, v3, L), fl_pow22523(fl_mul(u, v7, L), L), L);
-  const uint32_t check = fl_mul(v, fl_sq(r, L), L);
-  const uint32_t ok = fe_sqrt_ratio_fix_chk(fl_to_fe(u, L), fl_to_fe(check, L), fl_to_fe(r, L), x);
-  x = fe_canon(fe_select(x, fe_neg(x), enc[7] >> 31));  // -0 == 0 is accepted (no rejection)
-  return ok;
+  const uint32_t rl = fl_mul(fl_mul(ul, v3, L), fl_pow22523(fl_mul(ul, v7, L), L), L);
+  const fe check = fl_to_fe(fl_mul(v, fl_sq(rl, L), L), L);
+  const fe u = fl_to_fe(ul, L), r = fl_to_fe(rl, L);
+  // fe_sqrt_ratio_fix_chk: lane 0 -u sqrt(-1), lane 1 r sqrt(-1); then lane 0
+  // check == u, lane 1 check == -u, lane 2 check == -u sqrt(-1)
+  const fe neg_u = fe_neg(u);
+  const fe t = fe_mul(fe_row_pick3(neg_u, r, r), fe_sqrtm1());
+  const uint32_t e = fe_eq(check, fe_row_pick3(u, neg_u, fe_row_bcast<0>(t)));
+  const uint32_t correct = row_bcast<0>(e), flipped = row_bcast<1>(e), flipped_i = row_bcast<2>(e);
+  const fe rr = fe_select(r, fe_row_bcast<1>(t), flipped | flipped_i);
+  // the non-negative root, then x's sign bit (-0 == 0 is accepted): one
+  // negation decided by both, canonical; y canonical beside it on lane 1
+  const uint32_t flip = fe_is_negative(rr) ^ (enc[7] >> 31);
+  const fe c = fe_canon(fe_row_pick3(fe_select(rr, fe_neg(rr), flip), y, y));
+  x = fe_row_bcast<0>(c);
+  small = y_is_small_order_canon(fe_row_bcast<1>(c));
+  return correct | flipped;
 }
 
 }  // namespace hsv

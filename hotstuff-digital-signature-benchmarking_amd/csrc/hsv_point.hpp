@@ -218,10 +218,31 @@ HSV_INL void ge_decompress2(const uint32_t ea[8], const uint32_t eb[8], fe &xa, 
   xb = fe_canon(fe_select(xb, fe_neg(xb), eb[7] >> 31));
 }
 
-// [8]P == O  <=>  canonical y in {0, 1, p-1, y8, p-y8}  (the y values of E[8])
+// [8]P == O  <=>  canonical y in {0, 1, p-1, y8, p-y8}  (the y values of E[8]);
+// y_is_small_order_canon takes y already canonical (limbs exact, < p)
+HSV_INL uint32_t y_is_small_order_words(const uint32_t c[8]);
 HSV_INL uint32_t y_is_small_order(const fe &y) {
   uint32_t c[8];
   fe_pack(y, c);
+  return y_is_small_order_words(c);
+}
+HSV_INL uint32_t y_is_small_order_canon(const fe &y) {
+#if HSV_FE_RADIX != 26
+  return y_is_small_order(y);
+#else
+  uint32_t c[8];
+  HSV_UNROLL
+  for (int j = 0; j < 8; ++j) c[j] = 0;
+  HSV_UNROLL
+  for (int i = 0; i < 10; ++i) {  // fe_pack without its fe_canon
+    const int off = fe26_off(i), wi = off >> 5, sh = off & 31;
+    c[wi] |= y.v[i] << sh;
+    if (sh + fe26_bits(i) > 32 && wi + 1 < 8) c[wi + 1] |= y.v[i] >> (32 - sh);
+  }
+  return y_is_small_order_words(c);
+#endif
+}
+HSV_INL uint32_t y_is_small_order_words(const uint32_t c[8]) {
   const uint32_t y8[8] = {0x706a17c7u, 0x4fd84d3du, 0x760b3cbau, 0x0f67100du,
                           0xfa53202au, 0xc6cc392cu, 0x77fdc74eu, 0x7a03ac92u};
   const uint32_t py8[8] = {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u,
