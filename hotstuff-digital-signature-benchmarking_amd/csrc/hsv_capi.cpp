@@ -824,6 +824,23 @@ int hsv_init(int device) {
   Global &g = G();
   if (device >= g.ndev || device < -1) return fail(HSV_ERR_INVALID_ARG, "device index out of range");
   g.bound = device;
+  // The first slot's three pipeline streams are created now, before the
+  // application creates its own: HIP spreads streams over a few hardware
+  // queues (GPU_MAX_HW_QUEUES, 4 here), and streams created late can share a
+  // queue and so serialise.  A 2^20 host call whose streams were created
+  // after bench.py's device work took 11.0 ms against 10.3 ms
+  // (tools/host_api_late_probe.py, profiles/r03zi_host_api_late.txt).
+  static const bool eager = env_int("HSV_EAGER_STREAMS", 1) != 0;  // measurement switch
+  if (eager)
+    for (int d = device < 0 ? 0 : device; d < (device < 0 ? g.ndev : device + 1); ++d) {
+      DeviceGuard guard(d);
+      if (guard.status() != hipSuccess) continue;
+      SlotLease lease(ctx(d));
+      Slot &s = lease.slot();
+      if (!s.stream && hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) s.stream = nullptr;
+      if (s.stream) (void)slot_pipeline(s);
+      (void)hipGetLastError();
+    }
   return device < 0 ? g.ndev : 1;
 }
 
