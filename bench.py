@@ -462,12 +462,13 @@ def host_api_bench(w, dev, reps=5):
     import torch
     from hsverify import _testing, verifier
     verifier.verify_flags(w.pk, w.sig, w.msg)
-    ts, stats = [], []
+    ts, stats, marks = [], [], []
     for _ in range(reps):
         t0 = time.perf_counter()
         f = verifier.verify_flags(w.pk, w.sig, w.msg)
         ts.append(time.perf_counter() - t0)
         stats.append(_testing.host_call_stats())
+        marks.append(_testing.host_call_marks())
     k = int(np.argsort(ts)[len(ts) // 2])
     ms = float(ts[k] * 1e3)
     st = stats[k]
@@ -487,6 +488,8 @@ def host_api_bench(w, dev, reps=5):
             "call_ms": st["call_ms"], "pack_ms": st["pack_ms"], "pack_threads": _testing.pack_threads() + 1,
             "h2d_bytes": st["h2d_bytes"], "input_rate_GBps": st["h2d_bytes"] / (ms * 1e-3) / 1e9,
             "h2d_alone_ms_for_128MiB": h2d_ms, "h2d_link_GBps": nbytes / (h2d_ms * 1e-3) / 1e9,
+            "rep_ms": [round(t * 1e3, 3) for t in ts],
+            "median_call_last_launch_enqueued_ms": marks[k][-1] if marks[k] else None,
             "honest_all_accepted": bool((f[w.accept] & 1).all()),
             "corrupted_all_rejected": bool(not (f[~w.accept] & 1).any())}
 
@@ -609,6 +612,9 @@ def main():
     # contiguous shard of the global batch: rank r owns items [r*n, (r+1)*n)
     w = synth.independent_triples(a.n, seed=0xC4 * 1000 + rank, corrupt_frac=0.05, nthreads=host_threads)
     log(f"[rank {rank}] synthesized {a.n} triples in {time.perf_counter() - t0:.1f}s")
+    early_host_api = None
+    if os.environ.get("HSV_BENCH_HOST_API_EARLY") and not a.no_qc:  # diagnosis: the same leg before any device work
+        early_host_api = host_api_bench(w, torch.device("cuda", local_rank))
     pk, sig, msg = (torch.from_numpy(x).to(dev) for x in (w.pk, w.sig, w.msg))
     stream = torch.cuda.current_stream(dev)
     # Consecutive batches alternate over a.streams streams, each with its own
@@ -748,6 +754,8 @@ def main():
         # is compared with (after the other benchmarks it read 11.62 against
         # 11.21 ms on the same box, profiles/r03p_bench.json)
         out["host_api"] = host_api_bench(w, dev)
+        if early_host_api is not None:
+            out["host_api_early"] = early_host_api
     if world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(w, f, a.cpu_sample)
     if not a.no_qc:

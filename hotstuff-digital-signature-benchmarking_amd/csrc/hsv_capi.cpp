@@ -157,10 +157,28 @@ SlotLease::SlotLease(DevCtx &c) {
   lk_ = std::unique_lock<std::mutex>(s_->mu);
 }
 
+// A slot's streams are created at the greatest stream priority.  HIP spreads
+// streams over a few hardware queues per priority (GPU_MAX_HW_QUEUES, 4 on
+// the box); at normal priority a slot whose streams were created after the
+// application's own shared their queues, and the pipelined 2^20 host call
+// took 10.9-11.0 ms against 10.1-10.3 ms at the greatest priority, with the
+// application's three-stream C4 line unchanged (8.89-8.92 ms per step;
+// tools/eager_streams_ab.sh, profiles/r03zm_eager_streams_ab.txt).
+// HSV_PIPE_PRIO=0 restores normal priority (measurement switch).
+hipError_t pipe_stream_create(hipStream_t *s) {
+  static const bool prio = env_int("HSV_PIPE_PRIO", 1) != 0;
+  if (prio) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+      return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
+  }
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
 int slot_prepare(Slot &s, size_t dev_bytes, size_t host_bytes) {
   hipError_t e;
   if (!s.stream) {
-    e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+    e = pipe_stream_create(&s.stream);
     if (e != hipSuccess) return hip_fail("hipStreamCreate", e);
   }
   if (dev_bytes > s.d_cap) {
@@ -186,7 +204,7 @@ int slot_prepare(Slot &s, size_t dev_bytes, size_t host_bytes) {
 
 int slot_stream2(Slot &s) {
   if (s.stream2) return HSV_OK;
-  const hipError_t e = hipStreamCreateWithFlags(&s.stream2, hipStreamNonBlocking);
+  const hipError_t e = pipe_stream_create(&s.stream2);
   return e == hipSuccess ? HSV_OK : hip_fail("hipStreamCreate", e);
 }
 
@@ -194,7 +212,7 @@ int slot_pipeline(Slot &s) {
   int rc = slot_stream2(s);
   if (rc != HSV_OK) return rc;
   hipError_t e = hipSuccess;
-  if (!s.copy) e = hipStreamCreateWithFlags(&s.copy, hipStreamNonBlocking);
+  if (!s.copy) e = pipe_stream_create(&s.copy);
   for (int i = 0; i < 4 && e == hipSuccess; ++i)
     if (!s.ev[i]) e = hipEventCreateWithFlags(&s.ev[i], hipEventDisableTiming);
   return e == hipSuccess ? HSV_OK : hip_fail("creating the pipeline streams and events", e);
@@ -824,23 +842,6 @@ int hsv_init(int device) {
   Global &g = G();
   if (device >= g.ndev || device < -1) return fail(HSV_ERR_INVALID_ARG, "device index out of range");
   g.bound = device;
-  // The first slot's three pipeline streams are created now, before the
-  // application creates its own: HIP spreads streams over a few hardware
-  // queues (GPU_MAX_HW_QUEUES, 4 here), and streams created late can share a
-  // queue and so serialise.  A 2^20 host call whose streams were created
-  // after bench.py's device work took 11.0 ms against 10.3 ms
-  // (tools/host_api_late_probe.py, profiles/r03zi_host_api_late.txt).
-  static const bool eager = env_int("HSV_EAGER_STREAMS", 1) != 0;  // measurement switch
-  if (eager)
-    for (int d = device < 0 ? 0 : device; d < (device < 0 ? g.ndev : device + 1); ++d) {
-      DeviceGuard guard(d);
-      if (guard.status() != hipSuccess) continue;
-      SlotLease lease(ctx(d));
-      Slot &s = lease.slot();
-      if (!s.stream && hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) s.stream = nullptr;
-      if (s.stream) (void)slot_pipeline(s);
-      (void)hipGetLastError();
-    }
   return device < 0 ? g.ndev : 1;
 }
 

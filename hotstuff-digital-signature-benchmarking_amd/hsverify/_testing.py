@@ -53,6 +53,15 @@ def host_call_stats() -> dict:
     return {"pack_ms": v[0].value, "h2d_bytes": v[1].value, "call_ms": v[2].value}
 
 
+def host_call_marks() -> list:
+    """Per-chunk host marks of the calling thread's last pipelined call, ms
+    from its start: staging buffer free, packed, copy enqueued, launch
+    enqueued (4 per chunk; empty for calls below the pipeline's size)."""
+    buf = (ctypes.c_double * 256)()
+    n = _lib.load().hsv_host_call_marks(buf, 256)
+    return [round(buf[i], 4) for i in range(max(0, n))]
+
+
 def pack_threads() -> int:
     """Helper threads of the library's staging-copy pool (HSV_PACK_THREADS)."""
     return _lib.load().hsv_pack_threads()

@@ -64,3 +64,10 @@ print(json.dumps({"tag": "mad_peak", "T": probe / 1e12}), flush=True)
 host_calls("after_mad_peak")
 time.sleep(2.0)
 host_calls("after_2s_idle")
+# bench.py's own host_api leg in this process (its reps, median and marks)
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+r = bench.host_api_bench(w, dev)
+print(json.dumps({"tag": "bench_host_api_bench", "ms": r["ms"], "rep_ms": r["rep_ms"], "call_ms": r["call_ms"],
+                  "pack_ms": r["pack_ms"], "last_launch_enqueued_ms": r["median_call_last_launch_enqueued_ms"]}),
+      flush=True)
