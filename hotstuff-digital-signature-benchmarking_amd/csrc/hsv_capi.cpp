@@ -470,7 +470,7 @@ SideStreamLease::SideStreamLease(DevCtx &c) : c_(c) {
     c.side_free.pop_back();
     return;
   }
-  if (hipStreamCreateWithFlags(&s_, hipStreamNonBlocking) != hipSuccess) {
+  if (pipe_stream_create(&s_) != hipSuccess) {  // own queue pool, as the slots' streams
     s_ = nullptr;
     return;
   }
