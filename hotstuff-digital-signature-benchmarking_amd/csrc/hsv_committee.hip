@@ -105,27 +105,6 @@ constexpr bool kRowChecks = kCombLanes == 16;
 #endif
 // After the swap rounds every lane of the vote's row holds Q, and the row is a
 // DPP row, so the final checks run as rounds of one field operation per lane.
-// ge_is_sane (hsv_point.hpp) in three rounds instead of seven operations:
-// X^2 | Y^2 | Z^2, then (Y^2 - X^2) Z^2 | X^2 Y^2 | Z^4, then d X^2 Y^2.
-// Z != 0 comes back separately for the equation check.
-__device__ __forceinline__ uint32_t ge_is_sane_row(const ge_ext &p, uint32_t &z_nonzero) {
-  const fe s1 = fe_sq(fe_row_pick3(p.X, p.Y, p.Z));
-  const fe xx = fe_row_bcast<0>(s1), yy = fe_row_bcast<1>(s1), zz = fe_row_bcast<2>(s1);
-  const fe s2 = fe_mul(fe_row_pick3(fe_sub(yy, xx), xx, zz), fe_row_pick3(zz, yy, zz));
-  const fe lhs = fe_row_bcast<0>(s2), xy = fe_row_bcast<1>(s2), z4 = fe_row_bcast<2>(s2);
-  const fe dxy = fe_mul(xy, fe_d());
-  z_nonzero = fe_is_zero(p.Z) ^ 1u;
-  return fe_eq(lhs, fe_add(z4, dxy)) & z_nonzero;
-}
-
-// ge_eq_affine (Q == (x, y), Z != 0 known): x Z == X on row lane 0 and
-// y Z == Y on lane 1, one product each
-__device__ __forceinline__ uint32_t ge_eq_affine_row(const ge_ext &p, const fe &x, const fe &y, uint32_t z_nonzero) {
-  const fe t = fe_mul(fe_row_pick3(x, y, y), p.Z);
-  const uint32_t e = fe_eq(t, fe_row_pick3(p.X, p.Y, p.Y));
-  return row_bcast<0>(e) & row_bcast<1>(e) & z_nonzero;
-}
-
 __device__ __forceinline__ ge_ext ge_swap_xor(const ge_ext &p, int m) {
   ge_ext r;
   HSV_UNROLL

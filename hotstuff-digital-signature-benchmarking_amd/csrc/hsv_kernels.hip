@@ -18,6 +18,7 @@
 #include "hsv_internal.h"
 #include "hsv_verify_core.hpp"
 #include "hsv_verify_hc.hpp"
+#include "hsv_rowpoint.hpp"
 
 namespace hsv {
 
@@ -697,6 +698,106 @@ hsv_verify_pair_fused_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
   }
 }
 
+// Row form of the latency kernel (default at <= kRowMax items): every field
+// product of a verification spread over a 16-lane DPP row (hsv_rowpoint.hpp),
+// two rows per item as the pair form's two lanes.  A block of four waves takes
+// kRowItems items: waves 0-2 hold 12 rows (row 2i decompresses R of item i and
+// builds [0..8](-R), row 2i + 1 the same for A, tables in LDS), wave 3 runs the
+// scalar prepass of the block's items into an LDS record meanwhile.  After the
+// barrier each row runs its one-scalar Straus (c1 for R, |c0| for A) and half
+// of the B comb; the two rows of an item swap their sums (lane ^ 16) and add
+// them.  Fallback items (no short lattice pair) run the full-length one-lane
+// path on lane 0 of their R row.  Same flags, self-checks and canaries as the
+// pair form.
+constexpr int kRowItems = 6;
+constexpr int kRowRows = 2 * kRowItems;
+template <int WA, int CB>
+__global__ void __launch_bounds__(4 * 64)
+hsv_verify_row_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const uint8_t *__restrict__ sig,
+                      uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
+                      uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
+                      uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b, int lat_bits,
+                      uint32_t *__restrict__ canary, uint32_t nonce, uint32_t inject, uint32_t *__restrict__ fault) {
+  using G = HalfCombWindows<WA>;
+  constexpr int TS = 1 << (WA - 1);
+  constexpr int kEnt = TS + 1;
+  __shared__ uint32_t srec[kPrepWords * kRowItems];
+  __shared__ uint32_t stab[kRowRows * kEnt * 64];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint32_t base = blockIdx.x * kRowItems;
+  if (wave == 3) {
+    if (lane < (uint32_t)kRowItems) {
+      const uint32_t li = base + lane < n ? base + lane : n - 1u;
+      uint32_t pkw[8], sigw[16], msgw[8];
+      load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, li, pkw, sigw, msgw);
+      (void)prep_scalars<WA>(pkw, sigw, msgw, srec + lane, kRowItems, lat_bits);
+    }
+    __syncthreads();
+    return;
+  }
+  const RowLane L;
+  const uint32_t rb = wave * 4u + (lane >> 4);  // row of the block
+  const uint32_t il = rb >> 1, role = rb & 1u;  // role 0: R, 1: A
+  const uint32_t item = base + il;
+  const uint32_t li = item < n ? item : n - 1u;
+  const uint32_t slot = blockIdx.x * (uint32_t)kRowRows + rb;
+  canary[slot] = inject == kInjectCanary ? ~nonce : nonce;
+  uint32_t ok, small;
+  uint32_t *tab = stab + rb * (uint32_t)(kEnt * 64);
+  {
+    uint32_t enc[8];
+    const uint4 *ep = reinterpret_cast<const uint4 *>(role ? pk + (uint64_t)li * pk_stride : sig + (uint64_t)li * sig_stride);
+    const uint4 e0 = ep[0], e1 = ep[1];
+    enc[0] = e0.x; enc[1] = e0.y; enc[2] = e0.z; enc[3] = e0.w;
+    enc[4] = e1.x; enc[5] = e1.y; enc[6] = e1.z; enc[7] = e1.w;
+    fe x, y;
+    ok = ge_decompress_row(enc, x, y, small, L);
+    small &= ok;
+    row_table_build<TS>(tab, x, y, L, inject, role == 0u);
+  }
+  __syncthreads();
+  const uint32_t meta = srec[(kPrepWords - 1) * kRowItems + il];
+  uint32_t f = 0, bad = 0;
+  if (meta & kPrepFallback) {
+    if (role == 0u && L.k == 0u) {
+      GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)slot * vt_lane_uint4<WA>(), inject};
+      uint32_t pkw[8], sigw[16], msgw[8];
+      load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, li, pkw, sigw, msgw);
+      f = verify_one_full_comb<WA, false, CB>(pkw, sigw, msgw, comb_b, vt);
+      bad = (f & kFault) ? 1u : 0u;
+    }
+  } else {
+    uint32_t d[5];
+    HSV_UNROLL
+    for (int i = 0; i < 5; ++i) d[i] = srec[(i + 5 * (int)role) * kRowItems + il];
+    rp_ext q = row_straus<WA, G::NW>(d, tab, (role && (meta & kPrepC0Neg)) ? 1u : 0u, L);
+    uint32_t b[8];
+    HSV_UNROLL
+    for (int i = 0; i < 8; ++i) b[i] = srec[(10 + i) * kRowItems + il];
+    q = row_comb_half<CB>(q, b, comb_b, role, L);
+    // both rows of the item end with the whole sum Q
+    q = rp_add_cached(q, rp_to_cached(rp_swap_rows(q), fl_from_fe(fe_d2(), L), L), false, L);
+    const uint32_t ok_o = (uint32_t)__shfl_xor((int)ok, 16, 64), small_o = (uint32_t)__shfl_xor((int)small, 16, 64);
+    const uint32_t r_ok = role ? ok_o : ok, small_r = role ? small_o : small;
+    const uint32_t a_ok = role ? ok : ok_o, small_a = role ? small : small_o;
+    ge_ext qe;
+    qe.X = fl_to_fe(q.X, L);
+    qe.Y = fl_to_fe(q.Y, L);
+    qe.Z = fl_to_fe(q.Z, L);
+    qe.T = qe.Z;
+    uint32_t z_nonzero;
+    const uint32_t sane = ge_is_sane_row(qe, z_nonzero);
+    const uint32_t same = fe_is_zero(qe.X) & fe_eq(qe.Y, qe.Z) & z_nonzero;  // ge_is_neutral
+    f = flags_byte(meta & kPrepSOk, a_ok, r_ok, small_a, small_r, same);
+    bad = (a_ok & r_ok & (sane ^ 1u)) ? 1u : 0u;
+  }
+  report_faults(fault, bad | (canary[slot] != nonce ? 2u : 0u));
+  if (item < n && role == 0u && L.k == 0u) {
+    if (flags_out) flags_out[item] = (uint8_t)f;
+    if (strict_bits && (f & kStrictOk)) atomicOr(&strict_bits[item >> 5], 1u << (item & 31u));
+  }
+}
+
 #if HSV_ALL_VARIANTS
 // Point pass with a pair-lane tail (variant 22): as hsv_verify_hp_kernel, but
 // the last n_tail items (a multiple-of-64 boundary, about one round of the
@@ -1084,6 +1185,12 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
 // launches; at 2^12 items the pair form is 27 % faster end to end than the
 // point pass, at 2^15 7 % slower (profiles/r01o_qc_latency.json).
 constexpr uint32_t kPairMax = 1u << 13;
+// The row form at or below this many items.  p50 of a generic call, row /
+// pair form (tools/row_cutover_probe.py, profiles/r03zp_row_cutover.txt):
+// 0.216 / 0.450 ms at 64 items, 0.226 / 0.466 at 1024, 0.230 / 0.467 at 1536
+// (256 blocks of four waves: one block per CU), 0.422 / 0.470 at 2048, 0.427 /
+// 0.477 at 3072, 0.626 / 0.487 at 4096.
+constexpr uint32_t kRowMaxDefault = 3072;
 
 template <int WA, int CB>
 hipError_t launch_pair(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
@@ -1115,6 +1222,46 @@ hipError_t launch_pair(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig
   return e != hipSuccess ? e : ef;
 }
 
+// Row form (variant 21 at <= row_max() items): kRowItems items per block of
+// four waves.  The workspace holds one full-length table and one canary per
+// row (the fallback path's tables; the row tables live in LDS).
+uint32_t row_max() {  // HSV_ROW_MAX: measurement switch (0: always the pair form)
+  static const uint32_t m = [] {
+    const char *v = std::getenv("HSV_ROW_MAX");
+    return v ? (uint32_t)std::atoi(v) : kRowMaxDefault;
+  }();
+  return m;
+}
+
+template <int WA, int CB>
+hipError_t launch_row(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
+                      const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
+                      uint32_t *strict_bits, const uint32_t *comb_b, uint32_t *fault, hipStream_t stream,
+                      void *ws_in = nullptr, size_t ws_cap = 0, size_t *ws_need = nullptr) {
+  const uint32_t grid = (n + hsv::kRowItems - 1) / hsv::kRowItems;
+  const size_t slots = (size_t)grid * hsv::kRowRows;
+  const size_t ws_bytes = slots * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
+  const size_t need = ws_bytes + slots * sizeof(uint32_t);
+  if (ws_need) {
+    *ws_need = need;
+    return hipSuccess;
+  }
+  void *ws = ws_in && ws_cap >= need ? ws_in : nullptr;
+  const bool own = ws == nullptr;
+  hipError_t e = own ? hsv_ws_malloc(&ws, need, stream) : hipSuccess;
+  if (e != hipSuccess) return e;
+  if (strict_bits) e = hipMemsetAsync(strict_bits, 0, (size_t)((n + 31u) / 32u) * 4u, stream);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL((hsv::hsv_verify_row_kernel<WA, CB>), dim3(grid), dim3(4 * 64), 0, stream, pk, pk_stride,
+                       sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, static_cast<uint4 *>(ws), comb_b,
+                       g_lat_bits.load(), reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(ws) + ws_bytes),
+                       next_nonce(), g_inject.load(), fault);
+    e = hipGetLastError();
+  }
+  const hipError_t ef = own ? hipFreeAsync(ws, stream) : hipSuccess;
+  return e != hipSuccess ? e : ef;
+}
+
 }  // namespace
 
 extern "C" hipError_t hsv_launch_verify_ws(int variant, const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig,
@@ -1126,6 +1273,9 @@ extern "C" hipError_t hsv_launch_verify_ws(int variant, const uint8_t *pk, uint6
     return hsv_launch_verify(variant, pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits,
                              comb_b, fault, stream);
   if (!comb_b || !fault) return hipErrorInvalidValue;
+  if (variant == 21 && n <= row_max())
+    return launch_row<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b,
+                             fault, stream, ws, ws_cap);
   if (variant == 21 && n <= kPairMax)
     return launch_pair<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b,
                               fault, stream, ws, ws_cap);
@@ -1135,7 +1285,10 @@ extern "C" hipError_t hsv_launch_verify_ws(int variant, const uint8_t *pk, uint6
 
 extern "C" size_t hsv_launch_ws_bytes(int variant, uint32_t n) {
   size_t need = 0;
-  if (variant == 21 && n <= kPairMax)
+  if (variant == 21 && n <= row_max())
+    (void)launch_row<4, 16>(nullptr, 0, nullptr, 0, nullptr, 0, n, nullptr, nullptr, nullptr, nullptr, nullptr,
+                            nullptr, 0, &need);
+  else if (variant == 21 && n <= kPairMax)
     (void)launch_pair<4, 16>(nullptr, 0, nullptr, 0, nullptr, 0, n, nullptr, nullptr, nullptr, nullptr, nullptr,
                              nullptr, 0, &need);
   else if (variant == 19 || variant == 21)
@@ -1157,6 +1310,9 @@ extern "C" hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t
       return launch_hp<4, 3, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b,
                                  fault, stream);
     case 21:
+      if (n <= row_max())
+        return launch_row<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b,
+                                 fault, stream);
       if (n <= kPairMax)
         return launch_pair<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b,
                                   fault, stream);

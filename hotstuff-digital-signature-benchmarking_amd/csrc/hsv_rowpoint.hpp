@@ -1,0 +1,199 @@
+// Edwards25519 point arithmetic in the row form (hsv_fe16x16.hpp): one
+// point per 16-lane DPP row, lane k holding limb k of each coordinate.  The
+// formulas are hsv_point.hpp's (HWCD, complete for a = -1), operation for
+// operation, so the row kernels compute exactly what the one-lane kernels do.
+//
+// Operand bounds (limbs; tools/lanesplit_model.py replays these sequences on
+// worst-case limbs, tests/test_lanesplit.py):
+//   * a product's output is <= 2^16.3 when its operands are < 2^18.75 (the
+//     model's largest over these formulas: 2^16.23);
+//   * a - b is a + 4p - b (4p = 2^257 - 76 as limbs 0x1ffb4, 0x1fffe, ...,
+//     each >= 2^17 - 76): b must be a product output;
+//   * every product operand is a product output, a sum of two of them, or
+//     one difference (< 2^18.4), below the 2^18.75 the rotated operand of
+//     fl_mul allows (its limb times 38 feeds v_mul_u32_u24);
+//   * the doubling's F (2 Z^2 + X^2 - Y^2) gets one carry pass, as in
+//     ge_dbl_rt (fe_carry).
+#pragma once
+#include "hsv_fe16x16.hpp"
+#include "hsv_verify_hc.hpp"
+
+#if defined(__HIPCC__)
+namespace hsv {
+
+struct rp_ext {
+  uint32_t X, Y, Z, T;
+};
+struct rp_cached {
+  uint32_t YpX, YmX, Z2, T2d;
+};
+
+__device__ __forceinline__ uint32_t fl_small(uint32_t v, const RowLane &L) { return L.k == 0u ? v : 0u; }
+__device__ __forceinline__ uint32_t fl_4p(const RowLane &L) { return L.k == 0u ? 0x1ffb4u : 0x1fffeu; }
+// a - b (b a product output)
+__device__ __forceinline__ uint32_t fl_sub(uint32_t a, uint32_t b, const RowLane &L) { return a + fl_4p(L) - b; }
+// one carry pass (limbs < 2^24 in, <= 2^16 + 38 * 2^8 out)
+__device__ __forceinline__ uint32_t fl_carry(uint32_t x, const RowLane &L) {
+  return (x & 0xffffu) + row_ror1(__umul24(x >> 16, L.wout));
+}
+
+__device__ __forceinline__ rp_ext rp_identity(const RowLane &L) {
+  return rp_ext{0u, fl_small(1, L), fl_small(1, L), 0u};
+}
+
+// X3 = E F, Y3 = G H, Z3 = F G, T3 = E H (ge_finish_rt); without T, T is 0
+__device__ __forceinline__ rp_ext rp_finish(uint32_t E, uint32_t F, uint32_t G, uint32_t H, bool with_t,
+                                            const RowLane &L) {
+  rp_ext r;
+  r.X = fl_mul(E, F, L);
+  r.Y = fl_mul(G, H, L);
+  r.Z = fl_mul(F, G, L);
+  r.T = with_t ? fl_mul(E, H, L) : 0u;
+  return r;
+}
+
+// 2P (ge_dbl_rt)
+__device__ __forceinline__ rp_ext rp_dbl(const rp_ext &p, bool with_t, const RowLane &L) {
+  const uint32_t A = fl_sq(p.X, L), B = fl_sq(p.Y, L), C = fl_sq(p.Z, L), S = fl_sq(p.X + p.Y, L);
+  const uint32_t H = A + B;
+  const uint32_t E = fl_sub(H, S, L);
+  const uint32_t G = fl_sub(A, B, L);
+  const uint32_t F = fl_carry(C + C + G, L);
+  return rp_finish(E, F, G, H, with_t, L);
+}
+
+// P + Q, Q cached (ge_add_cached_rt)
+__device__ __forceinline__ rp_ext rp_add_cached(const rp_ext &p, const rp_cached &q, bool with_t, const RowLane &L) {
+  const uint32_t A = fl_mul(fl_sub(p.Y, p.X, L), q.YmX, L);
+  const uint32_t B = fl_mul(p.Y + p.X, q.YpX, L);
+  const uint32_t C = fl_mul(p.T, q.T2d, L);
+  const uint32_t D = fl_mul(p.Z, q.Z2, L);
+  return rp_finish(fl_sub(B, A, L), fl_sub(D, C, L), D + C, B + A, with_t, L);
+}
+
+// P + Q, Q affine Niels (y + x, y - x, 2dxy) (ge_add_niels)
+__device__ __forceinline__ rp_ext rp_add_niels(const rp_ext &p, uint32_t ypx, uint32_t ymx, uint32_t xy2d,
+                                               bool with_t, const RowLane &L) {
+  const uint32_t A = fl_mul(fl_sub(p.Y, p.X, L), ymx, L);
+  const uint32_t B = fl_mul(p.Y + p.X, ypx, L);
+  const uint32_t C = fl_mul(p.T, xy2d, L);
+  const uint32_t D = p.Z + p.Z;
+  return rp_finish(fl_sub(B, A, L), fl_sub(D, C, L), D + C, B + A, with_t, L);
+}
+
+__device__ __forceinline__ rp_cached rp_to_cached(const rp_ext &p, uint32_t d2, const RowLane &L) {
+  return rp_cached{p.Y + p.X, fl_sub(p.Y, p.X, L), p.Z + p.Z, fl_mul(p.T, d2, L)};
+}
+
+// The row's point from the partner row (lane ^ 16: rows 0 <-> 1, 2 <-> 3)
+__device__ __forceinline__ rp_ext rp_swap_rows(const rp_ext &p) {
+  return rp_ext{(uint32_t)__shfl_xor((int)p.X, 16, 64), (uint32_t)__shfl_xor((int)p.Y, 16, 64),
+                (uint32_t)__shfl_xor((int)p.Z, 16, 64), (uint32_t)__shfl_xor((int)p.T, 16, 64)};
+}
+
+// ---- the per-row variable-base table in LDS --------------------------------
+// Entries m = 0..TS of [m](-P), cached form, at tab[(m * 4 + c) * 16 + k]
+// (c: YpX, YmX, Z2, T2d); entry 0 is the identity.  Built as
+// [m](-P) = [m-1](-P) + (-P) with -P in affine Niels form, as vt_build.
+// inject (tests): entries 1.. stored as zeros, or with one bit flipped when
+// flip_this_table (the pair kernel's table 0, R).
+template <int TS>
+__device__ __forceinline__ void row_table_build(uint32_t *tab, const fe &x, const fe &y, const RowLane &L,
+                                                uint32_t inject, bool flip_this_table) {
+  const uint32_t nx = fl_from_fe(fe_carry(fe_neg(x)), L);  // -x
+  const uint32_t yl = fl_from_fe(y, L);
+  const uint32_t d2 = fl_from_fe(fe_d2(), L);
+  const uint32_t t1 = fl_mul(nx, yl, L);
+  const uint32_t ypx = yl + nx, ymx = fl_sub(yl, nx, L), xy2d = fl_mul(t1, d2, L);
+  auto put = [&](int m, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    if (m > 0 && inject == kInjectZeroTables) a = b = c = d = 0u;
+    if (m > 0 && inject == kInjectFlipTables && flip_this_table && L.k == 0u) a ^= 1u;
+    tab[(m * 4 + 0) * 16 + L.k] = a;
+    tab[(m * 4 + 1) * 16 + L.k] = b;
+    tab[(m * 4 + 2) * 16 + L.k] = c;
+    tab[(m * 4 + 3) * 16 + L.k] = d;
+  };
+  put(0, fl_small(1, L), fl_small(1, L), fl_small(2, L), 0u);
+  put(1, ypx, ymx, fl_small(2, L), xy2d);
+  rp_ext p{nx, yl, fl_small(1, L), t1};
+  HSV_NOUNROLL
+  for (int m = 2; m <= TS; ++m) {
+    p = rp_add_niels(p, ypx, ymx, xy2d, true, L);
+    const rp_cached c = rp_to_cached(p, d2, L);
+    put(m, c.YpX, c.YmX, c.Z2, c.T2d);
+  }
+}
+
+// entry m of the row's table, negated when neg (swap Y+X / Y-X, -2dT)
+__device__ __forceinline__ rp_cached row_table_entry(const uint32_t *tab, uint32_t m, uint32_t neg,
+                                                     const RowLane &L) {
+  const uint32_t *e = tab + m * 64u + L.k;
+  const uint32_t a = e[0], b = e[16], z2 = e[32], t = e[48];
+  return rp_cached{neg ? b : a, neg ? a : b, z2, neg ? fl_sub(0u, t, L) : t};
+}
+
+// One-scalar Straus over the row's table: the digit registers d (5 words,
+// top window at the top bits, as recode_top5) of NW windows of WA bits;
+// flip negates every digit.  Leading windows whose digits are zero in every
+// row of the wave are skipped (wave-uniform).  T is valid on return.
+template <int WA, int NW>
+__device__ __forceinline__ rp_ext row_straus(uint32_t d[5], const uint32_t *tab, uint32_t flip, const RowLane &L) {
+  constexpr int TS = 1 << (WA - 1);
+  rp_ext q = rp_identity(L);
+  int top = NW - 1;
+  HSV_NOUNROLL
+  while (top > 0) {
+    if (__ballot(((d[4] >> (32 - WA)) ^ (uint32_t)TS) != 0u)) break;
+    limbs_shl<5>(d, WA);
+    --top;
+  }
+  HSV_NOUNROLL
+  for (int i = top; i >= 0; --i) {
+    uint32_t neg;
+    const uint32_t m = digit_mag<TS>(d[4] >> (32 - WA), neg);
+    limbs_shl<5>(d, WA);
+    if (i != top) {
+      HSV_NOUNROLL
+      for (int j = 0; j < WA; ++j) q = rp_dbl(q, j == WA - 1, L);
+    }
+    q = rp_add_cached(q, row_table_entry(tab, m, neg ^ flip, L), i == 0, L);
+  }
+  return q;
+}
+
+// q + the comb digits of half h of s (comb_add_b_half): positions
+// [h NP/2, (h+1) NP/2) of the CB-bit comb table tb; each lane reads its 16-bit
+// limb of the entry's three packed coordinates.
+template <int CB>
+__device__ __forceinline__ rp_ext row_comb_half(rp_ext q, const uint32_t s[8], const uint32_t *tb, uint32_t h,
+                                                const RowLane &L) {
+  constexpr int NP = 256 / CB, HALF = NP / 2;
+  constexpr int ENT = 1 << (CB - 1);
+  uint32_t sr[9];
+  recode_add<9, CB, NP>(s, 8, sr);
+  HSV_UNROLL
+  for (int i = 0; i < 4; ++i) sr[i] = h ? sr[i + 4] : sr[i];
+  const uint32_t wsel = L.k >> 1, hs = (L.k & 1u) * 16u;
+  HSV_NOUNROLL
+  for (int j = 0; j < HALF; ++j) {
+    const uint32_t cb = sr[0] & ((1u << CB) - 1u);
+    HSV_UNROLL
+    for (int i = 0; i < 3; ++i) sr[i] = (sr[i] >> CB) | (sr[i + 1] << (32 - CB));
+    sr[3] >>= CB;
+    const int32_t dg = (int32_t)cb - (1 << (CB - 1));
+    const uint32_t neg = dg < 0, mag = (uint32_t)(neg ? -dg : dg);
+    const uint32_t idx = mag == 0u ? 0u : mag - 1u;
+    const uint32_t *e = tb + ((uint64_t)(j + (int)h * HALF) * ENT + idx) * kCombEntryWords;
+    uint32_t a = (e[wsel] >> hs) & 0xffffu, b = (e[8 + wsel] >> hs) & 0xffffu, c = (e[16 + wsel] >> hs) & 0xffffu;
+    if (mag == 0u) {
+      a = fl_small(1, L);
+      b = fl_small(1, L);
+      c = 0u;
+    }
+    q = rp_add_niels(q, neg ? b : a, neg ? a : b, neg ? fl_sub(0u, c, L) : c, true, L);
+  }
+  return q;
+}
+
+}  // namespace hsv
+#endif

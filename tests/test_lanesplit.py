@@ -30,6 +30,12 @@ def test_row_product_bounds_model():
     assert st["acc"] < 2**43
 
 
+def test_row_point_formula_bounds_model():
+    import lanesplit_model
+    st = lanesplit_model.run_points(trials=40, seed=11)
+    assert st["out"] < 2**16.3
+
+
 def _words(v):
     return [(v >> (32 * i)) & 0xFFFFFFFF for i in range(8)]
 

@@ -85,6 +85,102 @@ def run(trials=400, seed=1):
     return st
 
 
+
+# ---- the row-form point formulas (csrc/hsv_rowpoint.hpp), bounds only ----
+FOURP = [0x1FFB4] + [0x1FFFE] * 15
+assert value(FOURP) == 4 * P
+
+
+def fl_add(a, b):
+    return [x + y for x, y in zip(a, b)]
+
+
+def fl_sub(a, b):
+    assert all(y <= q for y, q in zip(b, FOURP)), "fl_sub subtrahend above 4p's limbs"
+    return [x + q - y for x, y, q in zip(a, b, FOURP)]
+
+
+def fl_carry(x):
+    assert max(x) < 2**24
+    lo = [a & 0xFFFF for a in x]
+    t = [(a >> 16) * (38 if k == 15 else 1) for k, a in enumerate(x)]
+    return [lo[k] + t[(k - 1) % 16] for k in range(16)]
+
+
+def rp_finish(E, F, G, H, st):
+    return (fl_mul(E, F, st), fl_mul(G, H, st), fl_mul(F, G, st), fl_mul(E, H, st))
+
+
+def rp_dbl(p, st):
+    X, Y, Z, _ = p
+    A, B, C, S = fl_mul(X, X, st), fl_mul(Y, Y, st), fl_mul(Z, Z, st), fl_mul(fl_add(X, Y), fl_add(X, Y), st)
+    H = fl_add(A, B)
+    E = fl_sub(H, S)
+    G = fl_sub(A, B)
+    F = fl_carry(fl_add(fl_add(C, C), G))
+    return rp_finish(E, F, G, H, st)
+
+
+def rp_add_cached(p, q, st):
+    X, Y, Z, T = p
+    YpX, YmX, Z2, T2d = q
+    A = fl_mul(fl_sub(Y, X), YmX, st)
+    B = fl_mul(fl_add(Y, X), YpX, st)
+    C = fl_mul(T, T2d, st)
+    D = fl_mul(Z, Z2, st)
+    return rp_finish(fl_sub(B, A), fl_sub(D, C), fl_add(D, C), fl_add(B, A), st)
+
+
+def rp_add_niels(p, n, st):
+    X, Y, Z, T = p
+    ypx, ymx, xy2d = n
+    A = fl_mul(fl_sub(Y, X), ymx, st)
+    B = fl_mul(fl_add(Y, X), ypx, st)
+    C = fl_mul(T, xy2d, st)
+    D = fl_add(Z, Z)
+    return rp_finish(fl_sub(B, A), fl_sub(D, C), fl_add(D, C), fl_add(B, A), st)
+
+
+def rp_to_cached(p, d2, st):
+    X, Y, Z, T = p
+    return (fl_add(Y, X), fl_sub(Y, X), fl_add(Z, Z), fl_mul(T, d2, st))
+
+
+def run_points(trials=60, seed=3):
+    """Doublings, cached and Niels additions, negated entries and table
+    builds on worst-case and random limbs: every fl_mul / fl_sub bound holds."""
+    rnd = random.Random(seed)
+    st = {}
+    top = 0x1A000  # a product output's lane-0 limb can reach ~2^16.7
+
+    def elem(hi=0xFFFF):
+        return [rnd.choice([0, hi, rnd.randrange(hi + 1)]) for _ in range(16)]
+
+    def prod():  # a product output (worst case: large lane-0 limb)
+        x = elem()
+        x[0] = rnd.choice([x[0], top])
+        return x
+
+    d2 = limbs_of(2 * (-121665 * pow(121666, P - 2, P)) % P)
+    for _ in range(trials):
+        p = (prod(), prod(), prod(), prod())
+        for _ in range(4):
+            p = rp_dbl(p, st)
+        c = (fl_add(prod(), prod()), fl_sub(prod(), prod()), fl_add(prod(), prod()), prod())
+        p = rp_add_cached(p, c, st)
+        neg = (c[1], c[0], c[2], fl_sub([0] * 16, c[3]))
+        p = rp_add_cached(p, neg, st)
+        n = (elem(), elem(), elem())
+        p = rp_add_niels(p, n, st)
+        p = rp_add_niels(p, (n[1], n[0], fl_sub([0] * 16, n[2])), st)
+        p = rp_add_cached(p, rp_to_cached(p, d2, st), st)
+        for _ in range(2):
+            p = rp_dbl(p, st)
+    return st
+
+
 if __name__ == "__main__":
     st = run()
-    print({k: round(math.log2(v), 4) for k, v in st.items()})
+    print("products", {k: round(math.log2(v), 4) for k, v in st.items()})
+    st = run_points()
+    print("point formulas", {k: round(math.log2(v), 4) for k, v in st.items()})

@@ -18,7 +18,7 @@ CHILD = r"""
 import json, sys
 sys.path.insert(0, {root!r}); sys.path.insert(0, {root!r} + "/hotstuff-digital-signature-benchmarking_amd")
 import bench
-r = bench.qc_latency({reps}, auto=True)
+r = bench.qc_latency({reps}, auto={auto})
 print(json.dumps({{k: v["p50_ms"] for k, v in r.items() if isinstance(v, dict)}}))
 """
 
@@ -27,13 +27,22 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--reps", type=int, default=200)
+    ap.add_argument("--generic", action="store_true", help="committee cache off: the generic kernels")
+    ap.add_argument("--env", action="append", default=[],
+                    help="NAME=VALUE for every child (repeatable); a LIB argument of the form "
+                         "lib.so:NAME=VALUE sets NAME for that run only")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     res = {lib: [] for lib in a.libs}
     for _ in range(a.rounds):
         for lib in a.libs:
-            r = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT, reps=a.reps)], capture_output=True,
-                               text=True, timeout=300, env=dict(os.environ, HSV_LIB=lib))
+            name, _, extra = lib.partition(":")
+            env = dict(os.environ, HSV_LIB=name)
+            for kv in a.env + ([extra] if extra else []):
+                k, _, v = kv.partition("=")
+                env[k] = v
+            r = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT, reps=a.reps, auto=not a.generic)],
+                               capture_output=True, text=True, timeout=300, env=env)
             if r.returncode != 0:
                 print(r.stdout, r.stderr[-2000:])
                 return r.returncode

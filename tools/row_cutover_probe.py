@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Cut-over between the row-form latency kernel and the pair form: p50 of a
+generic hsv_verify call (committee cache off) at several batch sizes, one
+process with the row form forced (HSV_ROW_MAX=1<<13) and one with it off
+(HSV_ROW_MAX=0).
+
+python tools/row_cutover_probe.py
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHILD = r"""
+import json, sys, time
+import numpy as np
+sys.path.insert(0, {root!r} + "/hotstuff-digital-signature-benchmarking_amd")
+from hsverify import _lib, synth, verifier
+lib = _lib.load()
+lib.hsv_set_auto_committee(0)
+w = synth.independent_triples(8192, seed=77, corrupt_frac=0.05, nthreads=16)
+out = {{}}
+for n in (64, 256, 512, 1024, 1536, 2048, 3072, 4096, 8192):
+    args = (w.pk[:n], w.sig[:n], w.msg[:n])
+    for _ in range(5):
+        verifier.verify_flags(*args)
+    ts = []
+    for _ in range(60):
+        t0 = time.perf_counter()
+        verifier.verify_flags(*args)
+        ts.append(time.perf_counter() - t0)
+    out[n] = round(float(np.median(ts)) * 1e3, 4)
+print(json.dumps(out))
+"""
+
+
+def main():
+    for rnd in range(2):
+        for rm in ("8192", "0"):
+            r = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT)], capture_output=True, text=True,
+                               timeout=600, env=dict(os.environ, HSV_ROW_MAX=rm))
+            line = r.stdout.strip().splitlines()[-1] if r.returncode == 0 else f"rc={r.returncode} {r.stderr[-400:]}"
+            print(json.dumps({"HSV_ROW_MAX": rm, "p50_ms_by_n": line}), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
