@@ -41,14 +41,16 @@ def generic(env):
 def test_generic_paths_report_faults(env, generic, mode):
     _lib, _testing, crypto, synth, verifier = env
     lib = _lib.load()
-    w = synth.qc_votes(100, seed=5)                                # 67 votes, pair latency kernel
+    w = synth.qc_votes(100, seed=5)                                # 67 votes, row-form latency kernel
+    mid = synth.independent_triples(4096, seed=8, corrupt_frac=0.0)  # pair latency kernel (3073..8192)
     big = synth.independent_triples((1 << 13) + 64, seed=6, corrupt_frac=0.0)  # point-pass kernels
     packed = np.concatenate([w.pk, w.sig], axis=1).copy()
     want_small = verifier.verify_flags(w.pk, w.sig, w.msg)
+    want_mid = verifier.verify_flags(mid.pk, mid.sig, mid.msg)
     want_big = verifier.verify_flags(big.pk, big.sig, big.msg)
-    assert (want_small & 1).all() and (want_big & 1).all()
+    assert (want_small & 1).all() and (want_mid & 1).all() and (want_big & 1).all()
     with _testing.injected_fault(mode):
-        for pk, sig, msg in ((w.pk, w.sig, w.msg), (big.pk, big.sig, big.msg)):
+        for pk, sig, msg in ((w.pk, w.sig, w.msg), (mid.pk, mid.sig, mid.msg), (big.pk, big.sig, big.msg)):
             with pytest.raises(_lib.HsvLibraryError, match="HSV_ERR_DEVICE_FAULT"):
                 verifier.verify_flags(pk, sig, msg)
         assert lib.hsv_verify_batch_packed(w.msg.tobytes(), packed.tobytes(), w.n) == FAULT
@@ -61,6 +63,7 @@ def test_generic_paths_report_faults(env, generic, mode):
             crypto.Signature.verify_batch(crypto.Digest(w.msg.tobytes()), votes)
     # injection off: the same calls verify again, nothing stale in the slots
     assert (verifier.verify_flags(w.pk, w.sig, w.msg) == want_small).all()
+    assert (verifier.verify_flags(mid.pk, mid.sig, mid.msg) == want_mid).all()
     assert (verifier.verify_flags(big.pk, big.sig, big.msg) == want_big).all()
     assert lib.hsv_verify_batch_packed(w.msg.tobytes(), packed.tobytes(), w.n) == 1
 
