@@ -167,7 +167,9 @@ __device__ __forceinline__ fe fl_to_fe(uint32_t x, const RowLane &L) {
   const uint32_t sh = L.k == 15u ? 15u : 16u;
   const uint32_t mask = (1u << sh) - 1u;
   const uint32_t w19 = L.k == 15u ? 19u : 1u;
-  for (;;) {
+  // at most 17 passes carry anything (a carry can ripple once round the row);
+  // the cap keeps the loop finite whatever the limbs hold
+  for (int pass = 0; pass < 20; ++pass) {
     const uint32_t t = x >> sh;
     x = (x & mask) + row_ror1(__umul24(t, w19));
     if (!__ballot(t != 0u)) break;
