@@ -42,13 +42,59 @@ struct Reader {
   }
 };
 
-int b64_value(uint8_t c) {
-  if (c >= 'A' && c <= 'Z') return c - 'A';
-  if (c >= 'a' && c <= 'z') return c - 'a' + 26;
-  if (c >= '0' && c <= '9') return c - '0' + 52;
-  if (c == '+') return 62;
-  if (c == '/') return 63;
-  return -1;
+// base64 standard alphabet: value of each byte, 0xff for none
+struct B64Table {
+  uint8_t v[256];
+  B64Table() {
+    std::memset(v, 0xff, sizeof(v));
+    const char *a = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+    for (int i = 0; i < 64; ++i) v[(uint8_t)a[i]] = (uint8_t)i;
+  }
+};
+const B64Table kB64;
+
+// Decodes s[0, n) under b64_decode's rules, keeping the first `keep` bytes in
+// out; returns the decoded length, or -1 for an invalid string.
+long b64_decode_prefix(const uint8_t *s, size_t n, uint8_t *out, size_t keep) {
+  size_t end = n;
+  while (end > 0 && s[end - 1] == '=') --end;
+  if (n - end > 2) return -1;
+  if (n != end && n % 4 != 0) return -1;  // padded input comes in whole quads
+  const size_t rem = end % 4;
+  if (rem == 1) return -1;
+  size_t o = 0, i = 0;
+  uint8_t bad = 0;
+  for (; i + 4 <= end; i += 4) {  // whole quads: 3 bytes each
+    const uint8_t a = kB64.v[s[i]], b = kB64.v[s[i + 1]], c = kB64.v[s[i + 2]], d = kB64.v[s[i + 3]];
+    bad |= a | b | c | d;
+    const uint32_t q = ((uint32_t)a << 18) | ((uint32_t)b << 12) | ((uint32_t)c << 6) | d;
+    if (o + 3 <= keep) {
+      out[o] = (uint8_t)(q >> 16);
+      out[o + 1] = (uint8_t)(q >> 8);
+      out[o + 2] = (uint8_t)q;
+    } else {
+      for (int k = 0; k < 3; ++k)
+        if (o + k < keep) out[o + k] = (uint8_t)(q >> (16 - 8 * k));
+    }
+    o += 3;
+  }
+  if (bad & 0xc0) return -1;  // a byte outside the alphabet (0xff) in a quad
+  uint32_t acc = 0;
+  int bits = 0;
+  for (; i < end; ++i) {  // the last 2 or 3 characters
+    const uint8_t v = kB64.v[s[i]];
+    if (v > 63) return -1;
+    acc = (acc << 6) | v;
+    bits += 6;
+    if (bits >= 8) {
+      bits -= 8;
+      if (o < keep) out[o] = (uint8_t)(acc >> bits);
+      ++o;
+      acc &= (1u << bits) - 1u;
+    }
+  }
+  if (acc != 0) return -1;  // the leftover (trailing) bits must be zero
+  return (long)o;
 }
 
 // PublicKey from its bincode str
@@ -56,10 +102,7 @@ bool read_public_key(Reader &r, uint8_t pk[32]) {
   uint64_t len = 0;
   const uint8_t *s = nullptr;
   if (!r.u64(len) || len > r.left || !r.bytes(s, (size_t)len)) return false;
-  std::vector<uint8_t> dec;
-  if (!b64_decode(s, (size_t)len, dec) || dec.size() < 32) return false;
-  std::memcpy(pk, dec.data(), 32);
-  return true;
+  return b64_decode_prefix(s, (size_t)len, pk, 32) >= 32;
 }
 
 void put_le64(uint8_t *p, uint64_t v) {
@@ -69,28 +112,14 @@ void put_le64(uint8_t *p, uint64_t v) {
 }  // namespace
 
 bool b64_decode(const uint8_t *s, size_t n, std::vector<uint8_t> &out) {
-  size_t end = n;
-  while (end > 0 && s[end - 1] == '=') --end;
-  if (n - end > 2) return false;
-  if (n != end && n % 4 != 0) return false;  // padded input comes in whole quads
-  const size_t rem = end % 4;
-  if (rem == 1) return false;
-  out.clear();
-  out.reserve(end * 3 / 4);
-  uint32_t acc = 0;
-  int bits = 0;
-  for (size_t i = 0; i < end; ++i) {
-    const int v = b64_value(s[i]);
-    if (v < 0) return false;
-    acc = (acc << 6) | (uint32_t)v;
-    bits += 6;
-    if (bits >= 8) {
-      bits -= 8;
-      out.push_back((uint8_t)(acc >> bits));
-      acc &= (1u << bits) - 1u;
-    }
+  out.assign(n / 4 * 3 + 3, 0);
+  const long m = b64_decode_prefix(s, n, out.data(), out.size());
+  if (m < 0) {
+    out.clear();
+    return false;
   }
-  return acc == 0;  // the leftover (trailing) bits must be zero
+  out.resize((size_t)m);
+  return true;
 }
 
 bool parse_qc(const uint8_t *buf, size_t len, QcParsed &out, std::string &err) {
