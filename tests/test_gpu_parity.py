@@ -63,6 +63,23 @@ def test_golden_row_form_chunks(api, golden):
         lib.hsv_set_auto_committee(1)
 
 
+def test_golden_pair_form_range(api, golden):
+    """Batches between the row form's cut-over (3072) and 2^13 run the pair
+    kernel (hsv_verify_pair_fused_kernel): the golden records tiled to 4096
+    items, every flag bit.  Committee cache off."""
+    _, verifier, _ = api
+    from hsverify import _lib
+    lib = _lib.load()
+    lib.hsv_set_auto_committee(0)
+    try:
+        idx = np.arange(4096) % len(golden["flags"])
+        got = verifier.verify_flags(golden["pk"][idx], golden["sig"][idx], golden["msg"][idx])
+        bad = np.nonzero(got != golden["flags"][idx])[0]
+        assert bad.size == 0, [(golden["cases"][idx[i]], int(got[i]), int(golden["flags"][idx[i]])) for i in bad[:8]]
+    finally:
+        lib.hsv_set_auto_committee(1)
+
+
 @pytest.mark.parametrize("bits", [133, 0])
 def test_lattice_fallback_records_every_variant(api, fallback_records, bits):
     """The fixture challenges have no lattice pair below 2^133: with the bound
@@ -85,6 +102,10 @@ def test_lattice_fallback_records_every_variant(api, fallback_records, bits):
             assert (got == fb["flags"]).all(), (v, np.nonzero(got != fb["flags"])[0][:8])
             # mixed into a wave of ordinary records (the fallback lane diverges)
             idx = np.arange(256) % len(fb["flags"])
+            got = verifier.verify_flags(fb["pk"][idx], fb["sig"][idx], fb["msg"][idx])
+            assert (got == fb["flags"][idx]).all(), v
+            # the pair form's range (3073 .. 2^13 items)
+            idx = np.arange(4096) % len(fb["flags"])
             got = verifier.verify_flags(fb["pk"][idx], fb["sig"][idx], fb["msg"][idx])
             assert (got == fb["flags"][idx]).all(), v
             # past the pair form's cut-over: the point pass deals fallback batches first
