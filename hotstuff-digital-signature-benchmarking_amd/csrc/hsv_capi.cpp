@@ -526,6 +526,23 @@ size_t pipe_chunk() {  // HSV_PIPE_CHUNK_LOG2 (14..22): measurement switch
   return c;
 }
 
+// The slot's two launch workspaces (one per compute stream), grown to at
+// least `need` bytes each; kept across calls, so no launch allocates.
+int slot_workspaces(Slot &s, size_t need) {
+  if (need <= s.ws_cap) return HSV_OK;
+  for (uint8_t *&w : s.d_ws) {
+    if (w) (void)hipFree(w);
+    w = nullptr;
+  }
+  s.ws_cap = 0;
+  for (uint8_t *&w : s.d_ws) {
+    const hipError_t ea = hipMalloc(&w, need);
+    if (ea != hipSuccess) return hip_fail("allocating the launch workspaces", ea);
+  }
+  s.ws_cap = need;
+  return HSV_OK;
+}
+
 // Chunk sizes of a pipelined call over n items (n >= 2 pipe_chunk()).
 // Nothing hides the first chunk's pack and copy, so it is half a chunk
 // (2^16 items: 10.73 ms per 2^20 against 10.99 for a full first chunk sent
@@ -613,19 +630,8 @@ int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, siz
   // one launch workspace per compute stream, kept by the slot: a pool
   // allocation per launch made the enqueue of each chunk wait ~1 ms for an
   // earlier chunk (tools/host_api_probe.py marks)
-  const size_t ws_need = hsv_launch_ws_bytes(v, (uint32_t)maxm);
-  if (ws_need > s.ws_cap) {
-    for (uint8_t *&w : s.d_ws) {
-      if (w) (void)hipFree(w);
-      w = nullptr;
-    }
-    s.ws_cap = 0;
-    for (uint8_t *&w : s.d_ws) {
-      const hipError_t ea = hipMalloc(&w, ws_need);
-      if (ea != hipSuccess) return hip_fail("allocating the pipeline workspaces", ea);
-    }
-    s.ws_cap = ws_need;
-  }
+  rc = slot_workspaces(s, hsv_launch_ws_bytes(v, (uint32_t)maxm));
+  if (rc != HSV_OK) return rc;
   hipStream_t comp[2] = {s.stream, s.stream2};
   hipEvent_t staged[2] = {s.ev[0], s.ev[1]};
   auto drain = [&](int code) -> int {
@@ -769,8 +775,12 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
       // the pinned staging buffer and write the flags through its device
       // mapping, so no copy launches sit on the latency path
       uint8_t *dh = static_cast<uint8_t *>(hd);
-      e = hsv_launch_verify(v, dh + pk_off, 32, dh + sig_off, 64, dh + msg_off, msg_stride ? 32 : 0, (uint32_t)m,
-                            dh + flag_off, nullptr, comb_b, reinterpret_cast<uint32_t *>(dh + fault_off), st);
+      // the launch workspace the slot keeps: no pool allocation on the latency path
+      rc = slot_workspaces(s, hsv_launch_ws_bytes(v, (uint32_t)m));
+      if (rc != HSV_OK) return rc;
+      e = hsv_launch_verify_ws(v, dh + pk_off, 32, dh + sig_off, 64, dh + msg_off, msg_stride ? 32 : 0, (uint32_t)m,
+                               dh + flag_off, nullptr, comb_b, reinterpret_cast<uint32_t *>(dh + fault_off), s.d_ws[0],
+                               s.ws_cap, st);
     } else {
       // inputs, the zeroed flags and the zeroed self-check words in one copy
       const size_t in_bytes = fault_off + kFaultBytes;
