@@ -76,6 +76,9 @@ extern "C" {
  * Without a call, the environment variable HSV_DEVICE (same values) applies,
  * else -1.  Each device keeps a pool of HSV_SLOTS (default 4) staging slots,
  * so concurrent calls (several tokio workers) do not queue behind one buffer.
+ * A slot's streams (and the device API's side streams) are created at the
+ * greatest stream priority, so they draw on hardware queues of their own
+ * instead of sharing the application's.
  * Device-resident calls (hsv_*_device*) always run on the device that owns
  * their input pointers; a stream of another device is an error.
  * Returns < 0 for a device index out of range. */
