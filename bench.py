@@ -504,6 +504,8 @@ def parse_args(argv=None):
     ap.add_argument("--streams", type=int, default=3,
                     help="consecutive batches alternate over this many HIP streams, so a batch's launch can "
                          "start in the previous one's grid end (1: every batch on one stream)")
+    ap.add_argument("--stream-priority", choices=("normal", "high"), default="normal",
+                    help="priority of the C4 line's extra streams (measurement switch)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20,
                     help="triples the CPU port verifies (default: the whole C4 batch)")
     ap.add_argument("--qc-reps", type=int, default=1000,
@@ -622,7 +624,8 @@ def main():
     # them.  The next batch's prepass and point pass then fill the SIMDs the
     # previous point pass leaves idle at its grid end.
     nst = max(1, a.streams)
-    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(nst - 1)]
+    prio = {"normal": 0, "high": -1}[a.stream_priority]
+    streams = [stream] + [torch.cuda.Stream(dev, priority=prio) for _ in range(nst - 1)]
     outs = [(torch.zeros(a.n, dtype=torch.uint8, device=dev),
              torch.zeros((a.n + 31) // 32, dtype=torch.int32, device=dev)) for _ in range(nst)]
     flags, bits = outs[0]
