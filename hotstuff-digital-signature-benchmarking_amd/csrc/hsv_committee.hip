@@ -97,14 +97,16 @@ constexpr int kCombLanes = HSV_COMB_LANES;
 static_assert(kCombLanes == 4 || kCombLanes == 8 || kCombLanes == 16, "lanes per vote");
 constexpr int kCombPosPerLane = kCombPos / kCombLanes;
 
-// ---- checks of a vote's final sum spread over its 16-lane row (L = 16) ----
+// Checks of a vote's final sum spread over its 16-lane row (L = 16): after
+// the swap rounds every lane of the vote's row holds Q, and the row is a DPP
+// row, so the self-check and the equation run as rounds of one field
+// operation per lane (ge_is_sane_row, ge_eq_affine_row in hsv_fe16x16.hpp).
 #ifdef HSV_COMB_SEQ_CHECKS  // measurement builds only: the one-lane checks of round 2
 constexpr bool kRowChecks = false;
 #else
 constexpr bool kRowChecks = kCombLanes == 16;
 #endif
-// After the swap rounds every lane of the vote's row holds Q, and the row is a
-// DPP row, so the final checks run as rounds of one field operation per lane.
+
 __device__ __forceinline__ ge_ext ge_swap_xor(const ge_ext &p, int m) {
   ge_ext r;
   HSV_UNROLL
