@@ -15,6 +15,8 @@
 //                          the additions, R decompressed by a second wave.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "hsv_comb.hpp"
 #include "hsv_fe16x16.hpp"
 #include "hsv_internal.h"
@@ -94,7 +96,7 @@ hsv_comb_verify_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__re
 #define HSV_COMB_LANES 16
 #endif
 constexpr int kCombLanes = HSV_COMB_LANES;
-static_assert(kCombLanes == 4 || kCombLanes == 8 || kCombLanes == 16, "lanes per vote");
+static_assert(kCombLanes == 4 || kCombLanes == 8 || kCombLanes == 16 || kCombLanes == 32, "lanes per vote");
 constexpr int kCombPosPerLane = kCombPos / kCombLanes;
 
 // Checks of a vote's final sum spread over its 16-lane row (L = 16): after
@@ -104,7 +106,7 @@ constexpr int kCombPosPerLane = kCombPos / kCombLanes;
 #ifdef HSV_COMB_SEQ_CHECKS  // measurement builds only: the one-lane checks of round 2
 constexpr bool kRowChecks = false;
 #else
-constexpr bool kRowChecks = kCombLanes == 16;
+constexpr bool kRowChecks = kCombLanes >= 16;
 #endif
 
 __device__ __forceinline__ ge_ext ge_swap_xor(const ge_ext &p, int m) {
@@ -129,14 +131,69 @@ __device__ __forceinline__ ge_ext ge_swap_xor(const ge_ext &p, int m) {
 // (ge_decompress_row, hsv_fe16x16.hpp: 32 us for the root chain on a lone
 // wave against 57 us on one lane, profiles/r03z_ubench_lanesplit.txt), four
 // votes per wave.  HSV_COMB_R_ONELANE (measurement builds only) keeps round
-// 2's single R wave with one vote per lane.
+// 2's single R wave with one vote per lane.  Each vote takes two rows
+// (RowLane2: a product's 16 steps split 8 + 8 between the rows, 25.4 against
+// 32.2 us for the root chain, profiles/r03zz_ubench_lanesplit2.txt), two
+// votes per wave; HSV_COMB_R_ROWS=1 (measurement builds) keeps one row.
+#ifndef HSV_COMB_R_ROWS
+#define HSV_COMB_R_ROWS 2
+#endif
+constexpr int kRRows = HSV_COMB_R_ROWS;
+static_assert(kRRows == 1 || kRRows == 2, "HSV_COMB_R_ROWS is 1 or 2");
+using RLane = std::conditional_t<kRRows == 2, RowLane2, RowLane>;
+constexpr int kRVotesPerWave = 4 / kRRows;
 constexpr int kFusedVotes = 64 / kCombLanes;
 #ifdef HSV_COMB_R_ONELANE
 constexpr int kFusedRWaves = 1;
 #else
-constexpr int kFusedRWaves = (kFusedVotes + 3) / 4;
+constexpr int kFusedRWaves = (kFusedVotes + kRVotesPerWave - 1) / kRVotesPerWave;
 #endif
-constexpr int kFusedThreads = 64 * (1 + kFusedRWaves);
+// A hash wave (the last of the block) computes k = H(R || A || M) mod l and
+// its comb digits for the block's votes while the comb wave adds the s half
+// (the B table needs no hash), and hands the digits over in LDS: the comb
+// wave's path becomes max(hash, s additions) + k additions + swap rounds
+// instead of their sum.  HSV_COMB_HASH_WAVE=0 (measurement builds) keeps the
+// hash on the comb wave.
+#ifndef HSV_COMB_HASH_WAVE
+#define HSV_COMB_HASH_WAVE 1
+#endif
+constexpr bool kHashWave = HSV_COMB_HASH_WAVE != 0;
+constexpr uint32_t kHashWaveIdx = 1 + kFusedRWaves;
+constexpr int kFusedThreads = 64 * (1 + kFusedRWaves + (kHashWave ? 1 : 0));
+
+// one vote's words: the key A, the signature (R, s) and the message digest M
+__device__ __forceinline__ void load_vote_words(const uint8_t *__restrict__ pks, uint32_t kk,
+                                                const uint8_t *__restrict__ sig, uint64_t sig_stride,
+                                                const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t i,
+                                                uint32_t pkw[8], uint32_t sigw[16], uint32_t msgw[8]) {
+  const uint4 *p = reinterpret_cast<const uint4 *>(pks + (uint64_t)kk * 32);
+  const uint4 *sp = reinterpret_cast<const uint4 *>(sig + (uint64_t)i * sig_stride);
+  const uint4 *gp = reinterpret_cast<const uint4 *>(msg + (uint64_t)i * msg_stride);
+  const uint4 p0 = p[0], p1 = p[1];
+  const uint4 s0 = sp[0], s1 = sp[1], s2 = sp[2], s3 = sp[3];
+  const uint4 m0 = gp[0], m1 = gp[1];
+  pkw[0] = p0.x; pkw[1] = p0.y; pkw[2] = p0.z; pkw[3] = p0.w;
+  pkw[4] = p1.x; pkw[5] = p1.y; pkw[6] = p1.z; pkw[7] = p1.w;
+  sigw[0] = s0.x; sigw[1] = s0.y; sigw[2] = s0.z; sigw[3] = s0.w;
+  sigw[4] = s1.x; sigw[5] = s1.y; sigw[6] = s1.z; sigw[7] = s1.w;
+  sigw[8] = s2.x; sigw[9] = s2.y; sigw[10] = s2.z; sigw[11] = s2.w;
+  sigw[12] = s3.x; sigw[13] = s3.y; sigw[14] = s3.z; sigw[15] = s3.w;
+  msgw[0] = m0.x; msgw[1] = m0.y; msgw[2] = m0.z; msgw[3] = m0.w;
+  msgw[4] = m1.x; msgw[5] = m1.y; msgw[6] = m1.z; msgw[7] = m1.w;
+}
+
+// lane g's 8 P digit bits of a recoded scalar, starting at bit 8 g P
+__device__ __forceinline__ uint64_t lane_digits(const uint32_t r[9], uint32_t g) {
+  constexpr int kBits = 8 * kCombPosPerLane;
+  uint64_t d = 0;
+  HSV_UNROLL
+  for (int q = 0; q < kCombLanes; ++q) {
+    const int w = (q * kBits) / 32, sh = (q * kBits) % 32;
+    const uint64_t v = ((((uint64_t)r[w + 1] << 32) | r[w]) >> sh) & (kBits == 64 ? ~0ull : ((1ull << kBits) - 1));
+    d = g == (uint32_t)q ? v : d;
+  }
+  return d;
+}
 
 __global__ void __launch_bounds__(kFusedThreads)
 hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__restrict__ sig,
@@ -146,12 +203,37 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
                                   const uint32_t *__restrict__ btable, uint8_t *__restrict__ flags_out,
                                   uint32_t inject, uint32_t *__restrict__ fault) {
   __shared__ uint32_t r_x[kFusedVotes][kFeLimbs], r_y[kFusedVotes][kFeLimbs], r_fl[kFusedVotes];
+  __shared__ uint32_t k_rec[kFusedVotes][9], k_ready;
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint32_t base = blockIdx.x * kFusedVotes;
+  if constexpr (kHashWave) {
+    // LDS keeps the last block's flag: cleared before any wave can look
+    if (threadIdx.x == 0) k_ready = 0u;
+    __syncthreads();
+    if (wave == kHashWaveIdx) {
+      const uint32_t vl = lane / kCombLanes, g = lane % kCombLanes;
+      const uint32_t i = base + vl < m ? base + vl : m - 1u;
+      const uint32_t kidx = key_idx[i];
+      const uint32_t kk = kidx < nkeys ? kidx : 0u;
+      uint32_t pkw[8], sigw[16], msgw[8], h[16], kr[9];
+      load_vote_words(pks, kk, sig, sig_stride, msg, msg_stride, i, pkw, sigw, msgw);
+      sha512_96(sigw, pkw, msgw, h);
+      const sc k = sc_reduce512(h);
+      recode_add<9, 8, kCombPos>(k.v, 8, kr);
+      if (g == 0u) {
+        HSV_UNROLL
+        for (int w = 0; w < 9; ++w) k_rec[vl][w] = kr[w];
+      }
+      __hip_atomic_store(&k_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __syncthreads();
+      return;
+    }
+  }
   if (wave >= 1) {
 #ifndef HSV_COMB_R_ONELANE
-    const RowLane L;
-    const uint32_t vr = (wave - 1u) * 4u + (lane >> 4);  // this row's vote in the block
+    const RLane L;
+    const uint32_t row = lane >> 4;
+    const uint32_t vr = (wave - 1u) * kRVotesPerWave + row / kRRows;  // this row's vote in the block
     if (vr < (uint32_t)kFusedVotes) {
       const uint32_t i = base + vr < m ? base + vr : m - 1u;
       const uint4 *sp = reinterpret_cast<const uint4 *>(sig + (uint64_t)i * sig_stride);
@@ -167,7 +249,7 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
       const uint32_t r_ok = ge_decompress_row(rw, rx, ry, small, L);
 #endif
       const uint32_t small_r = r_ok & small;
-      if (L.k == 0u) {
+      if (L.k == 0u && row % kRRows == 0u) {
         HSV_UNROLL
         for (int l = 0; l < kFeLimbs; ++l) {
           r_x[vr][l] = rx.v[l];
@@ -204,60 +286,61 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
   const bool kvalid = kidx < nkeys;
   const uint32_t kk = kvalid ? kidx : 0u;
   uint32_t pkw[8], sigw[16], msgw[8];
-  {
-    const uint4 *p = reinterpret_cast<const uint4 *>(pks + (uint64_t)kk * 32);
-    const uint4 *sp = reinterpret_cast<const uint4 *>(sig + (uint64_t)i * sig_stride);
-    const uint4 *gp = reinterpret_cast<const uint4 *>(msg + (uint64_t)i * msg_stride);
-    const uint4 p0 = p[0], p1 = p[1];
-    const uint4 s0 = sp[0], s1 = sp[1], s2 = sp[2], s3 = sp[3];
-    const uint4 m0 = gp[0], m1 = gp[1];
-    pkw[0] = p0.x; pkw[1] = p0.y; pkw[2] = p0.z; pkw[3] = p0.w;
-    pkw[4] = p1.x; pkw[5] = p1.y; pkw[6] = p1.z; pkw[7] = p1.w;
-    sigw[0] = s0.x; sigw[1] = s0.y; sigw[2] = s0.z; sigw[3] = s0.w;
-    sigw[4] = s1.x; sigw[5] = s1.y; sigw[6] = s1.z; sigw[7] = s1.w;
-    sigw[8] = s2.x; sigw[9] = s2.y; sigw[10] = s2.z; sigw[11] = s2.w;
-    sigw[12] = s3.x; sigw[13] = s3.y; sigw[14] = s3.z; sigw[15] = s3.w;
-    msgw[0] = m0.x; msgw[1] = m0.y; msgw[2] = m0.z; msgw[3] = m0.w;
-    msgw[4] = m1.x; msgw[5] = m1.y; msgw[6] = m1.z; msgw[7] = m1.w;
-  }
+  load_vote_words(pks, kk, sig, sig_stride, msg, msg_stride, i, pkw, sigw, msgw);
   const uint32_t s_ok = sc_is_canonical(sigw + 8);
 #ifdef HSV_TIMING_STUB_QUADPATH  // tools/qc_phase_probe.py only: wrong flags, the R waves' time alone
   ge_ext q = ge_identity();
   const uint32_t *ta = key_tables[kk];
   (void)ta;
 #else
-  uint32_t h[16];
-  sha512_96(sigw, pkw, msgw, h);
-  const sc k = sc_reduce512(h);
-  uint32_t kr[9], sr[9];
-  recode_add<9, 8, kCombPos>(k.v, 8, kr);
-  recode_add<9, 8, kCombPos>(sigw + 8, 8, sr);
-  // this lane's 8P digit bits, starting at bit 8 g P
-  uint64_t kd = 0, sd = 0;
-  HSV_UNROLL
-  for (int q = 0; q < kCombLanes; ++q) {
-    constexpr int kBits = 8 * kCombPosPerLane;
-    const int w = (q * kBits) / 32, sh = (q * kBits) % 32;
-    const uint64_t kq = ((((uint64_t)kr[w + 1] << 32) | kr[w]) >> sh) & (kBits == 64 ? ~0ull : ((1ull << kBits) - 1));
-    const uint64_t sq = ((((uint64_t)sr[w + 1] << 32) | sr[w]) >> sh) & (kBits == 64 ? ~0ull : ((1ull << kBits) - 1));
-    const bool me = g == (uint32_t)q;
-    kd = me ? kq : kd;
-    sd = me ? sq : sd;
-  }
   const uint32_t *ta = key_tables[kk];
   ge_ext q = ge_identity();
-  HSV_NOUNROLL
-  for (int jj = 0; jj < kCombPosPerLane; ++jj) {
-    const uint32_t j = g * kCombPosPerLane + (uint32_t)jj;
-    const uint32_t ca = (uint32_t)kd & 0xffu, cb = (uint32_t)sd & 0xffu;
-    kd >>= 8;
-    sd >>= 8;
-    const CombPosTab tpa{ta + (uint64_t)j * kCombEnt * kCombEntryWords};
-    const CombPosTab tpb{btable + (uint64_t)j * kCombEnt * kCombEntryWords};
-    ge_niels na = select_niels<8>(tpa, ca);
-    if (inject != kInjectNone && jj == 0) na = niels_injected(na, inject);
-    q = ge_add_niels<true>(q, na);
-    q = ge_add_niels<true>(q, select_niels<8>(tpb, cb));
+  uint32_t sr[9];
+  recode_add<9, 8, kCombPos>(sigw + 8, 8, sr);
+  uint64_t sd = lane_digits(sr, g), kd;
+  if constexpr (kHashWave) {
+    // the s half first, while the hash wave works on k
+    HSV_NOUNROLL
+    for (int jj = 0; jj < kCombPosPerLane; ++jj) {
+      const uint32_t j = g * kCombPosPerLane + (uint32_t)jj;
+      const CombPosTab tpb{btable + (uint64_t)j * kCombEnt * kCombEntryWords};
+      q = ge_add_niels<true>(q, select_niels<8>(tpb, (uint32_t)sd & 0xffu));
+      sd >>= 8;
+    }
+    while (__hip_atomic_load(&k_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+      __builtin_amdgcn_s_sleep(1);
+    uint32_t kr[9];
+    HSV_UNROLL
+    for (int w = 0; w < 9; ++w) kr[w] = k_rec[vl][w];
+    kd = lane_digits(kr, g);
+    HSV_NOUNROLL
+    for (int jj = 0; jj < kCombPosPerLane; ++jj) {
+      const uint32_t j = g * kCombPosPerLane + (uint32_t)jj;
+      const CombPosTab tpa{ta + (uint64_t)j * kCombEnt * kCombEntryWords};
+      ge_niels na = select_niels<8>(tpa, (uint32_t)kd & 0xffu);
+      kd >>= 8;
+      if (inject != kInjectNone && jj == 0) na = niels_injected(na, inject);
+      q = ge_add_niels<true>(q, na);
+    }
+  } else {
+    uint32_t h[16], kr[9];
+    sha512_96(sigw, pkw, msgw, h);
+    const sc k = sc_reduce512(h);
+    recode_add<9, 8, kCombPos>(k.v, 8, kr);
+    kd = lane_digits(kr, g);
+    HSV_NOUNROLL
+    for (int jj = 0; jj < kCombPosPerLane; ++jj) {
+      const uint32_t j = g * kCombPosPerLane + (uint32_t)jj;
+      const uint32_t ca = (uint32_t)kd & 0xffu, cb = (uint32_t)sd & 0xffu;
+      kd >>= 8;
+      sd >>= 8;
+      const CombPosTab tpa{ta + (uint64_t)j * kCombEnt * kCombEntryWords};
+      const CombPosTab tpb{btable + (uint64_t)j * kCombEnt * kCombEntryWords};
+      ge_niels na = select_niels<8>(tpa, ca);
+      if (inject != kInjectNone && jj == 0) na = niels_injected(na, inject);
+      q = ge_add_niels<true>(q, na);
+      q = ge_add_niels<true>(q, select_niels<8>(tpb, cb));
+    }
   }
   HSV_UNROLL
   for (int mask = 1; mask < kCombLanes; mask <<= 1)
@@ -294,15 +377,18 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
   if (valid && g == 0u) flags_out[i0] = kvalid ? (uint8_t)f : (uint8_t)0;
 }
 
-// Test hook (tests/test_lanesplit.py): the row form of hsv_fe16x16.hpp
-// against the one-lane form, one 16-lane row per input of 16 words (a | b,
-// 8 little-endian words each).  out[row] bit 0: a * b differs, bit 1:
-// a^((p-5)/8) differs, bit 2: ge_decompress_row(a) differs from
+// Test hook (tests/test_lanesplit.py): the row forms of hsv_fe16x16.hpp
+// against the one-lane form, one input of 16 words (a | b, 8 little-endian
+// words each) per element: one 16-lane row (RowLane) or two (RowLane2).
+// Bits (shifted by 3 for the two-row form): bit 0 a * b differs, bit 1
+// a^((p-5)/8) differs, bit 2 ge_decompress_row(a) differs from
 // ge_decompress(a) in its flag or, for a decodable a, in (x, y).
+template <class Lane, int kRows>
 __global__ void __launch_bounds__(64) hsv_lanesplit_check_kernel(const uint32_t *__restrict__ in, uint32_t rows,
                                                                  uint32_t *__restrict__ out) {
-  const RowLane L;
-  const uint32_t r = blockIdx.x * 4u + (threadIdx.x >> 4);
+  const Lane L;
+  constexpr uint32_t kPerWave = 4u / kRows, kShift = kRows == 1 ? 0u : 3u;
+  const uint32_t r = blockIdx.x * kPerWave + (threadIdx.x >> 4) / kRows;
   const uint32_t rr = r < rows ? r : rows - 1u;
   uint32_t aw[8], bw[8];
   HSV_UNROLL
@@ -319,7 +405,9 @@ __global__ void __launch_bounds__(64) hsv_lanesplit_check_kernel(const uint32_t 
   const uint32_t ok0 = ge_decompress(aw, x0, y0);
   const uint32_t ok1 = ge_decompress_row(aw, x1, y1, small1, L);
   bad |= (ok0 == ok1 && (!ok0 || (fe_eq(x0, x1) && fe_eq(y0, y1) && y_is_small_order(y0) == small1))) ? 0u : 4u;
-  if (r < rows && L.k == 0u) out[r] = bad;
+  // the odd row of a pair checks its own copy too
+  if constexpr (kRows == 2) bad |= __shfl_xor(bad, 16);
+  if (r < rows && (threadIdx.x & (16u * kRows - 1u)) == 0u) out[r] |= bad << kShift;
 }
 
 // one lane per (position j, chunk c) of the wide B table; j is wave-uniform
@@ -352,8 +440,15 @@ extern "C" int hsv_test_lanesplit_check(const uint32_t *in, uint32_t rows, uint3
   hipError_t e = hipMalloc(&d_in, (size_t)rows * 64);
   if (e == hipSuccess) e = hipMalloc(&d_out, (size_t)rows * 4);
   if (e == hipSuccess) e = hipMemcpy(d_in, in, (size_t)rows * 64, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemset(d_out, 0, (size_t)rows * 4);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(hsv::hsv_lanesplit_check_kernel, dim3((rows + 3) / 4), dim3(64), 0, 0, d_in, rows, d_out);
+    hipLaunchKernelGGL((hsv::hsv_lanesplit_check_kernel<hsv::RowLane, 1>), dim3((rows + 3) / 4), dim3(64), 0, 0,
+                       d_in, rows, d_out);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL((hsv::hsv_lanesplit_check_kernel<hsv::RowLane2, 2>), dim3((rows + 1) / 2), dim3(64), 0, 0,
+                       d_in, rows, d_out);
     e = hipGetLastError();
   }
   if (e == hipSuccess) e = hipDeviceSynchronize();

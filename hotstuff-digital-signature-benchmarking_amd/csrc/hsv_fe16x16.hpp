@@ -106,14 +106,66 @@ __device__ __forceinline__ uint32_t fl_mul(uint32_t f, uint32_t g, const RowLane
 
 __device__ __forceinline__ uint32_t fl_sq(uint32_t f, const RowLane &L) { return fl_mul(f, f, L); }
 
-__device__ __forceinline__ uint32_t fl_sqn(uint32_t f, int n, const RowLane &L) {
+// ---- two rows per element ---------------------------------------------------
+// Rows 2j and 2j+1 hold the same element; a product splits its 16 steps
+// between them (the even row steps 0..7, the odd row steps 8..15, starting
+// from g turned by 8 lanes with the wrapped half times 38 and from f turned by
+// 8 so that row_newbcast:i yields f_(i+8)), and v_permlane16_swap adds the two
+// rows' column sums, so both rows end with the whole product.  8 steps instead
+// of 16 on the critical path.
+struct RowLane2 : RowLane {
+  uint32_t w8;  // 38 on lanes 0..7 of an odd row (their turned limbs wrapped), else 1
+  __device__ __forceinline__ RowLane2() : RowLane() { w8 = ((__lane_id() >> 4) & 1u) && k < 8u ? 38u : 1u; }
+};
+
+// x on even rows, x turned by 8 lanes on odd rows: one DPP move whose row
+// mask (0xa) leaves the even rows' old value
+__device__ __forceinline__ uint32_t row_odd_ror8(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x128, 0xa, 0xf, false);
+}
+
+template <int I>
+__device__ __forceinline__ void fl2_mul_step(uint64_t &acc, uint32_t &gr, uint32_t f, const RowLane &L) {
+  if constexpr (I > 0) gr = __umul24(row_ror1(gr), L.win);
+  acc += (uint64_t)row_bcast<I>(f) * gr;
+  if constexpr (I < 7) fl2_mul_step<I + 1>(acc, gr, f, L);
+}
+
+__device__ __forceinline__ uint32_t fl2_mul(uint32_t f, uint32_t g, const RowLane2 &L) {
+  HSV_SCHED_FENCE();
+  uint64_t acc = 0;
+  uint32_t gr = __umul24(row_odd_ror8(g), L.w8);
+  fl2_mul_step<0>(acc, gr, row_odd_ror8(f), L);
+  // each row's half column sums split at bit 16, then the two rows' halves
+  // added across the pair (lane 15's column has no wrapped terms, so the
+  // summed carry times 38 stays below 2^32 as in fl_mul)
+  const uint32_t lo_h = (uint32_t)acc & 0xffffu;
+  const uint32_t t_h = __builtin_amdgcn_alignbit((uint32_t)(acc >> 32), (uint32_t)acc, 16);
+  const auto ls = __builtin_amdgcn_permlane16_swap(lo_h, lo_h, false, false);
+  const auto ts = __builtin_amdgcn_permlane16_swap(t_h, t_h, false, false);
+  uint32_t x = (ls[0] + ls[1]) + row_ror1((ts[0] + ts[1]) * L.wout);
+  uint32_t lo16 = x & 0xffffu;
+  uint32_t t = x >> 16;
+  x = lo16 + row_ror1(__umul24(t, L.wout));
+  HSV_SCHED_FENCE();
+  return x;
+}
+
+// the two-row form behind the same names, so fl_pow22523 and
+// ge_decompress_row take either lane layout
+__device__ __forceinline__ uint32_t fl_mul(uint32_t f, uint32_t g, const RowLane2 &L) { return fl2_mul(f, g, L); }
+__device__ __forceinline__ uint32_t fl_sq(uint32_t f, const RowLane2 &L) { return fl2_mul(f, f, L); }
+
+template <class Lane>
+__device__ __forceinline__ uint32_t fl_sqn(uint32_t f, int n, const Lane &L) {
   HSV_NOUNROLL
   for (int i = 0; i < n; ++i) f = fl_sq(f, L);
   return f;
 }
 
 // z^((p-5)/8) = z^(2^252 - 3), the chain of fe_pow22523 (hsv_field.hpp)
-__device__ __forceinline__ uint32_t fl_pow22523(uint32_t z, const RowLane &L) {
+template <class Lane>
+__device__ __forceinline__ uint32_t fl_pow22523(uint32_t z, const Lane &L) {
   uint32_t t0 = fl_sq(z, L);                 // 2
   uint32_t t1 = fl_sq(fl_sq(t0, L), L);      // 8
   t1 = fl_mul(z, t1, L);                     // 9
@@ -217,8 +269,9 @@ __device__ __forceinline__ uint32_t ge_eq_affine_row(const ge_ext &p, const fe &
 // independent operations on separate lanes of the row (one product, then one
 // comparison per lane).  Every lane of the row returns the same (x, y),
 // flag and small-order bit as ge_decompress and y_is_small_order.
+template <class Lane>
 __device__ __forceinline__ uint32_t ge_decompress_row(const uint32_t enc[8], fe &x, fe &y, uint32_t &small,
-                                                      const RowLane &L) {
+                                                      const Lane &L) {
   y = fe_from_words_masked(enc);
   uint32_t yl = row_limb_of_words(enc, L);
   if (L.k == 15u) yl &= 0x7fffu;  // bit 255 is the sign of x

@@ -71,7 +71,8 @@ def lanesplit_check(words):
     """Row-form field arithmetic against the one-lane form on the GPU
     (hsv_test_lanesplit_check): words is an (n, 16) uint32 array of element
     pairs a | b; returns per-row mismatch bits (1 product, 2 root chain,
-    4 decompression of a as an encoding)."""
+    4 decompression of a as an encoding) of the one-row form, and the same
+    three shifted by 3 (8, 16, 32) for the two-row form (RowLane2)."""
     import numpy as np
     w = np.ascontiguousarray(words, dtype=np.uint32)
     out = np.zeros(len(w), np.uint32)

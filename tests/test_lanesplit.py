@@ -4,9 +4,10 @@
 
 CPU: the bit-exact model of the row product (tools/lanesplit_model.py) keeps
 every instruction's operand bound over worst-case limbs.
-GPU: the row form against the one-lane radix-2^25.5 form (the path the golden
-vectors pin) on random elements and on edge encodings -- products, the root
-chain x^((p-5)/8), and CompressedEdwardsY::decompress (flag, x, y) of every
+GPU: the row form (one element per row, and two rows per element as the
+committee R waves run it) against the one-lane radix-2^25.5 form (the path the
+golden vectors pin) on random elements and on edge encodings -- products, the
+root chain x^((p-5)/8), and CompressedEdwardsY::decompress (flag, x, y) of every
 public key and R of the golden records plus constructed y values (0, 1,
 p - 1, p, p + 1, 2^255 - 1, both sign bits).
 """

@@ -53,6 +53,33 @@ __global__ void __launch_bounds__(64) k_check(const uint32_t *in, uint32_t *out,
   if (r < rows && (threadIdx.x & 15u) == 0u) out[r] = bad;
 }
 
+// rows 2j, 2j+1 hold element j (two rows per element, RowLane2): fl_mul / fl_pow22523
+// against the one-lane form; out[j] bits as k_check
+__global__ void __launch_bounds__(64) k_check2(const uint32_t *in, uint32_t *out, uint32_t pairs) {
+  const RowLane2 L;
+  const uint32_t r = blockIdx.x * 2u + (threadIdx.x >> 5);
+  const uint32_t rr = r < pairs ? r : pairs - 1u;
+  const fe a = load_fe(in + 16u * rr), b = load_fe(in + 16u * rr + 8u);
+  uint32_t bad = 0;
+  bad |= fe_eq(fe_mul(a, b), fl_to_fe(fl2_mul(fl_from_fe(a, L), fl_from_fe(b, L), L), L)) ? 0u : 1u;
+  bad |= fe_eq(fe_pow22523(a), fl_to_fe(fl_pow22523(fl_from_fe(a, L), L), L)) ? 0u : 2u;
+  if (r < pairs && (threadIdx.x & 31u) == 0u) out[r] = bad;
+}
+
+__global__ void __launch_bounds__(64) k_time_ls2(const uint32_t *in, uint32_t *sink, unsigned long long *clk, int reps) {
+  const RowLane2 L;
+  const fe a = load_fe(in + 16u * (threadIdx.x >> 5));
+  uint32_t x = fl_from_fe(a, L);
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), w0 = wall_clock64();
+  for (int i = 0; i < reps; ++i) x = fl_pow22523(x, L);
+  const uint64_t t1 = __builtin_amdgcn_s_memtime(), w1 = wall_clock64();
+  if (x == 0x12345678u) sink[0] = x;
+  if (threadIdx.x == 0) {
+    clk[0] = t1 - t0;
+    clk[1] = w1 - w0;
+  }
+}
+
 // one wave: `reps` root chains in a row, each lane-split row its own input
 __global__ void __launch_bounds__(64) k_time_ls(const uint32_t *in, uint32_t *sink, unsigned long long *clk, int reps) {
   const RowLane L;
@@ -132,18 +159,30 @@ int main() {
     for (int b = 0; b < 3; ++b) bad[b] += (out[r] >> b) & 1u;
   std::printf("{\"check_rows\": %u, \"mul_mismatch\": %d, \"pow22523_mismatch\": %d, \"chain40_mismatch\": %d}\n", rows,
               bad[0], bad[1], bad[2]);
+  hipLaunchKernelGGL(k_check2, dim3(rows / 2), dim3(64), 0, 0, d_in, d_out, rows);
+  CK(hipGetLastError());
+  CK(hipDeviceSynchronize());
+  CK(hipMemcpy(out.data(), d_out, rows * 4, hipMemcpyDeviceToHost));
+  int bad2[2] = {0, 0};
+  for (uint32_t r = 0; r < rows; ++r)
+    for (int b = 0; b < 2; ++b) bad2[b] += (out[r] >> b) & 1u;
+  std::printf("{\"two_row_check\": %u, \"mul_mismatch\": %d, \"pow22523_mismatch\": %d}\n", rows, bad2[0], bad2[1]);
+  bad[0] += bad2[0];
+  bad[1] += bad2[1];
   const int reps = 20;
   unsigned long long c[2];
-  for (int form = 0; form < 2; ++form) {
+  for (int form = 0; form < 3; ++form) {
     for (int warm = 0; warm < 2; ++warm) {
       if (form == 0) hipLaunchKernelGGL(k_time_ls, dim3(1), dim3(64), 0, 0, d_in, d_sink, d_clk, reps);
-      else hipLaunchKernelGGL(k_time_one, dim3(1), dim3(64), 0, 0, d_in, d_sink, d_clk, reps);
+      else if (form == 1) hipLaunchKernelGGL(k_time_one, dim3(1), dim3(64), 0, 0, d_in, d_sink, d_clk, reps);
+      else hipLaunchKernelGGL(k_time_ls2, dim3(1), dim3(64), 0, 0, d_in, d_sink, d_clk, reps);
       CK(hipGetLastError());
       CK(hipDeviceSynchronize());
     }
     CK(hipMemcpy(c, d_clk, 16, hipMemcpyDeviceToHost));
     std::printf("{\"form\": \"%s\", \"root_chain_clocks\": %.0f, \"root_chain_us\": %.2f}\n",
-                form == 0 ? "lane_split_16x16" : "one_lane_26x10", (double)c[0] / reps, (double)c[1] / reps / 100.0);
+                form == 0 ? "lane_split_16x16" : form == 1 ? "one_lane_26x10" : "two_rows_16x16", (double)c[0] / reps,
+                (double)c[1] / reps / 100.0);
   }
   return bad[0] + bad[1] + bad[2] ? 2 : 0;
 }
