@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <atomic>
 #include <mutex>
 #include <unordered_map>
@@ -708,10 +709,14 @@ hsv_verify_pair_fused_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
 // of the B comb; the two rows of an item swap their sums (lane ^ 16) and add
 // them.  Fallback items (no short lattice pair) run the full-length one-lane
 // path on lane 0 of their R row.  Same flags, self-checks and canaries as the
-// pair form.
-constexpr int kRowItems = 6;
-constexpr int kRowRows = 2 * kRowItems;
-template <int WA, int CB>
+// pair form.  RR = 2 (late round 3): every element over a pair of rows
+// (RowLane2, hsv_fe16x16.hpp), so a block takes 3 items: rows 4i, 4i + 1 hold
+// R of item i, rows 4i + 2, 4i + 3 hold A, and the R and A pairs swap their
+// sums at lane ^ 32.
+constexpr int kRowRows = 12;
+template <int RR>
+constexpr int kRowItemsOf = kRowRows / (2 * RR);
+template <int WA, int CB, int RR>
 __global__ void __launch_bounds__(4 * 64)
 hsv_verify_row_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const uint8_t *__restrict__ sig,
                       uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
@@ -721,6 +726,7 @@ hsv_verify_row_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const 
   using G = HalfCombWindows<WA>;
   constexpr int TS = 1 << (WA - 1);
   constexpr int kEnt = TS + 1;
+  constexpr int kRowItems = kRowItemsOf<RR>;
   __shared__ uint32_t srec[kPrepWords * kRowItems];
   __shared__ uint32_t stab[kRowRows * kEnt * 64];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
@@ -735,9 +741,12 @@ hsv_verify_row_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const 
     __syncthreads();
     return;
   }
-  const RowLane L;
+  const std::conditional_t<RR == 2, RowLane2, RowLane> L;
   const uint32_t rb = wave * 4u + (lane >> 4);  // row of the block
-  const uint32_t il = rb >> 1, role = rb & 1u;  // role 0: R, 1: A
+  const uint32_t el = rb / RR;                  // element (row or row pair) of the block
+  const uint32_t il = el >> 1, role = el & 1u;  // role 0: R, 1: A
+  const bool lead = rb % RR == 0u;              // the row that reports (one of a pair)
+  constexpr int kSwap = 16 * RR;
   const uint32_t item = base + il;
   const uint32_t li = item < n ? item : n - 1u;
   const uint32_t slot = blockIdx.x * (uint32_t)kRowRows + rb;
@@ -759,7 +768,7 @@ hsv_verify_row_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const 
   const uint32_t meta = srec[(kPrepWords - 1) * kRowItems + il];
   uint32_t f = 0, bad = 0;
   if (meta & kPrepFallback) {
-    if (role == 0u && L.k == 0u) {
+    if (role == 0u && L.k == 0u && lead) {
       GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)slot * vt_lane_uint4<WA>(), inject};
       uint32_t pkw[8], sigw[16], msgw[8];
       load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, li, pkw, sigw, msgw);
@@ -776,8 +785,9 @@ hsv_verify_row_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const 
     for (int i = 0; i < 8; ++i) b[i] = srec[(10 + i) * kRowItems + il];
     q = row_comb_half<CB>(q, b, comb_b, role, L);
     // both rows of the item end with the whole sum Q
-    q = rp_add_cached(q, rp_to_cached(rp_swap_rows(q), fl_from_fe(fe_d2(), L), L), false, L);
-    const uint32_t ok_o = (uint32_t)__shfl_xor((int)ok, 16, 64), small_o = (uint32_t)__shfl_xor((int)small, 16, 64);
+    q = rp_add_cached(q, rp_to_cached(rp_swap_rows(q, kSwap), fl_from_fe(fe_d2(), L), L), false, L);
+    const uint32_t ok_o = (uint32_t)__shfl_xor((int)ok, kSwap, 64);
+    const uint32_t small_o = (uint32_t)__shfl_xor((int)small, kSwap, 64);
     const uint32_t r_ok = role ? ok_o : ok, small_r = role ? small_o : small;
     const uint32_t a_ok = role ? ok : ok_o, small_a = role ? small : small_o;
     ge_ext qe;
@@ -792,7 +802,7 @@ hsv_verify_row_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const 
     bad = (a_ok & r_ok & (sane ^ 1u)) ? 1u : 0u;
   }
   report_faults(fault, bad | (canary[slot] != nonce ? 2u : 0u));
-  if (item < n && role == 0u && L.k == 0u) {
+  if (item < n && role == 0u && L.k == 0u && lead) {
     if (flags_out) flags_out[item] = (uint8_t)f;
     if (strict_bits && (f & kStrictOk)) atomicOr(&strict_bits[item >> 5], 1u << (item & 31u));
   }
@@ -1233,12 +1243,26 @@ uint32_t row_max() {  // HSV_ROW_MAX: measurement switch (0: always the pair for
   return m;
 }
 
+// Two rows per element up to row2_max() items (HSV_ROW2_MAX: measurement
+// switch, 0: one row per element): 3 items per block, so 768 items fill the
+// 256 CUs with one block each.
+constexpr uint32_t kRow2MaxDefault = 768;
+uint32_t row2_max() {
+  static const uint32_t m = [] {
+    const char *v = std::getenv("HSV_ROW2_MAX");
+    return v ? (uint32_t)std::atoi(v) : kRow2MaxDefault;
+  }();
+  return m;
+}
+
 template <int WA, int CB>
 hipError_t launch_row(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
                       const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
                       uint32_t *strict_bits, const uint32_t *comb_b, uint32_t *fault, hipStream_t stream,
                       void *ws_in = nullptr, size_t ws_cap = 0, size_t *ws_need = nullptr) {
-  const uint32_t grid = (n + hsv::kRowItems - 1) / hsv::kRowItems;
+  const bool two = n <= row2_max();
+  const uint32_t items = two ? hsv::kRowItemsOf<2> : hsv::kRowItemsOf<1>;
+  const uint32_t grid = (n + items - 1) / items;
   const size_t slots = (size_t)grid * hsv::kRowRows;
   const size_t ws_bytes = slots * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
   const size_t need = ws_bytes + slots * sizeof(uint32_t);
@@ -1252,10 +1276,11 @@ hipError_t launch_row(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig,
   if (e != hipSuccess) return e;
   if (strict_bits) e = hipMemsetAsync(strict_bits, 0, (size_t)((n + 31u) / 32u) * 4u, stream);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL((hsv::hsv_verify_row_kernel<WA, CB>), dim3(grid), dim3(4 * 64), 0, stream, pk, pk_stride,
-                       sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, static_cast<uint4 *>(ws), comb_b,
-                       g_lat_bits.load(), reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(ws) + ws_bytes),
-                       next_nonce(), g_inject.load(), fault);
+    auto kern = two ? hsv::hsv_verify_row_kernel<WA, CB, 2> : hsv::hsv_verify_row_kernel<WA, CB, 1>;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(4 * 64), 0, stream, pk, pk_stride, sig, sig_stride, msg, msg_stride,
+                       n, flags_out, strict_bits, static_cast<uint4 *>(ws), comb_b, g_lat_bits.load(),
+                       reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(ws) + ws_bytes), next_nonce(),
+                       g_inject.load(), fault);
     e = hipGetLastError();
   }
   const hipError_t ef = own ? hipFreeAsync(ws, stream) : hipSuccess;

@@ -1,5 +1,7 @@
 // Edwards25519 point arithmetic in the row form (hsv_fe16x16.hpp): one
-// point per 16-lane DPP row, lane k holding limb k of each coordinate.  The
+// point per 16-lane DPP row, lane k holding limb k of each coordinate (or one
+// point per pair of rows, Lane = RowLane2, with the products split between
+// them).  The
 // formulas are hsv_point.hpp's (HWCD, complete for a = -1), operation for
 // operation, so the row kernels compute exactly what the one-lane kernels do.
 //
@@ -42,8 +44,9 @@ __device__ __forceinline__ rp_ext rp_identity(const RowLane &L) {
 }
 
 // X3 = E F, Y3 = G H, Z3 = F G, T3 = E H (ge_finish_rt); without T, T is 0
+template <class Lane>
 __device__ __forceinline__ rp_ext rp_finish(uint32_t E, uint32_t F, uint32_t G, uint32_t H, bool with_t,
-                                            const RowLane &L) {
+                                            const Lane &L) {
   rp_ext r;
   r.X = fl_mul(E, F, L);
   r.Y = fl_mul(G, H, L);
@@ -53,7 +56,8 @@ __device__ __forceinline__ rp_ext rp_finish(uint32_t E, uint32_t F, uint32_t G, 
 }
 
 // 2P (ge_dbl_rt)
-__device__ __forceinline__ rp_ext rp_dbl(const rp_ext &p, bool with_t, const RowLane &L) {
+template <class Lane>
+__device__ __forceinline__ rp_ext rp_dbl(const rp_ext &p, bool with_t, const Lane &L) {
   const uint32_t A = fl_sq(p.X, L), B = fl_sq(p.Y, L), C = fl_sq(p.Z, L), S = fl_sq(p.X + p.Y, L);
   const uint32_t H = A + B;
   const uint32_t E = fl_sub(H, S, L);
@@ -63,7 +67,8 @@ __device__ __forceinline__ rp_ext rp_dbl(const rp_ext &p, bool with_t, const Row
 }
 
 // P + Q, Q cached (ge_add_cached_rt)
-__device__ __forceinline__ rp_ext rp_add_cached(const rp_ext &p, const rp_cached &q, bool with_t, const RowLane &L) {
+template <class Lane>
+__device__ __forceinline__ rp_ext rp_add_cached(const rp_ext &p, const rp_cached &q, bool with_t, const Lane &L) {
   const uint32_t A = fl_mul(fl_sub(p.Y, p.X, L), q.YmX, L);
   const uint32_t B = fl_mul(p.Y + p.X, q.YpX, L);
   const uint32_t C = fl_mul(p.T, q.T2d, L);
@@ -72,8 +77,9 @@ __device__ __forceinline__ rp_ext rp_add_cached(const rp_ext &p, const rp_cached
 }
 
 // P + Q, Q affine Niels (y + x, y - x, 2dxy) (ge_add_niels)
+template <class Lane>
 __device__ __forceinline__ rp_ext rp_add_niels(const rp_ext &p, uint32_t ypx, uint32_t ymx, uint32_t xy2d,
-                                               bool with_t, const RowLane &L) {
+                                               bool with_t, const Lane &L) {
   const uint32_t A = fl_mul(fl_sub(p.Y, p.X, L), ymx, L);
   const uint32_t B = fl_mul(p.Y + p.X, ypx, L);
   const uint32_t C = fl_mul(p.T, xy2d, L);
@@ -81,14 +87,16 @@ __device__ __forceinline__ rp_ext rp_add_niels(const rp_ext &p, uint32_t ypx, ui
   return rp_finish(fl_sub(B, A, L), fl_sub(D, C, L), D + C, B + A, with_t, L);
 }
 
-__device__ __forceinline__ rp_cached rp_to_cached(const rp_ext &p, uint32_t d2, const RowLane &L) {
+template <class Lane>
+__device__ __forceinline__ rp_cached rp_to_cached(const rp_ext &p, uint32_t d2, const Lane &L) {
   return rp_cached{p.Y + p.X, fl_sub(p.Y, p.X, L), p.Z + p.Z, fl_mul(p.T, d2, L)};
 }
 
-// The row's point from the partner row (lane ^ 16: rows 0 <-> 1, 2 <-> 3)
-__device__ __forceinline__ rp_ext rp_swap_rows(const rp_ext &p) {
-  return rp_ext{(uint32_t)__shfl_xor((int)p.X, 16, 64), (uint32_t)__shfl_xor((int)p.Y, 16, 64),
-                (uint32_t)__shfl_xor((int)p.Z, 16, 64), (uint32_t)__shfl_xor((int)p.T, 16, 64)};
+// The point of the partner row (lane ^ 16: rows 0 <-> 1, 2 <-> 3), or of the
+// partner row pair (lane ^ 32) in the two-row form
+__device__ __forceinline__ rp_ext rp_swap_rows(const rp_ext &p, int mask = 16) {
+  return rp_ext{(uint32_t)__shfl_xor((int)p.X, mask, 64), (uint32_t)__shfl_xor((int)p.Y, mask, 64),
+                (uint32_t)__shfl_xor((int)p.Z, mask, 64), (uint32_t)__shfl_xor((int)p.T, mask, 64)};
 }
 
 // ---- the per-row variable-base table in LDS --------------------------------
@@ -97,8 +105,8 @@ __device__ __forceinline__ rp_ext rp_swap_rows(const rp_ext &p) {
 // [m](-P) = [m-1](-P) + (-P) with -P in affine Niels form, as vt_build.
 // inject (tests): entries 1.. stored as zeros, or with one bit flipped when
 // flip_this_table (the pair kernel's table 0, R).
-template <int TS>
-__device__ __forceinline__ void row_table_build(uint32_t *tab, const fe &x, const fe &y, const RowLane &L,
+template <int TS, class Lane>
+__device__ __forceinline__ void row_table_build(uint32_t *tab, const fe &x, const fe &y, const Lane &L,
                                                 uint32_t inject, bool flip_this_table) {
   const uint32_t nx = fl_from_fe(fe_carry(fe_neg(x)), L);  // -x
   const uint32_t yl = fl_from_fe(y, L);
@@ -136,8 +144,8 @@ __device__ __forceinline__ rp_cached row_table_entry(const uint32_t *tab, uint32
 // top window at the top bits, as recode_top5) of NW windows of WA bits;
 // flip negates every digit.  Leading windows whose digits are zero in every
 // row of the wave are skipped (wave-uniform).  T is valid on return.
-template <int WA, int NW>
-__device__ __forceinline__ rp_ext row_straus(uint32_t d[5], const uint32_t *tab, uint32_t flip, const RowLane &L) {
+template <int WA, int NW, class Lane>
+__device__ __forceinline__ rp_ext row_straus(uint32_t d[5], const uint32_t *tab, uint32_t flip, const Lane &L) {
   constexpr int TS = 1 << (WA - 1);
   rp_ext q = rp_identity(L);
   int top = NW - 1;
@@ -164,9 +172,9 @@ __device__ __forceinline__ rp_ext row_straus(uint32_t d[5], const uint32_t *tab,
 // q + the comb digits of half h of s (comb_add_b_half): positions
 // [h NP/2, (h+1) NP/2) of the CB-bit comb table tb; each lane reads its 16-bit
 // limb of the entry's three packed coordinates.
-template <int CB>
+template <int CB, class Lane>
 __device__ __forceinline__ rp_ext row_comb_half(rp_ext q, const uint32_t s[8], const uint32_t *tb, uint32_t h,
-                                                const RowLane &L) {
+                                                const Lane &L) {
   constexpr int NP = 256 / CB, HALF = NP / 2;
   constexpr int ENT = 1 << (CB - 1);
   uint32_t sr[9];

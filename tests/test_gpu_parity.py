@@ -38,22 +38,25 @@ def test_golden_every_variant(api, golden):
 
 
 def test_golden_row_form_chunks(api, golden):
-    """Batches at or below the row form's cut-over (HSV_ROW_MAX, default 1024)
-    run hsv_verify_row_kernel: the golden records in chunks of 1000 and in
-    ragged small batches (1, 5, 7, 13 items: partial blocks of six items),
-    every flag bit against the fixtures.  The committee cache is off so the
-    generic kernels run."""
+    """Batches at or below the row form's cut-over (HSV_ROW_MAX, default 3072)
+    run hsv_verify_row_kernel: the golden records in chunks of 1000 (one row
+    per element) and of 700 (at or below 768 items: two rows per element), and
+    in ragged small batches (1, 5, 7, 13 items: partial blocks), every flag bit
+    against the fixtures.  The committee cache is off so the generic kernels
+    run."""
     _, verifier, _ = api
     from hsverify import _lib
     lib = _lib.load()
     lib.hsv_set_auto_committee(0)
     try:
         n = len(golden["flags"])
-        for lo in range(0, n, 1000):
-            hi = min(n, lo + 1000)
-            got = verifier.verify_flags(golden["pk"][lo:hi], golden["sig"][lo:hi], golden["msg"][lo:hi])
-            bad = np.nonzero(got != golden["flags"][lo:hi])[0]
-            assert bad.size == 0, [(golden["cases"][lo + i], int(got[i]), int(golden["flags"][lo + i])) for i in bad[:8]]
+        for chunk in (1000, 700):
+            for lo in range(0, n, chunk):
+                hi = min(n, lo + chunk)
+                got = verifier.verify_flags(golden["pk"][lo:hi], golden["sig"][lo:hi], golden["msg"][lo:hi])
+                bad = np.nonzero(got != golden["flags"][lo:hi])[0]
+                assert bad.size == 0, [(chunk, golden["cases"][lo + i], int(got[i]), int(golden["flags"][lo + i]))
+                                       for i in bad[:8]]
         lo = 0
         for m in (1, 5, 7, 13, 1, 6, 12):
             got = verifier.verify_flags(golden["pk"][lo:lo + m], golden["sig"][lo:lo + m], golden["msg"][lo:lo + m])

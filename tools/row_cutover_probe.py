@@ -2,10 +2,13 @@
 """Cut-over between the row-form latency kernel and the pair form: p50 of a
 generic hsv_verify call (committee cache off) at several batch sizes, one
 process with the row form forced (HSV_ROW_MAX=1<<13) and one with it off
-(HSV_ROW_MAX=0).
+(HSV_ROW_MAX=0); or the environment settings named on the command line, one
+process each (e.g. HSV_ROW2_MAX=8192 HSV_ROW2_MAX=0: two rows per element
+against one).
 
-python tools/row_cutover_probe.py
+python tools/row_cutover_probe.py [--sizes 64,256,...] [NAME=V[,NAME=V] ...]
 """
+import argparse
 import json
 import os
 import subprocess
@@ -21,7 +24,7 @@ lib = _lib.load()
 lib.hsv_set_auto_committee(0)
 w = synth.independent_triples(8192, seed=77, corrupt_frac=0.05, nthreads=16)
 out = {{}}
-for n in (64, 256, 512, 1024, 1536, 2048, 3072, 4096, 8192):
+for n in {sizes!r}:
     args = (w.pk[:n], w.sig[:n], w.msg[:n])
     for _ in range(5):
         verifier.verify_flags(*args)
@@ -36,12 +39,19 @@ print(json.dumps(out))
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sizes", default="64,256,512,1024,1536,2048,3072,4096,8192")
+    ap.add_argument("configs", nargs="*", default=["HSV_ROW_MAX=8192", "HSV_ROW_MAX=0"])
+    a = ap.parse_args()
+    sizes = tuple(int(x) for x in a.sizes.split(","))
     for rnd in range(2):
-        for rm in ("8192", "0"):
-            r = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT)], capture_output=True, text=True,
-                               timeout=600, env=dict(os.environ, HSV_ROW_MAX=rm))
+        for cfg in a.configs:
+            env = dict(os.environ)
+            env.update(kv.split("=", 1) for kv in cfg.split(","))
+            r = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT, sizes=sizes)], capture_output=True,
+                               text=True, timeout=600, env=env)
             line = r.stdout.strip().splitlines()[-1] if r.returncode == 0 else f"rc={r.returncode} {r.stderr[-400:]}"
-            print(json.dumps({"HSV_ROW_MAX": rm, "p50_ms_by_n": line}), flush=True)
+            print(json.dumps({"env": cfg, "p50_ms_by_n": line}), flush=True)
     return 0
 
 
