@@ -702,7 +702,7 @@ hsv_verify_pair_fused_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
 // Row form of the latency kernel (default at <= kRowMax items): every field
 // product of a verification spread over a 16-lane DPP row (hsv_rowpoint.hpp),
 // two rows per item as the pair form's two lanes.  A block of four waves takes
-// kRowItems items: waves 0-2 hold 12 rows (row 2i decompresses R of item i and
+// 6 items (RR = 1): waves 0-2 hold 12 rows (row 2i decompresses R of item i and
 // builds [0..8](-R), row 2i + 1 the same for A, tables in LDS), wave 3 runs the
 // scalar prepass of the block's items into an LDS record meanwhile.  After the
 // barrier each row runs its one-scalar Straus (c1 for R, |c0| for A) and half
@@ -1232,8 +1232,8 @@ hipError_t launch_pair(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig
   return e != hipSuccess ? e : ef;
 }
 
-// Row form (variant 21 at <= row_max() items): kRowItems items per block of
-// four waves.  The workspace holds one full-length table and one canary per
+// Row form (variant 21 at <= row_max() items): kRowItemsOf<RR> items per
+// block of four waves.  The workspace holds one full-length table and one canary per
 // row (the fallback path's tables; the row tables live in LDS).
 uint32_t row_max() {  // HSV_ROW_MAX: measurement switch (0: always the pair form)
   static const uint32_t m = [] {
