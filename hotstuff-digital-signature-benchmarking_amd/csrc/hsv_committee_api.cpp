@@ -108,7 +108,11 @@ int committee_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t
     std::memset(h + fault_off, 0, kFaultBytes);
     void *hd = nullptr;
     uint8_t *dbuf = s.d_buf;
-    const bool zero_copy = k <= kZeroCopyMax && hipHostGetDevicePointer(&hd, h, 0) == hipSuccess && hd;
+    static const size_t zc_max = [] {  // HSV_COMMITTEE_ZC_MAX: measurement switch
+      const char *v = std::getenv("HSV_COMMITTEE_ZC_MAX");
+      return v ? (size_t)std::atoll(v) : kZeroCopyMax;
+    }();
+    const bool zero_copy = k <= zc_max && hipHostGetDevicePointer(&hd, h, 0) == hipSuccess && hd;
     if (zero_copy) {
       dbuf = static_cast<uint8_t *>(hd);
     } else {
