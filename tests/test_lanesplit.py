@@ -37,6 +37,14 @@ def test_row_point_formula_bounds_model():
     assert st["out"] < 2**16.3
 
 
+def test_two_row_product_bounds_model():
+    """The two-row product (RowLane2) keeps every instruction bound and gives
+    the one-row product's limbs exactly, for operands up to 2^18.4."""
+    import lanesplit_model
+    st = lanesplit_model.run_two_row(trials=120, seed=9)
+    assert st["out"] < 2**16.7
+
+
 def _words(v):
     return [(v >> (32 * i)) & 0xFFFFFFFF for i in range(8)]
 

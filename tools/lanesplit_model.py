@@ -60,6 +60,66 @@ def fl_mul(f, g, stats=None):
     return out
 
 
+def fl2_mul(f, g, stats=None):
+    """The two-row product (hsv_fe16x16.hpp, fl2_mul): the even row steps
+    0..7 from (f, g), the odd row steps 8..15 from f and g turned by 8 lanes
+    (g's wrapped half times 38); each row splits its half column sums at bit
+    16 and the pair adds the halves (v_permlane16_swap) before the carry
+    passes.  Asserts the same instruction bounds as fl_mul."""
+    def half(fr, gr):
+        acc = [0] * 16
+        for i in range(8):
+            if i:
+                src = [gr[(k - 1) % 16] for k in range(16)]  # DPP row_ror:1
+                assert max(src) < 2**24, "v_mul_u32_u24 input"
+                gr = [x * (38 if k == 0 else 1) for k, x in enumerate(src)]
+            for k in range(16):
+                acc[k] += fr[i] * gr[k]
+        assert max(acc) < 2**64
+        t = [a >> 16 for a in acc]
+        assert max(t) < 2**32, "half carry (v_alignbit_b32)"
+        return [a & 0xFFFF for a in acc], t
+    g8 = [g[(k - 8) % 16] for k in range(16)]  # row_ror:8 on the odd row
+    assert max(g8) < 2**24, "v_mul_u32_u24 input (odd row start)"
+    g8 = [x * (38 if k < 8 else 1) for k, x in enumerate(g8)]
+    lo_e, t_e = half(list(f), list(g))
+    lo_o, t_o = half([f[(i + 8) % 16] for i in range(16)], g8)
+    t = [a + b for a, b in zip(t_e, t_o)]
+    t = [x * (38 if k == 15 else 1) for k, x in enumerate(t)]
+    assert max(t) < 2**32, "summed carry times 38"
+    x = [lo_e[k] + lo_o[k] + t[(k - 1) % 16] for k in range(16)]
+    assert max(x) < 2**32
+    lo = [a & 0xFFFF for a in x]
+    c = [a >> 16 for a in x]
+    assert max(c) < 2**24, "pass-2 carry (v_mul_u32_u24)"
+    c = [v * (38 if k == 15 else 1) for k, v in enumerate(c)]
+    out = [lo[k] + c[(k - 1) % 16] for k in range(16)]
+    assert value(out) % P == value(f) * value(g) % P
+    if stats is not None:
+        stats["out"] = max(stats.get("out", 0), max(out))
+    return out
+
+
+def run_two_row(trials=200, seed=5):
+    """fl2_mul on the operands run() and run_points() feed fl_mul: limbs up
+    to 2^16.05 (product outputs) and up to 2^18.4 (sums and differences, the
+    largest operand hsv_rowpoint.hpp forms).  Its limbs equal fl_mul's, so
+    every bound of the one-row model carries over."""
+    rnd = random.Random(seed)
+    st = {}
+    for top in (int(2**16.05), 2**17, int(2**18.4)):
+        for _ in range(trials // 4):
+            f = [rnd.choice([0, 0xFFFF, rnd.randrange(top + 1), top]) for _ in range(16)]
+            g = [rnd.choice([0, 0xFFFF, rnd.randrange(top + 1), top]) for _ in range(16)]
+            y = fl2_mul(f, g, st)
+            assert y == fl_mul(f, g), "two-row and one-row products differ"
+            for _ in range(3):
+                y = fl2_mul(y, y, st)
+    x = [int(2**18.4)] * 16
+    fl2_mul(x, x, st)
+    return st
+
+
 def run(trials=400, seed=1):
     rnd = random.Random(seed)
     st = {}
@@ -184,3 +244,5 @@ if __name__ == "__main__":
     print("products", {k: round(math.log2(v), 4) for k, v in st.items()})
     st = run_points()
     print("point formulas", {k: round(math.log2(v), 4) for k, v in st.items()})
+    st = run_two_row()
+    print("two-row products", {k: round(math.log2(v), 4) for k, v in st.items()})
