@@ -211,18 +211,29 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
     if (threadIdx.x == 0) k_ready = 0u;
     __syncthreads();
     if (wave == kHashWaveIdx) {
+      // one lane per vote hashes (lanes 0..kFusedVotes-1); the rest of the
+      // wave stays masked off (HSV_COMB_HASH_ALL_LANES: every lane, as the
+      // comb wave's lanes did)
+#ifdef HSV_COMB_HASH_ALL_LANES
+      const bool hashes = true;
       const uint32_t vl = lane / kCombLanes, g = lane % kCombLanes;
-      const uint32_t i = base + vl < m ? base + vl : m - 1u;
-      const uint32_t kidx = key_idx[i];
-      const uint32_t kk = kidx < nkeys ? kidx : 0u;
-      uint32_t pkw[8], sigw[16], msgw[8], h[16], kr[9];
-      load_vote_words(pks, kk, sig, sig_stride, msg, msg_stride, i, pkw, sigw, msgw);
-      sha512_96(sigw, pkw, msgw, h);
-      const sc k = sc_reduce512(h);
-      recode_add<9, 8, kCombPos>(k.v, 8, kr);
-      if (g == 0u) {
-        HSV_UNROLL
-        for (int w = 0; w < 9; ++w) k_rec[vl][w] = kr[w];
+#else
+      const bool hashes = lane < (uint32_t)kFusedVotes;
+      const uint32_t vl = lane, g = 0u;
+#endif
+      if (hashes) {
+        const uint32_t i = base + vl < m ? base + vl : m - 1u;
+        const uint32_t kidx = key_idx[i];
+        const uint32_t kk = kidx < nkeys ? kidx : 0u;
+        uint32_t pkw[8], sigw[16], msgw[8], h[16], kr[9];
+        load_vote_words(pks, kk, sig, sig_stride, msg, msg_stride, i, pkw, sigw, msgw);
+        sha512_96(sigw, pkw, msgw, h);
+        const sc k = sc_reduce512(h);
+        recode_add<9, 8, kCombPos>(k.v, 8, kr);
+        if (g == 0u) {
+          HSV_UNROLL
+          for (int w = 0; w < 9; ++w) k_rec[vl][w] = kr[w];
+        }
       }
       __hip_atomic_store(&k_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       __syncthreads();
