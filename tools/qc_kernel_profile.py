@@ -6,7 +6,7 @@ warm (hsv_comb_verify_quad_fused_kernel) and 200 with it off
 p50s of bench.py.
 
 cd /tmp && rocprofv3 --kernel-trace --stats --output-format csv -d DIR -o qc -- \\
-    python3 /root/repo/tools/qc_kernel_profile.py
+    python3 /root/repo/tools/qc_kernel_profile.py [VOTES]
 """
 import os
 import sys
@@ -18,17 +18,20 @@ sys.path.insert(0, os.path.join(ROOT, "hotstuff-digital-signature-benchmarking_a
 
 from hsverify import _lib, synth  # noqa: E402
 
+# argv[1]: votes per QC (default 667, C3; 3 for C1), from a committee of 1000
+votes = int(sys.argv[1]) if len(sys.argv) > 1 else 667
 lib = _lib.load()
 w = synth.qc_votes(1000, seed=1000)
-packed = np.concatenate([w.pk, w.sig], axis=1).tobytes()
-digest = bytes(w.msg)
+rows = np.concatenate([w.pk, w.sig], axis=1)
 lib.hsv_set_auto_committee(1)
 for _ in range(3):
-    lib.hsv_verify_batch_packed(digest, packed, w.n)
+    lib.hsv_verify_batch_packed(bytes(w.msg), rows.tobytes(), w.n)
 lib.hsv_auto_committee_wait(60000)
-ok = all(lib.hsv_verify_batch_packed(digest, packed, w.n) == 1 for _ in range(200))
+packed = rows[:votes].tobytes()
+digest = bytes(w.msg)
+ok = all(lib.hsv_verify_batch_packed(digest, packed, votes) == 1 for _ in range(200))
 lib.hsv_set_auto_committee(0)
-ok &= all(lib.hsv_verify_batch_packed(digest, packed, w.n) == 1 for _ in range(200))
+ok &= all(lib.hsv_verify_batch_packed(digest, packed, votes) == 1 for _ in range(200))
 lib.hsv_set_auto_committee(1)
 print("all accepted" if ok else "VERDICT MISMATCH", flush=True)
 sys.exit(0 if ok else 1)
