@@ -200,7 +200,8 @@ def cpu_baseline(w, gpu_flags, sample):
 
 def _p(ts):
     ts = np.array(ts) * 1e3
-    return {"p50_ms": float(np.percentile(ts, 50)), "p99_ms": float(np.percentile(ts, 99)), "reps": len(ts)}
+    return {"p50_ms": float(np.percentile(ts, 50)), "p99_ms": float(np.percentile(ts, 99)),
+            "p999_ms": float(np.percentile(ts, 99.9)), "max_ms": float(ts.max()), "reps": len(ts)}
 
 
 def _timed(fn, reps, warm=10):
@@ -212,6 +213,64 @@ def _timed(fn, reps, warm=10):
         fn()
         ts.append(time.perf_counter() - t0)
     return ts
+
+
+MARKS = ("lookup", "slot", "staged", "launch", "sync", "done")  # hsv.h HSV_MARK_*
+
+
+def _timed_lib(fn, reps, warm=10):
+    """Latency of a libhsv call, with its attribution (round-3 VERDICT item 3).
+
+    Every rep keeps its wall time and the library's host timeline of that call
+    (hsv_host_call_marks: cache lookup, slot lease, staging, launch enqueue,
+    stream synchronisation, exit; ms from the library's entry).  Python's
+    cyclic garbage collector is paused while the reps run: the reference's
+    callers are Rust and have no collector, and a gen-2 collection of this
+    process (torch loaded) would land in a rep as a pause of its own.  The
+    reps above p99 are returned with their phases next to the median rep's."""
+    import ctypes
+    import gc
+    from hsverify import _lib
+    lib = _lib.load()
+    buf = (ctypes.c_double * 8)()
+    for _ in range(warm):
+        fn()
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    ts, marks = [], []
+    try:
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+            n = lib.hsv_host_call_marks(buf, 8)
+            marks.append([buf[i] for i in range(min(n, len(MARKS)))] if n == len(MARKS) else None)
+    finally:
+        if was:
+            gc.enable()
+    out = _p(ts)
+    wall = np.array(ts) * 1e3
+    if all(m is not None for m in marks):
+        m = np.array(marks)                                   # (reps, 6), -1: mark not passed
+        step = np.diff(np.concatenate([np.zeros((len(m), 1)), np.maximum(m, 0)], axis=1), axis=1)
+        step[m < 0] = 0.0                                     # per-phase ms (a skipped phase is 0)
+        lib_ms = m[:, -1]
+        phases = lambda rows: {k: round(float(np.median(step[rows, j])), 4) for j, k in enumerate(MARKS)}
+        cut = np.percentile(wall, 99)
+        tail = np.nonzero(wall > cut)[0]
+        out["lib_p50_ms"] = float(np.median(lib_ms))
+        out["lib_p99_ms"] = float(np.percentile(lib_ms, 99))
+        out["median_phases_ms"] = phases(np.arange(len(m)))
+        out["tail"] = {
+            "reps_above_p99": int(len(tail)),
+            "phases_ms": phases(tail) if len(tail) else {},
+            "outside_lib_ms": round(float(np.median(wall[tail] - lib_ms[tail])), 4) if len(tail) else None,
+            "rep_index": tail.tolist()[:16],
+            "wall_ms": [round(float(x), 4) for x in wall[tail][:16]],
+        }
+        out["outside_lib_p50_ms"] = round(float(np.median(wall - lib_ms)), 4)
+    return out
 
 
 def member_corrupted(make, committee, seed, frac=0.05):
@@ -257,7 +316,7 @@ def qc_latency(reps, auto=True):
         call = lambda: lib.hsv_verify_batch_packed(digest, packed, w.n)
         settle(call)
         assert call() == 1
-        res[f"n{committee}_votes{w.n}"] = _p(_timed(call, reps))
+        res[f"n{committee}_votes{w.n}"] = _timed_lib(call, reps)
     # C3 with 5 % corrupted votes (member keys): Err, every flag computed
     w = member_corrupted(synth.qc_votes, 1000, seed=1000)
     packed = np.concatenate([w.pk, w.sig], axis=1).tobytes()
@@ -265,14 +324,14 @@ def qc_latency(reps, auto=True):
     call = lambda: lib.hsv_verify_batch_packed(digest, packed, w.n)
     settle(call)
     assert call() == 0
-    res["n1000_votes667_corrupt5pct"] = dict(_p(_timed(call, reps)), corrupted=int((~w.accept).sum()))
+    res["n1000_votes667_corrupt5pct"] = dict(_timed_lib(call, reps), corrupted=int((~w.accept).sum()))
     # one strict verification (Vote::verify / Block::verify, consensus/src/messages.rs:136-146)
     w = synth.qc_votes(4, seed=4)
     pk0, sig0, d0 = bytes(w.pk[0]), bytes(w.sig[0]), bytes(w.msg)
     settle(lambda: lib.hsv_verify_batch_packed(d0, np.concatenate([w.pk, w.sig], 1).tobytes(), w.n))
     call = lambda: lib.hsv_verify_strict(d0, pk0, sig0)
     assert call() == 1
-    res["single_verify_strict"] = _p(_timed(call, reps))
+    res["single_verify_strict"] = _timed_lib(call, reps)
     # the C3 QC handed over as its bincode wire bytes (hsv_qc_verify_bincode:
     # parse + base64 keys + qc.digest() on the host, verification on the GPU)
     w = synth.qc_votes(1000, seed=1000)
@@ -282,7 +341,7 @@ def qc_latency(reps, auto=True):
     call = lambda: lib.hsv_qc_verify_bincode(buf, len(buf), ctypes.byref(nv), None)
     settle(call)
     assert call() == 1
-    res["n1000_votes667_bincode"] = dict(_p(_timed(call, reps)), bytes=len(buf))
+    res["n1000_votes667_bincode"] = dict(_timed_lib(call, reps), bytes=len(buf))
     return res
 
 
@@ -306,7 +365,7 @@ def tc_latency(reps, auto=True):
                 lib.hsv_verify_batch_packed(bytes(q.msg), pq, q.n)
             lib.hsv_auto_committee_wait(60000)
         call = lambda: lib.hsv_verify(pk.ctypes.data, sig.ctypes.data, msg.ctypes.data, 32, w.n, flags.ctypes.data)
-        res[f"n1000_votes667_{tag}_batched_strict"] = _p(_timed(call, reps))
+        res[f"n1000_votes667_{tag}_batched_strict"] = _timed_lib(call, reps)
         assert bool((flags & 1).all()) == (frac == 0)
         hqc = tc_hqc(1000, 1000)
         buf = wire.encode_tc(1000, [(bytes(p), bytes(s), int(h)) for p, s, h in zip(w.pk, w.sig, hqc)])
@@ -314,7 +373,7 @@ def tc_latency(reps, auto=True):
         call = lambda: lib.hsv_tc_verify_bincode(buf, len(buf), ctypes.byref(nv), None)
         rc = call()
         assert rc == (1 if frac == 0 else 0)
-        res[f"n1000_votes667_{tag}_bincode"] = dict(_p(_timed(call, reps)), bytes=len(buf))
+        res[f"n1000_votes667_{tag}_bincode"] = dict(_timed_lib(call, reps), bytes=len(buf))
     return res
 
 
@@ -336,7 +395,7 @@ def committee_bench(reps, dev, n_votes=1 << 20):
         h = c._h
         call = lambda: lib.hsv_committee_verify_batch_packed(h, digest, packed, w.n)
         assert call() == 1
-        res[f"qc_n{size}_votes{w.n}"] = dict(_p(_timed(call, reps)), table_build_ms=build_ms)
+        res[f"qc_n{size}_votes{w.n}"] = dict(_timed_lib(call, reps), table_build_ms=build_ms)
         c.close()
     # throughput: n_votes votes, each by one of 1000 members over its own digest
     seeds = synth.committee_seeds(1000, 7)
@@ -613,9 +672,13 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     _lib.load()
-    verifier.bind_device(local_rank)  # this rank's host-buffer calls stay on its GPU
     if a.variant is not None:
+        # a measurement run of another variant: every call goes to the test
+        # library (the product libhsv.so exports no variant switch)
+        _lib.set_override(_lib.load_test())
+        log(f"--variant {a.variant}: measuring libhsv_test.so (the product objects plus the hooks)")
         verifier.set_variant(a.variant)
+    verifier.bind_device(local_rank)  # this rank's host-buffer calls stay on its GPU
 
     host_threads = max(1, host_cores()[0] // max(1, world))
     t0 = time.perf_counter()

@@ -10,7 +10,9 @@
 // into the caller's output (the "host gather").  There is no CPU
 // verification path: without a GPU every call returns HSV_ERR_NO_DEVICE.
 #include <hip/hip_runtime_api.h>
+#if defined(__SSE2__)
 #include <emmintrin.h>
+#endif
 
 #include <algorithm>
 #include <atomic>
@@ -36,6 +38,16 @@ namespace {
 thread_local std::string t_last_error;
 
 constexpr int kUnbound = -2;
+
+// Host timeline of the calling thread's current / last public call
+// (hsv_host_call_marks).  CallScope opens it at every public entry point; a
+// nested entry (hsv_verify_strict -> hsv_verify) joins the outer call.
+struct CallClock {
+  int depth = 0;
+  std::chrono::steady_clock::time_point t0;
+  std::vector<double> marks;
+};
+thread_local CallClock t_clock;
 
 struct Global {
   std::mutex mu;
@@ -74,6 +86,29 @@ int hip_fail(const char *where, hipError_t e) {
 
 const std::string &last_error() { return t_last_error; }
 
+CallScope::CallScope() {
+  CallClock &c = t_clock;
+  if (c.depth++ == 0) {
+    c.t0 = std::chrono::steady_clock::now();
+    c.marks.assign(HSV_MARKS, -1.0);
+  }
+}
+
+CallScope::~CallScope() { --t_clock.depth; }
+
+static double clock_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_clock.t0).count();
+}
+
+void call_mark(int which) {
+  CallClock &c = t_clock;
+  if (c.depth > 0 && which >= 0 && (size_t)which < c.marks.size()) c.marks[which] = clock_ms();
+}
+
+void call_chunk_mark() {
+  if (t_clock.depth > 0) t_clock.marks.push_back(clock_ms());
+}
+
 int ensure_init() {
   Global &g = G();
   std::lock_guard<std::mutex> lk(g.mu);
@@ -92,7 +127,7 @@ int ensure_init() {
     g.ctx.push_back(c);
   }
   const int v = env_int("HSV_VARIANT", -1);
-  if (v >= 0 && hsv_variant_available(v)) g.variant = v;
+  if (v >= 0 && hsvi_variant_available(v)) g.variant = v;
   const int d = env_int("HSV_DEVICE", kUnbound);
   if (g.bound.load() == kUnbound && d >= -1 && d < n) g.bound = d;
   const int vs = env_int("HSV_VIRTUAL_SHARDS", 0);
@@ -387,12 +422,19 @@ constexpr size_t kPackPart = size_t(1) << 20;  // bytes per part of a split copy
 // only pays a read-for-ownership of a line nobody reads back: one thread packs
 // records at 37 GB/s this way against 16 GB/s with memcpy
 // (profiles/r03v_pack_probe.txt).  SSE2, baseline x86-64.
+// Other hosts: plain copies (the kernels do not depend on this).
+#if defined(__SSE2__)
 inline void nt_copy32(uint8_t *dst, const uint8_t *src) {
   const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src));
   const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + 16));
   _mm_stream_si128(reinterpret_cast<__m128i *>(dst), a);
   _mm_stream_si128(reinterpret_cast<__m128i *>(dst + 16), b);
 }
+inline void nt_fence() { _mm_sfence(); }
+#else
+inline void nt_copy32(uint8_t *dst, const uint8_t *src) { std::memcpy(dst, src, 32); }
+inline void nt_fence() {}
+#endif
 
 // items [lo, hi) as records pk | R || s (| digest) at dst + rec * i; dst and
 // rec multiples of 16 (pinned staging is page-aligned, rec is 96 or 128)
@@ -405,7 +447,7 @@ void pack_records(uint8_t *dst, size_t rec, const uint8_t *pk, size_t pk_stride,
     nt_copy32(r + 64, sig + i * sig_stride + 32);
     if (msg_stride) nt_copy32(r + 96, msg + i * msg_stride);
   }
-  _mm_sfence();  // streaming stores are weakly ordered: visible before the copy is enqueued
+  nt_fence();  // streaming stores are weakly ordered: visible before the copy is enqueued
 }
 
 // bytes from src to dst, with streaming stores for large copies to a
@@ -417,7 +459,7 @@ void nt_copy(uint8_t *dst, const uint8_t *src, size_t bytes) {
   }
   size_t o = 0;
   for (; o + 32 <= bytes; o += 32) nt_copy32(dst + o, src + o);
-  _mm_sfence();
+  nt_fence();
   if (o < bytes) std::memcpy(dst + o, src + o, bytes - o);
 }
 
@@ -460,6 +502,15 @@ int device_fault_words(DevCtx &c, uint32_t **out) {
     c.d_fault = p;
   }
   *out = c.d_fault;
+  return HSV_OK;
+}
+
+int call_fault_words(DevCtx &c, uint32_t *d_fault, hipStream_t stream, uint32_t **out) {
+  if (!d_fault) return device_fault_words(c, out);
+  if (reinterpret_cast<uintptr_t>(d_fault) & 3u) return fail(HSV_ERR_ALIGN, "d_fault must be 4-byte aligned");
+  const hipError_t e = hipMemsetAsync(d_fault, 0, kFaultBytes, stream);
+  if (e != hipSuccess) return hip_fail("zeroing the call's self-check words", e);
+  *out = d_fault;
   return HSV_OK;
 }
 
@@ -583,10 +634,6 @@ std::vector<size_t> pipe_schedule(size_t n) {
 // copied host-to-device, and the call's wall time.
 thread_local double t_pack_ms = 0, t_call_ms = 0;
 thread_local uint64_t t_h2d_bytes = 0;
-// per-chunk host timestamps of the last pipelined call (ms from its start):
-// waited for the staging buffer, packed, copies enqueued, launch enqueued
-thread_local std::vector<double> t_chunk_marks;
-
 double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -647,8 +694,7 @@ int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, siz
   if (e == hipSuccess && msg_stride == 0) e = hipMemcpyAsync(d + d_dig, msg, 32, hipMemcpyHostToDevice, s.copy);
   if (e != hipSuccess) return drain(hip_fail("hipMemsetAsync", e));
   bool used[2] = {false, false};
-  const auto t_start = std::chrono::steady_clock::now();
-  t_chunk_marks.clear();
+  t_clock.marks.clear();  // four marks per chunk instead of the HSV_MARK_* points
   for (size_t base = 0, k = 0, m = 0; k < sizes.size(); base += m, ++k) {
     m = sizes[k];
     const int b = (int)(k & 1);
@@ -657,7 +703,7 @@ int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, siz
       e = hipEventSynchronize(staged[b]);
       if (e != hipSuccess) return drain(hip_fail("hipEventSynchronize", e));
     }
-    t_chunk_marks.push_back(ms_since(t_start));
+    call_chunk_mark();
     uint8_t *dc = d + base * rec;  // chunk k's records in HBM
     // Items as records pk | R || s (| digest), so any item range is one
     // contiguous copy.  A full-size first chunk (HSV_PIPE_FIRST_LOG2) goes in
@@ -678,18 +724,18 @@ int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, siz
       e = hipMemcpyAsync(dc + lo0 * rec, h + lo0 * rec, (hi0 - lo0) * rec, hipMemcpyHostToDevice, s.copy);
       if (e != hipSuccess) return drain(hip_fail("hipMemcpyAsync H2D", e));
     }
-    t_chunk_marks.push_back(ms_since(t_start));
+    call_chunk_mark();
     e = hipEventRecord(staged[b], s.copy);
     if (e == hipSuccess) e = hipStreamWaitEvent(comp[b], staged[b], 0);
     if (e != hipSuccess) return drain(hip_fail("staging a chunk", e));
     used[b] = true;
-    t_chunk_marks.push_back(ms_since(t_start));
+    call_chunk_mark();
     t_h2d_bytes += m * rec;
     e = hsv_launch_verify_ws(v, dc, rec, dc + 32, rec, msg_stride ? dc + 96 : d + d_dig, msg_stride ? rec : 0,
                              (uint32_t)m, d + d_flag + base, nullptr, comb_b,
                              reinterpret_cast<uint32_t *>(d + d_fault), s.d_ws[b], s.ws_cap, comp[b]);
     if (e != hipSuccess) return drain(hip_fail("verify kernel launch", e));
-    t_chunk_marks.push_back(ms_since(t_start));
+    call_chunk_mark();
   }
   // join: the flags come back once both compute streams are done
   e = hipEventRecord(s.ev[3], s.stream2);
@@ -720,6 +766,7 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
   if (rc != HSV_OK) return rc;
   SlotLease lease(c);
   Slot &s = lease.slot();
+  call_mark(HSV_MARK_SLOT);
   const size_t pchunk = pipe_chunk();
   if (!no_pipe && n >= 2 * pchunk) {
     for (size_t base = 0; base < n; base += kChunk) {
@@ -768,6 +815,7 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
     std::memset(h + flag_off, 0, m);
     std::memset(h + fault_off, 0, kFaultBytes);
     t_pack_ms += ms_since(t_pack);
+    call_mark(HSV_MARK_STAGED);
     hipError_t e;
     void *hd = nullptr;
     if (!no_zero_copy && n <= kZeroCopyMax && hipHostGetDevicePointer(&hd, h, 0) == hipSuccess && hd) {
@@ -793,12 +841,15 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
         e = hipMemcpyAsync(h + flag_off, d + flag_off, fault_off + kFaultBytes - flag_off, hipMemcpyDeviceToHost,
                            st);
     }
+    call_mark(HSV_MARK_LAUNCH);
     const hipError_t es = hipStreamSynchronize(st);  // nothing of this call stays in flight
+    call_mark(HSV_MARK_SYNC);
     if (e != hipSuccess) return hip_fail("verify launch", e);
     if (es != hipSuccess) return hip_fail("hipStreamSynchronize", es);
     rc = check_faults(h + fault_off, "verify");
     if (rc != HSV_OK) return rc;
     std::memcpy(flags_out + base, h + flag_off, m);
+    call_mark(HSV_MARK_DONE);
   }
   t_call_ms = ms_since(t_call);
   return HSV_OK;
@@ -818,10 +869,12 @@ int run_host(const uint8_t *pk, size_t pk_stride, const uint8_t *sig, size_t sig
   std::vector<int> rcs(k, HSV_OK);
   std::vector<std::string> errs(k);
   std::vector<std::thread> th;
+  const int inject = hsvi_inject_mode();  // the caller's (test) injection reaches its shards
   for (int d = 0; d < k; ++d) {
     const size_t lo = n * d / k, hi = n * (d + 1) / k;
     const int dev = shard_device(d, k);
-    th.emplace_back([&, d, lo, hi, dev]() {
+    th.emplace_back([&, d, lo, hi, dev, inject]() {
+      (void)hsvi_set_inject(inject);
       if (hi > lo)
         rcs[d] = run_on_device(ctx(dev), pk + lo * pk_stride, pk_stride, sig + lo * sig_stride, sig_stride,
                                msg + lo * msg_stride, msg_stride, hi - lo, flags_out + lo);
@@ -861,11 +914,11 @@ int hsv_bound_device(void) {
   return b == kUnbound ? -1 : b;
 }
 
-// Test hook (not in hsv.h): split host batches of >= 2^16 items into k
-// contiguous shards, each on its own host thread and slot, mapped onto the
-// bound device (or round-robin over the visible devices); k = 0 restores the
-// default.  Lets the multi-device gather path run on a one-GPU box.
-int hsv_set_virtual_shards(int k) {
+// Test hook (exported by libhsv_test.so only): split host batches of >= 2^16
+// items into k contiguous shards, each on its own host thread and slot, mapped
+// onto the bound device (or round-robin over the visible devices); k = 0
+// restores the default.  Lets the multi-device gather path run on a one-GPU box.
+int hsvi_set_virtual_shards(int k) {
   if (k < 0 || k > 64) return fail(HSV_ERR_INVALID_ARG, "virtual shards must be in [0, 64]");
   (void)ensure_init();
   G().virtual_shards = k;
@@ -941,9 +994,9 @@ const char *hsv_last_error(void) { return t_last_error.c_str(); }
 
 const char *hsv_version(void) { return "hsv 0.2.0 (gfx950)"; }
 
-// Measurement/test hooks (not in hsv.h): pick the kernel variant.
-int hsv_set_variant(int v) {
-  if (!hsv_variant_available(v)) return fail(HSV_ERR_INVALID_ARG, "variant not built into this library");
+// Measurement/test hook (exported by libhsv_test.so only): pick the kernel variant.
+int hsvi_set_variant(int v) {
+  if (!hsvi_variant_available(v)) return fail(HSV_ERR_INVALID_ARG, "variant not built into this library");
   G().variant = v;
   return HSV_OK;
 }
@@ -952,6 +1005,7 @@ int hsv_get_variant(void) { return G().variant.load(); }
 
 int hsv_verify(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, size_t msg_stride, size_t n,
                uint8_t *flags_out) {
+  CallScope call;
   if (msg_stride != 0 && msg_stride != 32) return fail(HSV_ERR_INVALID_ARG, "msg_stride must be 0 or 32");
   if (n && pk && sig && msg && flags_out) {
     const int rc = auto_committee_try(pk, sig, msg, msg_stride, n, flags_out);
@@ -968,6 +1022,7 @@ int hsv_verify_strict(const uint8_t digest[32], const uint8_t pk[32], const uint
 }
 
 int hsv_verify_batch(const uint8_t digest[32], const uint8_t *pk, const uint8_t *sig, size_t n) {
+  CallScope call;
   if (n == 0) return 1;  // dalek verify_batch over zero items is Ok
   if (!digest || !pk || !sig) return fail(HSV_ERR_INVALID_ARG, "null argument");
   std::vector<uint8_t> packed(n * 96);
@@ -980,7 +1035,7 @@ int hsv_verify_batch(const uint8_t digest[32], const uint8_t *pk, const uint8_t 
 
 int hsv_verify_device_bits(const uint8_t *d_pk, size_t pk_stride, const uint8_t *d_sig, size_t sig_stride,
                            const uint8_t *d_msg, size_t msg_stride, size_t n, uint8_t *d_flags,
-                           uint32_t *d_strict_bits, void *stream) {
+                           uint32_t *d_strict_bits, uint32_t *d_fault, void *stream) {
   if (n == 0) return HSV_OK;
   if (!d_pk || !d_sig || !d_msg) return fail(HSV_ERR_INVALID_ARG, "null input pointer");
   if (!d_flags && !d_strict_bits) return fail(HSV_ERR_INVALID_ARG, "no output");
@@ -1001,10 +1056,10 @@ int hsv_verify_device_bits(const uint8_t *d_pk, size_t pk_stride, const uint8_t 
   DevCtx &c = ctx(dev);
   rc = comb_table_for(c, v, &comb_b);
   if (rc != HSV_OK) return rc;
-  uint32_t *fault = nullptr;
-  rc = device_fault_words(c, &fault);
-  if (rc != HSV_OK) return rc;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  uint32_t *fault = nullptr;
+  rc = call_fault_words(c, d_fault, s, &fault);
+  if (rc != HSV_OK) return rc;
   // Batches of several kChunk launches alternate them over the caller's stream
   // and a second library stream leased for this call (fork/join through
   // events on the caller's stream): a chunk's launch starts on the SIMDs the
@@ -1042,7 +1097,8 @@ int hsv_verify_device_bits(const uint8_t *d_pk, size_t pk_stride, const uint8_t 
 int hsv_verify_device(const uint8_t *d_pk, size_t pk_stride, const uint8_t *d_sig, size_t sig_stride,
                       const uint8_t *d_msg, size_t msg_stride, size_t n, uint8_t *d_flags, void *stream) {
   if (!d_flags && n) return fail(HSV_ERR_INVALID_ARG, "null d_flags");
-  return hsv_verify_device_bits(d_pk, pk_stride, d_sig, sig_stride, d_msg, msg_stride, n, d_flags, nullptr, stream);
+  return hsv_verify_device_bits(d_pk, pk_stride, d_sig, sig_stride, d_msg, msg_stride, n, d_flags, nullptr, nullptr,
+                                stream);
 }
 
 int hsv_device_faults(int device, int clear) {
@@ -1062,17 +1118,31 @@ int hsv_device_faults(int device, int clear) {
     DeviceGuard guard(d);
     if (guard.status() != hipSuccess) return hip_fail("hipSetDevice", guard.status());
     uint32_t w[2] = {0, 0};
-    hipError_t e = hipMemcpy(w, words, sizeof(w), hipMemcpyDeviceToHost);
-    if (e == hipSuccess && clear) e = hipMemset(words, 0, sizeof(w));
+    hipError_t e;
+    if (clear) {
+      // one atomic exchange per word on the device: a fault that a launch on
+      // another stream records concurrently is either in `w` or stays in the
+      // word for the next read -- never cleared unseen (a copy followed by a
+      // memset could lose it).  Readers of one device take turns on the
+      // exchange's output words.
+      std::lock_guard<std::mutex> lk(c.fault_mu);
+      SideStreamLease side(c);
+      if (!side.stream()) return fail(HSV_ERR_HIP, "no stream for the fault-word exchange");
+      e = hsv_launch_fault_exchange(words, words + kFaultOutWord, side.stream());
+      if (e == hipSuccess) e = hipMemcpyAsync(w, words + kFaultOutWord, sizeof(w), hipMemcpyDeviceToHost, side.stream());
+      if (e == hipSuccess) e = hipStreamSynchronize(side.stream());
+    } else {
+      e = hipMemcpy(w, words, sizeof(w), hipMemcpyDeviceToHost);
+    }
     if (e != hipSuccess) return hip_fail("reading the device self-check words", e);
     bits |= (w[0] ? 1 : 0) | (w[1] ? 2 : 0);
   }
   return bits;
 }
 
-// Measurement hook (not in hsv.h): the calling thread's last host-buffer
-// verification -- host milliseconds spent packing into pinned staging, bytes
-// copied host-to-device, and the call's wall milliseconds.
+// The calling thread's last host-buffer verification (hsv.h): host
+// milliseconds spent packing into pinned staging, bytes copied host-to-device,
+// and the call's wall milliseconds.
 void hsv_host_call_stats(double *pack_ms, double *h2d_bytes, double *call_ms) {
   if (pack_ms) *pack_ms = t_pack_ms;
   if (h2d_bytes) *h2d_bytes = (double)t_h2d_bytes;
@@ -1081,11 +1151,12 @@ void hsv_host_call_stats(double *pack_ms, double *h2d_bytes, double *call_ms) {
 
 int hsv_pack_threads(void) { return PackPool::get().threads(); }
 
-// Measurement hook (not in hsv.h): the per-chunk host marks of the calling
-// thread's last pipelined call (4 per chunk, see t_chunk_marks); returns the count.
+// The host timeline of the calling thread's last call (hsv.h HSV_MARK_*, or
+// four marks per chunk of a pipelined call); returns the count.
 int hsv_host_call_marks(double *out, int cap) {
-  const int n = (int)t_chunk_marks.size();
-  for (int i = 0; out && i < n && i < cap; ++i) out[i] = t_chunk_marks[i];
+  const std::vector<double> &m = t_clock.marks;
+  const int n = (int)m.size();
+  for (int i = 0; out && i < n && i < cap; ++i) out[i] = m[i];
   return n;
 }
 
@@ -1097,6 +1168,6 @@ double hsv_measure_mad_peak(void) {
   return hsv_launch_mad_peak(ctx(dev).cus);
 }
 
-int hsv_set_error(int code, const char *msg) { return fail(code, msg ? msg : ""); }
+int hsvi_set_error(int code, const char *msg) { return fail(code, msg ? msg : ""); }
 
 }  // extern "C"

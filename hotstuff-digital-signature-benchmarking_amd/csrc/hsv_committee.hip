@@ -254,10 +254,10 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
 #ifdef HSV_TIMING_STUB_RWAVE  // tools/qc_phase_probe.py only: wrong flags, the quad path's time alone
       rx = fe_small(0);
       ry = fe_from_words_masked(rw);
-      const uint32_t r_ok = 1u, small = 0u;
+      const uint32_t r_ok = 1u, small = 0u, nc = 0u;
 #else
-      uint32_t small;
-      const uint32_t r_ok = ge_decompress_row(rw, rx, ry, small, L);
+      uint32_t small, nc = 0;
+      const uint32_t r_ok = ge_decompress_row(rw, rx, ry, small, nc, L);
 #endif
       const uint32_t small_r = r_ok & small;
       if (L.k == 0u && row % kRRows == 0u) {
@@ -266,7 +266,7 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
           r_x[vr][l] = rx.v[l];
           r_y[vr][l] = ry.v[l];
         }
-        r_fl[vr] = r_ok | (small_r << 1);
+        r_fl[vr] = r_ok | (small_r << 1) | (nc << 2);  // bit 2: self-check (fl_to_fe)
       }
     }
 #else
@@ -384,7 +384,7 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
   uint32_t fb;
   if constexpr (kRowChecks) fb = a_ok & r_ok & (sane ^ 1u);
   else fb = fault_bit(a_ok, r_ok, q) ? 1u : 0u;
-  if (fb) fault[0] = 1u;  // device self-check (hsv_kernels.hip report_faults)
+  if (fb | ((rf >> 2) & 1u)) fault[0] = 1u;  // device self-check (hsv_kernels.hip report_faults)
   if (valid && g == 0u) flags_out[i0] = kvalid ? (uint8_t)f : (uint8_t)0;
 }
 
@@ -414,8 +414,11 @@ __global__ void __launch_bounds__(64) hsv_lanesplit_check_kernel(const uint32_t 
   fe x0, y0, x1, y1;
   uint32_t small1;
   const uint32_t ok0 = ge_decompress(aw, x0, y0);
-  const uint32_t ok1 = ge_decompress_row(aw, x1, y1, small1, L);
-  bad |= (ok0 == ok1 && (!ok0 || (fe_eq(x0, x1) && fe_eq(y0, y1) && y_is_small_order(y0) == small1))) ? 0u : 4u;
+  uint32_t nc1 = 0;
+  const uint32_t ok1 = ge_decompress_row(aw, x1, y1, small1, nc1, L);
+  bad |= (ok0 == ok1 && nc1 == 0u && (!ok0 || (fe_eq(x0, x1) && fe_eq(y0, y1) && y_is_small_order(y0) == small1)))
+             ? 0u
+             : 4u;
   // the odd row of a pair checks its own copy too
   if constexpr (kRows == 2) bad |= __shfl_xor(bad, 16);
   if (r < rows && (threadIdx.x & (16u * kRows - 1u)) == 0u) out[r] |= bad << kShift;
@@ -445,7 +448,7 @@ extern "C" hipError_t hsv_launch_comb16_build(uint32_t *table, uint32_t *tmp, hi
 
 // Test hook, not in hsv.h: runs hsv_lanesplit_check_kernel on the current
 // device over `rows` host inputs of 16 words; 0 or a hipError_t.
-extern "C" int hsv_test_lanesplit_check(const uint32_t *in, uint32_t rows, uint32_t *out) {
+extern "C" int hsvi_lanesplit_check(const uint32_t *in, uint32_t rows, uint32_t *out) {
   if (rows == 0) return 0;
   uint32_t *d_in = nullptr, *d_out = nullptr;
   hipError_t e = hipMalloc(&d_in, (size_t)rows * 64);
@@ -495,7 +498,7 @@ extern "C" hipError_t hsv_launch_comb_verify(const uint32_t *key_idx, const uint
                                              uint8_t *flags_out, uint32_t *fault, hipStream_t stream) {
   if (m == 0) return hipSuccess;
   if (!fault) return hipErrorInvalidValue;
-  const uint32_t inject = (uint32_t)hsv_test_inject_mode();
+  const uint32_t inject = (uint32_t)hsvi_inject_mode();
   if (m <= kCombQuadMax) {  // latency form: four lanes per vote, R decompressed by the R waves
     hipLaunchKernelGGL(hsv::hsv_comb_verify_quad_fused_kernel, dim3((m + hsv::kFusedVotes - 1) / hsv::kFusedVotes),
                        dim3(hsv::kFusedThreads), 0, stream, key_idx, sig, sig_stride, msg, msg_stride, m, pks, key_flags, nkeys,

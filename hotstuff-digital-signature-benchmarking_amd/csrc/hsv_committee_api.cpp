@@ -88,6 +88,7 @@ int committee_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t
   if (rc != HSV_OK) return rc;
   SlotLease lease(c);
   Slot &s = lease.slot();
+  call_mark(HSV_MARK_SLOT);
   for (size_t base = 0; base < m; base += kChunk) {
     const size_t k = std::min(kChunk, m - base);
     const size_t idx_off = 0;
@@ -106,6 +107,7 @@ int committee_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t
     // unwritten flags read as rejections; self-check words start at zero
     std::memset(h + flag_off, 0, k);
     std::memset(h + fault_off, 0, kFaultBytes);
+    call_mark(HSV_MARK_STAGED);
     void *hd = nullptr;
     uint8_t *dbuf = s.d_buf;
     static const size_t zc_max = [] {  // HSV_COMMITTEE_ZC_MAX: measurement switch
@@ -126,12 +128,15 @@ int committee_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t
     if (e == hipSuccess && !zero_copy)
       e = hipMemcpyAsync(h + flag_off, s.d_buf + flag_off, fault_off + kFaultBytes - flag_off, hipMemcpyDeviceToHost,
                          s.stream);
+    call_mark(HSV_MARK_LAUNCH);
     const hipError_t es = hipStreamSynchronize(s.stream);  // nothing of this call stays in flight
+    call_mark(HSV_MARK_SYNC);
     if (e != hipSuccess) return hip_fail("committee verify launch", e);
     if (es != hipSuccess) return hip_fail("hipStreamSynchronize", es);
     rc = check_faults(h + fault_off, "committee verify");
     if (rc != HSV_OK) return rc;
     std::memcpy(flags_out + base, h + flag_off, k);
+    call_mark(HSV_MARK_DONE);
   }
   return HSV_OK;
 }
@@ -236,7 +241,7 @@ int64_t hsv_committee_index(const hsv_committee *cm, const uint8_t pk[32]) {
 
 int hsv_committee_verify_device(const hsv_committee *cm, const uint32_t *d_key_idx, const uint8_t *d_sig,
                                 size_t sig_stride, const uint8_t *d_msg, size_t msg_stride, size_t m, uint8_t *d_flags,
-                                void *stream) {
+                                uint32_t *d_fault, void *stream) {
   if (m == 0) return HSV_OK;
   if (!cm || !d_key_idx || !d_sig || !d_msg || !d_flags) return fail(HSV_ERR_INVALID_ARG, "null argument");
   if (((reinterpret_cast<uintptr_t>(d_sig) | reinterpret_cast<uintptr_t>(d_msg) | sig_stride | msg_stride) & 15u) != 0)
@@ -254,17 +259,18 @@ int hsv_committee_verify_device(const hsv_committee *cm, const uint32_t *d_key_i
   if (guard.status() != hipSuccess) return hip_fail("hipSetDevice", guard.status());
   rc = ensure_btable(c);  // the B table is rebuilt if hsv_shutdown released it
   if (rc != HSV_OK) return rc;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   uint32_t *fault = nullptr;
-  rc = device_fault_words(c, &fault);
+  rc = call_fault_words(c, d_fault, s, &fault);
   if (rc != HSV_OK) return rc;
   const hipError_t e = hsv_launch_comb_verify(d_key_idx, d_sig, sig_stride, d_msg, msg_stride, (uint32_t)m, cm->dev.d_pks,
-                                              cm->dev.d_kflags, cm->dev.n, cm->dev.d_tabptr, c.d_btable, d_flags, fault,
-                                              reinterpret_cast<hipStream_t>(stream));
+                                              cm->dev.d_kflags, cm->dev.n, cm->dev.d_tabptr, c.d_btable, d_flags, fault, s);
   return e == hipSuccess ? HSV_OK : hip_fail("committee verify launch", e);
 }
 
 int hsv_committee_verify(hsv_committee *cm, const uint32_t *key_idx, const uint8_t *sig, const uint8_t *msg,
                          size_t msg_stride, size_t m, uint8_t *flags_out) {
+  CallScope call;
   if (m == 0) return HSV_OK;
   if (!cm || !key_idx || !sig || !msg || !flags_out) return fail(HSV_ERR_INVALID_ARG, "null argument");
   if (msg_stride != 0 && msg_stride != 32) return fail(HSV_ERR_INVALID_ARG, "msg_stride must be 0 or 32");
@@ -272,6 +278,7 @@ int hsv_committee_verify(hsv_committee *cm, const uint32_t *key_idx, const uint8
 }
 
 int hsv_committee_verify_batch_packed(hsv_committee *cm, const uint8_t digest[32], const uint8_t *votes, size_t m) {
+  CallScope call;
   if (m == 0) return 1;
   if (!cm || !digest || !votes) return fail(HSV_ERR_INVALID_ARG, "null argument");
   std::vector<uint32_t> idx(m);
@@ -354,6 +361,7 @@ struct AutoCommittee {
   std::condition_variable idle;
   std::atomic<int> enabled{-1};  // -1: read HSV_AUTO_COMMITTEE on first use
   std::atomic<uint64_t> builds{0};
+  std::atomic<uint64_t> faults{0};  // cached-path launches whose self-check failed
   ~AutoCommittee() {
     std::unique_lock<std::mutex> lk(mu);
     idle.wait(lk, [&] { return !building; });
@@ -523,6 +531,35 @@ std::shared_ptr<const AutoView> auto_lookup(const uint8_t *pk, size_t pk_stride,
   return nullptr;
 }
 
+// The cached path's self-check failed: its tables (or the memory under them)
+// are no longer trusted.  Drop the view the failing call used -- unless a
+// newer one was published meanwhile -- and relearn from scratch; the call
+// itself is answered by the generic kernels.  Counted (hsv_auto_committee_faults).
+void auto_invalidate(const std::shared_ptr<const AutoView> &bad) {
+  AutoCommittee &a = AC();
+  a.faults.fetch_add(1);
+  std::lock_guard<std::mutex> lk(a.mu);
+  if (std::atomic_load(&a.view) != bad) return;
+  std::atomic_store(&a.view, std::shared_ptr<const AutoView>());
+  a.seen.clear();
+  a.pending.clear();
+  a.pending_set.clear();
+  a.miss_streak = 0;
+  ++a.generation;
+}
+
+// Run a batch on the cached tables.  HSV_OK, 1 (take the generic path:
+// the self-check failed, the view is dropped), or another error.
+int auto_run(const std::shared_ptr<const AutoView> &v, const uint32_t *idx, const uint8_t *sig, const uint8_t *msg,
+             size_t msg_stride, size_t n, uint8_t *flags_out) {
+  const int rc = committee_run(v->dev, idx, sig, msg, msg_stride, n, flags_out);
+  if (rc == HSV_ERR_DEVICE_FAULT) {
+    auto_invalidate(v);
+    return 1;
+  }
+  return rc;
+}
+
 void auto_reset(bool enable) {
   AutoCommittee &a = AC();
   std::unique_lock<std::mutex> lk(a.mu);
@@ -550,8 +587,20 @@ int auto_committee_try(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg
   if (n > kCommitteeTryMax || !auto_enabled()) return 1;
   std::vector<uint32_t> idx(n);
   std::shared_ptr<const AutoView> v = auto_lookup(pk, 32, n, idx.data(), false);
+  call_mark(HSV_MARK_LOOKUP);
   if (!v || v->dev.device != home_device()) return 1;
-  return committee_run(v->dev, idx.data(), sig, msg, msg_stride, n, flags_out);
+  return auto_run(v, idx.data(), sig, msg, msg_stride, n, flags_out);
+}
+
+int auto_committee_corrupt_tables() {
+  std::shared_ptr<const AutoView> v = current_view();
+  if (!v || v->store->blocks.empty()) return 0;
+  DeviceGuard guard(v->dev.device);
+  for (uint32_t *b : v->store->blocks) {
+    const hipError_t e = hipMemset(b, 0, (size_t)kBlockKeys * hsv_comb_table_bytes());
+    if (e != hipSuccess) return hip_fail("hipMemset", e);
+  }
+  return (int)v->dev.n;
 }
 
 void auto_committee_shutdown() {
@@ -566,6 +615,7 @@ void auto_committee_shutdown() {
 extern "C" {
 
 int hsv_verify_batch_packed(const uint8_t digest[32], const uint8_t *votes, size_t n) {
+  CallScope call;
   if (n == 0) return 1;
   if (!digest || !votes) return fail(HSV_ERR_INVALID_ARG, "null argument");
   int rc = ensure_init();
@@ -574,12 +624,14 @@ int hsv_verify_batch_packed(const uint8_t digest[32], const uint8_t *votes, size
   if (n >= 2 && auto_enabled()) {
     std::vector<uint32_t> idx(n);
     std::shared_ptr<const AutoView> v = auto_lookup(votes, 96, n, idx.data(), true);
+    call_mark(HSV_MARK_LOOKUP);
     if (v) {
       std::vector<uint8_t> sigs(n * 64);
       for (size_t i = 0; i < n; ++i) std::memcpy(sigs.data() + 64 * i, votes + 96 * i + 32, 64);
-      rc = committee_run(v->dev, idx.data(), sigs.data(), digest, 0, n, flags.data());
+      rc = auto_run(v, idx.data(), sigs.data(), digest, 0, n, flags.data());
       if (rc == HSV_OK) return batch_verdict(flags.data(), n);
-      // an infrastructure error on the cached path: the generic path answers
+      // the self-check failed (the cache is dropped) or another infrastructure
+      // error on the cached path: the generic path answers
     }
   }
   rc = run_host(votes, 96, votes + 32, 96, digest, 0, n, flags.data());
@@ -595,6 +647,8 @@ size_t hsv_auto_committee_size(void) {
   std::shared_ptr<const AutoView> v = current_view();
   return v ? v->dev.n : 0;
 }
+
+uint64_t hsv_auto_committee_faults(void) { return AC().faults.load(); }
 
 int hsv_auto_committee_wait(int timeout_ms) {
   AutoCommittee &a = AC();

@@ -212,8 +212,12 @@ __device__ __forceinline__ uint32_t fl_from_fe(const fe &a, const RowLane &L) {
 }
 
 // this row's element (limbs <= 2^16.05) -> ten limbs (class R, value < 2^255,
-// possibly >= p) in every lane of the row
-__device__ __forceinline__ fe fl_to_fe(uint32_t x, const RowLane &L) {
+// possibly >= p) in every lane of the row.  nc |= 1 when the carry passes did
+// not converge (a lane still holds bits above its limb width after the cap):
+// the bounds model (tools/lanesplit_model.py) never needs more than 17
+// passes, so that is an out-of-model input -- the callers OR it into the
+// launch's self-check word, so it becomes HSV_ERR_DEVICE_FAULT, never a verdict.
+__device__ __forceinline__ fe fl_to_fe(uint32_t x, const RowLane &L, uint32_t &nc) {
   // exact limbs: 16 bits each, 15 for limb 15, whose carry (weight 2^255)
   // wraps to lane 0 times 19; repeated until no lane of the wave carries
   const uint32_t sh = L.k == 15u ? 15u : 16u;
@@ -226,6 +230,7 @@ __device__ __forceinline__ fe fl_to_fe(uint32_t x, const RowLane &L) {
     x = (x & mask) + row_ror1(__umul24(t, w19));
     if (!__ballot(t != 0u)) break;
   }
+  if (__ballot((x >> sh) != 0u)) nc = 1u;
   // words: lane 2j holds limbs 2j | 2j+1, then each word to every lane
   const uint32_t pair = x | (row_shl1(x) << 16);
   uint32_t w[8];
@@ -238,6 +243,11 @@ __device__ __forceinline__ fe fl_to_fe(uint32_t x, const RowLane &L) {
   w[6] = row_bcast<12>(pair);
   w[7] = row_bcast<14>(pair);
   return fe_from_words_masked(w);
+}
+
+__device__ __forceinline__ fe fl_to_fe(uint32_t x, const RowLane &L) {
+  uint32_t nc = 0;
+  return fl_to_fe(x, L, nc);
 }
 
 // ---- checks of a point held identically by every lane of a row ----
@@ -269,9 +279,10 @@ __device__ __forceinline__ uint32_t ge_eq_affine_row(const ge_ext &p, const fe &
 // independent operations on separate lanes of the row (one product, then one
 // comparison per lane).  Every lane of the row returns the same (x, y),
 // flag and small-order bit as ge_decompress and y_is_small_order.
+// nc |= 1: a carry normalisation did not converge (fl_to_fe).
 template <class Lane>
 __device__ __forceinline__ uint32_t ge_decompress_row(const uint32_t enc[8], fe &x, fe &y, uint32_t &small,
-                                                      const Lane &L) {
+                                                      uint32_t &nc, const Lane &L) {
   y = fe_from_words_masked(enc);
   uint32_t yl = row_limb_of_words(enc, L);
   if (L.k == 15u) yl &= 0x7fffu;  // bit 255 is the sign of x
@@ -282,8 +293,8 @@ __device__ __forceinline__ uint32_t ge_decompress_row(const uint32_t enc[8], fe 
   const uint32_t v3 = fl_mul(fl_sq(v, L), v, L);
   const uint32_t v7 = fl_mul(fl_sq(v3, L), v, L);
   const uint32_t rl = fl_mul(fl_mul(ul, v3, L), fl_pow22523(fl_mul(ul, v7, L), L), L);
-  const fe check = fl_to_fe(fl_mul(v, fl_sq(rl, L), L), L);
-  const fe u = fl_to_fe(ul, L), r = fl_to_fe(rl, L);
+  const fe check = fl_to_fe(fl_mul(v, fl_sq(rl, L), L), L, nc);
+  const fe u = fl_to_fe(ul, L, nc), r = fl_to_fe(rl, L, nc);
   // fe_sqrt_ratio_fix_chk: lane 0 -u sqrt(-1), lane 1 r sqrt(-1); then lane 0
   // check == u, lane 1 check == -u, lane 2 check == -u sqrt(-1)
   const fe neg_u = fe_neg(u);

@@ -30,6 +30,20 @@ int fail(int code, const std::string &msg);
 int hip_fail(const char *where, hipError_t e);
 const std::string &last_error();
 
+// ---- host timeline of a call (hsv_host_call_marks) ---------------------------
+// Every public entry point that verifies opens a CallScope; the path below it
+// stamps the HSV_MARK_* points it passes (ms from the entry), or, in a
+// pipelined call, four marks per chunk.
+class CallScope {
+ public:
+  CallScope();
+  ~CallScope();
+  CallScope(const CallScope &) = delete;
+  CallScope &operator=(const CallScope &) = delete;
+};
+void call_mark(int which);
+void call_chunk_mark();
+
 // ---- sizes -------------------------------------------------------------------
 constexpr size_t kAlign = 256;
 constexpr size_t kChunk = size_t(1) << 22;        // items per verification launch
@@ -58,7 +72,9 @@ struct DevCtx {
   std::mutex table_mu;             // guards the two B tables and d_fault below
   uint32_t *d_btable = nullptr;    // narrow comb of B (committee kernels)
   uint32_t *d_btable16 = nullptr;  // wide comb of B (generic kernels)
-  uint32_t *d_fault = nullptr;     // self-check words of the device-resident calls (hsv_device_faults)
+  uint32_t *d_fault = nullptr;     // self-check words of the device-resident calls (hsv_device_faults);
+                                   // words kFaultOutWord.. receive the read-and-clear exchange
+  std::mutex fault_mu;             // one read-and-clear of d_fault at a time
   std::vector<std::unique_ptr<Slot>> slots;
   std::atomic<unsigned> rr{0};
   std::mutex side_mu;                    // guards the side-stream pool
@@ -117,6 +133,10 @@ int check_faults(const uint8_t *words, const char *where);
 // The per-device words of the stream-ordered device API (current device
 // must be c.device); allocated and zeroed on first use.
 int device_fault_words(DevCtx &c, uint32_t **out);
+constexpr size_t kFaultOutWord = 4;  // d_fault[4..5]: output of hsv_launch_fault_exchange
+// The words a device-API call reports into: the caller's d_fault (zeroed on
+// `stream` here), or the per-device words when d_fault is NULL.
+int call_fault_words(DevCtx &c, uint32_t *d_fault, hipStream_t stream, uint32_t **out);
 
 // A side stream of device c for one call (current device must be c.device),
 // returned to the pool when the lease ends: concurrent device-API calls never
@@ -146,6 +166,9 @@ int pointer_device(const void *p);
 // pointers, checked against the stream's device.  Returns HSV_OK and sets
 // *dev, or an error.
 int device_for_call(const void *d_ptr, void *stream, int *dev);
+
+// ---- hooks shared with hsv_test_hooks.cpp (exported by libhsv_test.so only) ----
+int auto_committee_corrupt_tables();  // zero the cached tables of the automatic committee
 
 // ---- the automatic committee cache (hsv_committee_api.cpp) --------------------
 // Strict verification of small batches whose keys are all cached: HSV_OK

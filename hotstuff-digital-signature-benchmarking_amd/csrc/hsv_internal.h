@@ -20,10 +20,16 @@ extern "C" {
 hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream);
 void hsv_ws_trim(void);  // hsv_shutdown: release the pools' free blocks
 
+// Everything declared here is internal: the library is built with
+// -fvisibility=hidden, so none of it is exported from libhsv.so (only the
+// HSV_API functions of include/hsv.h are).  The test and measurement hooks of
+// csrc/hsv_test_hooks.h are exported by libhsv_test.so only; they call the
+// hsvi_* functions below.
+
 // Enqueue one verification launch on `stream` (no synchronisation).
-int hsv_num_variants(void);            // id space
-int hsv_variant_list(int *out, int cap);  // ids built into this library; returns their count
-int hsv_variant_available(int variant);
+int hsvi_num_variants(void);            // id space
+int hsvi_variant_list(int *out, int cap);  // ids built into this library; returns their count
+int hsvi_variant_available(int variant);
 // fault: two device-visible words the caller zeroed before the launch; the
 // kernels set fault[0] (an item's final point failed the self-check) and
 // fault[1] (a workspace canary changed) -- see hsv_kernels.hip report_faults.
@@ -41,8 +47,19 @@ hipError_t hsv_launch_verify_ws(int variant, const uint8_t *pk, uint64_t pk_stri
                                 uint8_t *flags_out, uint32_t *strict_bits, const uint32_t *comb_b, uint32_t *fault,
                                 void *ws, size_t ws_cap, hipStream_t stream);
 size_t hsv_launch_ws_bytes(int variant, uint32_t n);
-// fault injection mode of the next launches (tests only; hsv_kernels.hip)
-int hsv_test_inject_mode(void);
+// Fault injection (tests only; hsv_kernels.hip): the mode of the launches the
+// calling thread issues (thread-scoped, so one test's injection never reaches
+// another thread's calls); hsvi_set_inject returns the previous mode, or -1.
+int hsvi_inject_mode(void);
+int hsvi_set_inject(int mode);
+// Lattice bound of the comb-path prepass (tests; 0 = default); returns the
+// previous bound or -1.
+int hsvi_set_lattice_bits(int bits);
+// Row-form field arithmetic against the one-lane form (hsv_committee.hip).
+int hsvi_lanesplit_check(const uint32_t *in, uint32_t rows, uint32_t *out);
+// Read-and-clear of two device fault words in one atomic exchange each, on
+// `stream`: out (device memory, 2 words) receives the old values.
+hipError_t hsv_launch_fault_exchange(uint32_t *words, uint32_t *out, hipStream_t stream);
 // digit width of the B comb table a variant reads: 8 (hsv_comb_table_bytes),
 // 16 (the wide table, hsv_comb16_table_bytes) or 0 (none); comb_b must be
 // that table for such variants
@@ -109,7 +126,10 @@ hipError_t hsv_launch_tx_mask(const uint64_t *offsets, uint32_t n, uint8_t *flag
 extern "C" {
 #endif
 // sets hsv_last_error() on the calling thread; returns code
-int hsv_set_error(int code, const char *msg);
+int hsvi_set_error(int code, const char *msg);
+// test hooks of hsv_capi.cpp (exported as hsv_set_* by libhsv_test.so only)
+int hsvi_set_virtual_shards(int k);
+int hsvi_set_variant(int v);
 #ifdef __cplusplus
 }
 #endif

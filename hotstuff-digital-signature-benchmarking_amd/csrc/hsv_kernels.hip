@@ -751,7 +751,7 @@ hsv_verify_row_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const 
   const uint32_t li = item < n ? item : n - 1u;
   const uint32_t slot = blockIdx.x * (uint32_t)kRowRows + rb;
   canary[slot] = inject == kInjectCanary ? ~nonce : nonce;
-  uint32_t ok, small;
+  uint32_t ok, small, nc = 0;
   uint32_t *tab = stab + rb * (uint32_t)(kEnt * 64);
   {
     uint32_t enc[8];
@@ -760,7 +760,7 @@ hsv_verify_row_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const 
     enc[0] = e0.x; enc[1] = e0.y; enc[2] = e0.z; enc[3] = e0.w;
     enc[4] = e1.x; enc[5] = e1.y; enc[6] = e1.z; enc[7] = e1.w;
     fe x, y;
-    ok = ge_decompress_row(enc, x, y, small, L);
+    ok = ge_decompress_row(enc, x, y, small, nc, L);
     small &= ok;
     row_table_build<TS>(tab, x, y, L, inject, role == 0u);
   }
@@ -791,9 +791,9 @@ hsv_verify_row_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const 
     const uint32_t r_ok = role ? ok_o : ok, small_r = role ? small_o : small;
     const uint32_t a_ok = role ? ok : ok_o, small_a = role ? small : small_o;
     ge_ext qe;
-    qe.X = fl_to_fe(q.X, L);
-    qe.Y = fl_to_fe(q.Y, L);
-    qe.Z = fl_to_fe(q.Z, L);
+    qe.X = fl_to_fe(q.X, L, nc);
+    qe.Y = fl_to_fe(q.Y, L, nc);
+    qe.Z = fl_to_fe(q.Z, L, nc);
     qe.T = qe.Z;
     uint32_t z_nonzero;
     const uint32_t sane = ge_is_sane_row(qe, z_nonzero);
@@ -801,7 +801,7 @@ hsv_verify_row_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const 
     f = flags_byte(meta & kPrepSOk, a_ok, r_ok, small_a, small_r, same);
     bad = (a_ok & r_ok & (sane ^ 1u)) ? 1u : 0u;
   }
-  report_faults(fault, bad | (canary[slot] != nonce ? 2u : 0u));
+  report_faults(fault, bad | nc | (canary[slot] != nonce ? 2u : 0u));
   if (item < n && role == 0u && L.k == 0u && lead) {
     if (flags_out) flags_out[item] = (uint8_t)f;
     if (strict_bits && (f & kStrictOk)) atomicOr(&strict_bits[item >> 5], 1u << (item & 31u));
@@ -938,7 +938,7 @@ __global__ void __launch_bounds__(256) hsv_mad_peak_kernel(uint32_t *sink, uint3
 //      prepass, then two lanes per item (hsv_verify_pair_kernel)
 //  22: as 21 with a pair-lane tail in the large-batch point pass (hsv_verify_hpt_kernel)
 // id space of the variants (hsv_variant_list gives the ids built into this library)
-extern "C" int hsv_num_variants(void) { return 23; }
+extern "C" int hsvi_num_variants(void) { return 23; }
 
 namespace {
 struct WsPools {
@@ -1003,12 +1003,14 @@ extern "C" hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream) 
 
 namespace {
 
-// Lattice bound of the comb-path prepass (hsv_set_lattice_bits; tests lower it
-// to 133 so the lattice-fallback fixtures take the full-length path).
+// Lattice bound of the comb-path prepass (hsvi_set_lattice_bits; tests lower
+// it to 133 so the lattice-fallback fixtures take the full-length path).
 std::atomic<int> g_lat_bits{hsv::kLatCombBits};
 
-// Fault injection mode of the next launches (hsv_test_inject_fault; tests only).
-std::atomic<uint32_t> g_inject{hsv::kInjectNone};
+// Fault injection mode of the launches the calling thread issues
+// (hsvi_set_inject; only libhsv_test.so exports a setter).  Thread-scoped: a
+// test that injects on one thread leaves every other thread's calls alone.
+thread_local uint32_t t_inject = hsv::kInjectNone;
 
 // Per-launch canary nonce: odd, so never 0 (zeroed memory) or all-ones.
 uint32_t next_nonce() {
@@ -1181,7 +1183,7 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
     {
       hipLaunchKernelGGL((hsv::hsv_verify_hp_kernel<WA, WAVES, CB>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
                          pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, vt_ws, comb_b, rec,
-                         ctr, fb_list, canary, next_nonce(), g_inject.load(), fault);
+                         ctr, fb_list, canary, next_nonce(), t_inject, fault);
     }
     e = hipGetLastError();
   }
@@ -1225,7 +1227,7 @@ hipError_t launch_pair(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig
                        pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits,
                        static_cast<uint4 *>(ws), comb_b, g_lat_bits.load(),
                        reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(ws) + ws_bytes), next_nonce(),
-                       g_inject.load(), fault);
+                       t_inject, fault);
     e = hipGetLastError();
   }
   const hipError_t ef = own ? hipFreeAsync(ws, stream) : hipSuccess;
@@ -1280,7 +1282,7 @@ hipError_t launch_row(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig,
     hipLaunchKernelGGL(kern, dim3(grid), dim3(4 * 64), 0, stream, pk, pk_stride, sig, sig_stride, msg, msg_stride,
                        n, flags_out, strict_bits, static_cast<uint4 *>(ws), comb_b, g_lat_bits.load(),
                        reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(ws) + ws_bytes), next_nonce(),
-                       g_inject.load(), fault);
+                       t_inject, fault);
     e = hipGetLastError();
   }
   const hipError_t ef = own ? hipFreeAsync(ws, stream) : hipSuccess;
@@ -1417,13 +1419,13 @@ static const int kVariantIds[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 
 static const int kVariantIds[] = {19, 21};
 #endif
 
-extern "C" int hsv_variant_list(int *out, int cap) {
+extern "C" int hsvi_variant_list(int *out, int cap) {
   const int n = (int)(sizeof(kVariantIds) / sizeof(kVariantIds[0]));
   for (int i = 0; out && i < n && i < cap; ++i) out[i] = kVariantIds[i];
   return n;
 }
 
-extern "C" int hsv_variant_available(int variant) {
+extern "C" int hsvi_variant_available(int variant) {
   for (int v : kVariantIds)
     if (v == variant) return 1;
   return 0;
@@ -1453,23 +1455,36 @@ extern "C" double hsv_launch_mad_peak(int device_cus) {
   return ms > 0.f ? macs / (ms * 1e-3) : -1.0;
 }
 
-// Test hook (not in hsv.h): the lattice bound of the comb-path prepass.
-// 0 restores the default (kLatCombBits); otherwise 128..kLatCombBits.
-// Returns the previous bound, or -1 for an out-of-range value.
-extern "C" int hsv_set_lattice_bits(int bits) {
+// The lattice bound of the comb-path prepass (tests): 0 restores the default
+// (kLatCombBits); otherwise 128..kLatCombBits.  Returns the previous bound, or
+// -1 for an out-of-range value.
+extern "C" int hsvi_set_lattice_bits(int bits) {
   if (bits == 0) bits = hsv::kLatCombBits;
   if (bits < 128 || bits > hsv::kLatCombBits) return -1;
   return g_lat_bits.exchange(bits);
 }
 
-// Test hook (not in hsv.h): fault injection mode of the following launches
-// (kInject*: 1 zeroed tables, 2 overwritten canary, 3 flipped table bits;
-// 0 = off).  Returns the previous mode, or -1 for an unknown one.
-extern "C" int hsv_test_inject_fault(int mode) {
+// Fault injection mode of the calling thread's following launches (kInject*:
+// 1 zeroed tables, 2 overwritten canary, 3 flipped table bits; 0 = off).
+// Returns the previous mode, or -1 for an unknown one.
+extern "C" int hsvi_set_inject(int mode) {
   if (mode < 0 || mode > (int)hsv::kInjectFlipTables) return -1;
-  return (int)g_inject.exchange((uint32_t)mode);
+  const int prev = (int)t_inject;
+  t_inject = (uint32_t)mode;
+  return prev;
 }
-extern "C" int hsv_test_inject_mode(void) { return (int)g_inject.load(); }
+extern "C" int hsvi_inject_mode(void) { return (int)t_inject; }
+
+namespace {
+__global__ void hsv_fault_exchange_kernel(uint32_t *words, uint32_t *out) {
+  if (threadIdx.x < 2) out[threadIdx.x] = atomicExch(&words[threadIdx.x], 0u);
+}
+}  // namespace
+
+extern "C" hipError_t hsv_launch_fault_exchange(uint32_t *words, uint32_t *out, hipStream_t stream) {
+  hipLaunchKernelGGL(hsv_fault_exchange_kernel, dim3(1), dim3(64), 0, stream, words, out);
+  return hipGetLastError();
+}
 
 extern "C" int hsv_variant_needs_comb(int variant) {
   if (variant >= 10 && variant <= 14) return 8;
@@ -1478,7 +1493,7 @@ extern "C" int hsv_variant_needs_comb(int variant) {
 }
 
 #ifdef HSV_PHASE_CLOCKS
-extern "C" int hsv_phase_clocks_read(uint64_t *dst, size_t words, int clear) {
+extern "C" __attribute__((visibility("default"))) int hsv_phase_clocks_read(uint64_t *dst, size_t words, int clear) {
   const size_t nw = std::min<size_t>(words, (size_t)hsv::kPhaseCap * 8);
   if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(hsv::g_phase_clk), nw * sizeof(uint64_t)) != hipSuccess) return -1;
   if (clear) {

@@ -1,0 +1,24 @@
+// The exported test and measurement hooks of libhsv_test.so (declared in
+// csrc/hsv_test_hooks.h).  Each forwards to an internal, hidden function of
+// the shared objects; libhsv.so is linked without this file.
+#include "hsv_test_hooks.h"
+
+#include "hsv_host.h"
+#include "hsv_internal.h"
+
+extern "C" {
+
+int hsv_test_inject_fault(int mode) { return hsvi_set_inject(mode); }
+int hsv_test_inject_mode(void) { return hsvi_inject_mode(); }
+int hsv_test_corrupt_auto_committee(void) { return hsvh::auto_committee_corrupt_tables(); }
+int hsv_test_lanesplit_check(const uint32_t *in, uint32_t rows, uint32_t *out) {
+  return hsvi_lanesplit_check(in, rows, out);
+}
+int hsv_set_lattice_bits(int bits) { return hsvi_set_lattice_bits(bits); }
+int hsv_set_variant(int variant) { return hsvi_set_variant(variant); }
+int hsv_variant_list(int *out, int cap) { return hsvi_variant_list(out, cap); }
+int hsv_variant_available(int variant) { return hsvi_variant_available(variant); }
+int hsv_num_variants(void) { return hsvi_num_variants(); }
+int hsv_set_virtual_shards(int k) { return hsvi_set_virtual_shards(k); }
+
+}  // extern "C"

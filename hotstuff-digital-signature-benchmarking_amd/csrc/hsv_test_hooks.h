@@ -1,0 +1,48 @@
+/*
+ * hsv_test_hooks.h -- test and measurement hooks of libhsv_test.so.
+ *
+ * libhsv_test.so is libhsv.so's object files plus csrc/hsv_test_hooks.cpp:
+ * the same kernels and host code, and in addition the hooks below.  The
+ * product library exports none of them (tests/test_capi.py checks its
+ * dynamic symbols against include/hsv.h), so no stray call can change the
+ * behaviour of a deployed process.  tests/ and tools/ load libhsv_test.so
+ * for the cases that need a hook (hsverify/_testing.py).
+ */
+#ifndef HSV_TEST_HOOKS_H_
+#define HSV_TEST_HOOKS_H_
+
+#include "hsv.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Fault injection for the launches the CALLING THREAD issues from now on
+ * (csrc/hsv_verify_core.hpp kInject*: 1 zeroed tables, 2 overwritten
+ * workspace canary, 3 one flipped table bit; 0 = off).  Other threads' calls
+ * are unaffected.  Returns the previous mode, or -1 for an unknown one. */
+HSV_API int hsv_test_inject_fault(int mode);
+HSV_API int hsv_test_inject_mode(void);
+/* Zero the tables of the automatic committee cache in HBM (a real
+ * corruption, for the cached path's self-check); returns the number of
+ * cached keys, 0 when there is no cache, < 0 on error. */
+HSV_API int hsv_test_corrupt_auto_committee(void);
+/* Row-form field arithmetic against the one-lane form (tests/test_lanesplit.py). */
+HSV_API int hsv_test_lanesplit_check(const uint32_t *in, uint32_t rows, uint32_t *out);
+/* Lattice bound of the comb-path prepass (0 = default 138; 133 sends the
+ * lattice-fallback fixtures down the full-length path); previous bound or -1. */
+HSV_API int hsv_set_lattice_bits(int bits);
+/* Kernel variant of the following calls (the ids hsv_variant_list reports). */
+HSV_API int hsv_set_variant(int variant);
+HSV_API int hsv_variant_list(int *out, int cap);
+HSV_API int hsv_variant_available(int variant);
+HSV_API int hsv_num_variants(void);
+/* Split host batches of >= 2^16 items into k shards on the bound device
+ * (the multi-device gather path on a one-GPU box); 0 restores the default. */
+HSV_API int hsv_set_virtual_shards(int k);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HSV_TEST_HOOKS_H_ */

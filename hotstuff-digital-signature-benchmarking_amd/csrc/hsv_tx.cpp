@@ -152,16 +152,18 @@ using namespace hsvh;
 extern "C" {
 
 int hsv_verify_transactions(const uint8_t *txs, const uint64_t *offsets, size_t n, uint8_t *flags_out) {
+  CallScope call;
   if (n && !offsets) return fail(HSV_ERR_INVALID_ARG, "null offsets");
   return run_tx_host(txs, offsets, 0, n, flags_out);
 }
 
 int hsv_verify_transactions_fixed(const uint8_t *txs, size_t tx_size, size_t n, uint8_t *flags_out) {
+  CallScope call;
   return run_tx_host(txs, nullptr, tx_size, n, flags_out);
 }
 
 int hsv_verify_transactions_device(const uint8_t *d_txs, const uint64_t *d_offsets, size_t tx_size, size_t n,
-                                   uint8_t *d_flags, uint32_t *d_strict_bits, void *stream) {
+                                   uint8_t *d_flags, uint32_t *d_strict_bits, uint32_t *d_fault, void *stream) {
   if (n == 0) return HSV_OK;
   if (!d_txs) return fail(HSV_ERR_INVALID_ARG, "null d_txs");
   if (!d_flags && !d_strict_bits) return fail(HSV_ERR_INVALID_ARG, "no output");
@@ -177,10 +179,10 @@ int hsv_verify_transactions_device(const uint8_t *d_txs, const uint64_t *d_offse
   const uint32_t *comb_b = nullptr;
   rc = comb_table_for(ctx(dev), v, &comb_b);
   if (rc != HSV_OK) return rc;
-  uint32_t *fault = nullptr;
-  rc = device_fault_words(ctx(dev), &fault);
-  if (rc != HSV_OK) return rc;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  uint32_t *fault = nullptr;
+  rc = call_fault_words(ctx(dev), d_fault, s, &fault);
+  if (rc != HSV_OK) return rc;
   const size_t per = std::min(n, kChunk);
   void *rec = nullptr;
   hipError_t e = hsv_ws_malloc(reinterpret_cast<void **>(&rec), per * 128, s);

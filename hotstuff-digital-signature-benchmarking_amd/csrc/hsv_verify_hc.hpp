@@ -227,7 +227,7 @@ constexpr int kPrepWords = 19;  // d(c1)[5] | d(|c0|)[5] | b[8] | meta
 enum : uint32_t { kPrepSOk = 1u, kPrepC0Neg = 2u, kPrepFallback = 4u };
 
 // lat_bits: the lattice bound (kLatCombBits; lower values only to exercise the
-// full-length path in tests, hsv_set_lattice_bits).
+// full-length path in tests, hsvi_set_lattice_bits).
 template <int WA>
 HSV_INL bool prep_scalars(const uint32_t pk[8], const uint32_t sig[16], const uint32_t msg[8], uint32_t *rec,
                           uint64_t stride, int lat_bits = kLatCombBits) {

@@ -18,19 +18,21 @@
 #include <vector>
 
 #include "hsv.h"
+#include "hsv_host.h"
 #include "hsv_internal.h"
 #include "hsv_wire_parse.h"
 
 namespace {
 
-int parse_error(const std::string &what) { return hsv_set_error(HSV_ERR_PARSE, ("bincode: " + what).c_str()); }
+int parse_error(const std::string &what) { return hsvi_set_error(HSV_ERR_PARSE, ("bincode: " + what).c_str()); }
 
 }  // namespace
 
 extern "C" {
 
 int hsv_qc_verify_bincode(const uint8_t *buf, size_t len, size_t *n_votes_out, uint8_t *pks_out) {
-  if (!buf && len) return hsv_set_error(HSV_ERR_INVALID_ARG, "null buffer");
+  hsvh::CallScope call;  // the host timeline includes the parse
+  if (!buf && len) return hsvi_set_error(HSV_ERR_INVALID_ARG, "null buffer");
   hsvw::QcParsed qc;
   std::string err;
   if (!hsvw::parse_qc(buf, len, qc, err)) return parse_error(err);
@@ -41,7 +43,8 @@ int hsv_qc_verify_bincode(const uint8_t *buf, size_t len, size_t *n_votes_out, u
 }
 
 int hsv_tc_verify_bincode(const uint8_t *buf, size_t len, size_t *n_votes_out, uint8_t *flags_out) {
-  if (!buf && len) return hsv_set_error(HSV_ERR_INVALID_ARG, "null buffer");
+  hsvh::CallScope call;
+  if (!buf && len) return hsvi_set_error(HSV_ERR_INVALID_ARG, "null buffer");
   hsvw::TcParsed tc;
   std::string err;
   if (!hsvw::parse_tc(buf, len, tc, err)) return parse_error(err);

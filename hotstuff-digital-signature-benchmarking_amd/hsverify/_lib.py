@@ -20,6 +20,13 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # HSV_LIB=libhsv_all.so selects the measurement build with every kernel
 # variant (make ALL_VARIANTS=1); it must live in this directory as well.
 LIB_PATH = os.path.join(_HERE, os.path.basename(os.environ.get("HSV_LIB", "libhsv.so")))
+# The same objects plus the exported test hooks (csrc/hsv_test_hooks.h);
+# loaded only by tests and tools through hsverify._testing.
+TEST_LIB_PATH = os.path.join(_HERE, "libhsv_test.so")
+# Exported by libhsv_test.so / libhsv_all.so only, never by libhsv.so.
+HOOKS = ("hsv_test_inject_fault", "hsv_test_inject_mode", "hsv_test_corrupt_auto_committee",
+         "hsv_test_lanesplit_check", "hsv_set_lattice_bits", "hsv_set_variant", "hsv_variant_list",
+         "hsv_variant_available", "hsv_num_variants", "hsv_set_virtual_shards")
 
 # flag bits (include/hsv.h)
 STRICT_OK = 0x01
@@ -49,7 +56,9 @@ class HsvLibraryError(RuntimeError):
 
 
 _lock = threading.Lock()
-_lib = None
+_lib = None        # the library every hsverify call uses (LIB_PATH)
+_test_lib = None   # libhsv_test.so, a second instance, loaded on demand
+_override = None   # hsverify._testing.test_library(): calls go to _test_lib
 
 
 def _declare(lib):
@@ -60,6 +69,7 @@ def _declare(lib):
         "hsv_bound_device": (ctypes.c_int, []),
         "hsv_set_virtual_shards": (ctypes.c_int, [ctypes.c_int]),
         "hsv_auto_committee_wait": (ctypes.c_int, [ctypes.c_int]),
+        "hsv_auto_committee_faults": (ctypes.c_uint64, []),
         "hsv_variant_list": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
         "hsv_variant_available": (ctypes.c_int, [ctypes.c_int]),
         "hsv_shutdown": (None, []),
@@ -72,10 +82,11 @@ def _declare(lib):
         "hsv_verify_batch_packed": (ctypes.c_int, [c_u8p, c_u8p, sz]),
         "hsv_verify_device": (ctypes.c_int, [c_u8p, sz, c_u8p, sz, c_u8p, sz, sz, c_u8p, ctypes.c_void_p]),
         "hsv_verify_device_bits": (ctypes.c_int, [c_u8p, sz, c_u8p, sz, c_u8p, sz, sz, c_u8p, c_u8p,
-                                                  ctypes.c_void_p]),
+                                                  ctypes.c_void_p, ctypes.c_void_p]),
         "hsv_verify_transactions": (ctypes.c_int, [c_u8p, c_u8p, sz, c_u8p]),
         "hsv_verify_transactions_fixed": (ctypes.c_int, [c_u8p, sz, sz, c_u8p]),
-        "hsv_verify_transactions_device": (ctypes.c_int, [c_u8p, c_u8p, sz, sz, c_u8p, c_u8p, ctypes.c_void_p]),
+        "hsv_verify_transactions_device": (ctypes.c_int, [c_u8p, c_u8p, sz, sz, c_u8p, c_u8p, ctypes.c_void_p,
+                                                          ctypes.c_void_p]),
         "hsv_qc_verify_bincode": (ctypes.c_int, [c_u8p, sz, ctypes.POINTER(ctypes.c_size_t), c_u8p]),
         "hsv_tc_verify_bincode": (ctypes.c_int, [c_u8p, sz, ctypes.POINTER(ctypes.c_size_t), c_u8p]),
         "hsv_set_auto_committee": (ctypes.c_int, [ctypes.c_int]),
@@ -91,20 +102,24 @@ def _declare(lib):
         "hsv_committee_verify": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u8p, c_u8p, sz, sz, c_u8p]),
         "hsv_committee_verify_batch_packed": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u8p, sz]),
         "hsv_committee_verify_device": (ctypes.c_int, [ctypes.c_void_p, c_u8p, c_u8p, sz, c_u8p, sz, sz, c_u8p,
-                                                       ctypes.c_void_p]),
+                                                       ctypes.c_void_p, ctypes.c_void_p]),
         "hsv_set_variant": (ctypes.c_int, [ctypes.c_int]),
         "hsv_get_variant": (ctypes.c_int, []),
         "hsv_set_lattice_bits": (ctypes.c_int, [ctypes.c_int]),
         "hsv_num_variants": (ctypes.c_int, []),
         "hsv_device_faults": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
         "hsv_test_inject_fault": (ctypes.c_int, [ctypes.c_int]),
+        "hsv_test_inject_mode": (ctypes.c_int, []),
+        "hsv_test_corrupt_auto_committee": (ctypes.c_int, []),
+        "hsv_test_lanesplit_check": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
         "hsv_host_call_stats": (None, [ctypes.POINTER(ctypes.c_double)] * 3),
+        "hsv_host_call_marks": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
         "hsv_pack_threads": (ctypes.c_int, []),
         "hsv_sign_mixed_order": (ctypes.c_int, [c_u8p, c_u8p, sz, ctypes.c_int, ctypes.c_int, c_u8p, c_u8p]),
     }
-    # test / measurement hooks absent from older A/B builds (tools/ab_probe.py)
-    optional = {"hsv_set_lattice_bits", "hsv_test_inject_fault", "hsv_host_call_stats", "hsv_pack_threads",
-                "hsv_device_faults", "hsv_sign_mixed_order"}
+    # hooks (libhsv_test.so only) and entry points absent from older A/B builds (tools/ab_probe.py)
+    optional = set(HOOKS) | {"hsv_host_call_stats", "hsv_host_call_marks", "hsv_pack_threads", "hsv_device_faults",
+                             "hsv_sign_mixed_order", "hsv_auto_committee_faults"}
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None) if name in optional else getattr(lib, name)
         if fn is None:
@@ -113,27 +128,69 @@ def _declare(lib):
         fn.argtypes = args
 
 
+def _open(path, require):
+    if not os.path.exists(path):
+        if require:
+            raise HsvLibraryError(
+                f"{path} not built: run `make` in {os.path.dirname(_HERE)} "
+                "or __graft_entry__.build(); there is no CPU fallback")
+        return None
+    if os.environ.get("HSV_NO_TORCH") != "1":
+        try:
+            import torch  # noqa: F401  (share torch's HIP runtime)
+        except Exception:  # pragma: no cover - torch absent is fine
+            pass
+    # RTLD_LOCAL: libhsv.so and libhsv_test.so export the same names and may
+    # both be loaded (two independent instances); neither may bind the other's.
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+    _declare(lib)
+    return lib
+
+
 def load(require: bool = True):
-    """Return the loaded CDLL (cached).  Raises HsvLibraryError if absent."""
+    """Return the library hsverify calls go to (cached): LIB_PATH, or
+    libhsv_test.so inside hsverify._testing.test_library().  Raises
+    HsvLibraryError if absent."""
     global _lib
     with _lock:
-        if _lib is not None:
-            return _lib
-        if not os.path.exists(LIB_PATH):
-            if require:
-                raise HsvLibraryError(
-                    f"{LIB_PATH} not built: run `make` in {os.path.dirname(_HERE)} "
-                    "or __graft_entry__.build(); there is no CPU fallback")
-            return None
-        if os.environ.get("HSV_NO_TORCH") != "1":
-            try:
-                import torch  # noqa: F401  (share torch's HIP runtime)
-            except Exception:  # pragma: no cover - torch absent is fine
-                pass
-        lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
-        _declare(lib)
-        _lib = lib
-        return lib
+        if _override is not None:
+            return _override
+        if _lib is None:
+            _lib = _open(LIB_PATH, require)
+        return _lib
+
+
+def load_test():
+    """libhsv_test.so: the product's objects plus the exported test hooks.  If
+    the library already loaded exports them (HSV_LIB=libhsv_test.so or
+    libhsv_all.so), that instance is returned instead of a second one."""
+    global _test_lib
+    main = load()
+    if getattr(main, "hsv_test_inject_fault", None) is not None:
+        return main
+    with _lock:
+        if _test_lib is None:
+            _test_lib = _open(TEST_LIB_PATH, True)
+        return _test_lib
+
+
+def set_override(lib):
+    """Route every hsverify call to `lib` (None: back to LIB_PATH); returns the
+    previous override.  Used by hsverify._testing.test_library()."""
+    global _override
+    with _lock:
+        prev, _override = _override, lib
+        return prev
+
+
+def hook(name: str):
+    """A test / measurement hook of the library in use; raises when it is the
+    product library, which exports none (csrc/hsv_test_hooks.h)."""
+    fn = getattr(load(), name, None)
+    if fn is None:
+        raise HsvLibraryError(f"{name} is a test hook: libhsv.so does not export it; run inside "
+                              "hsverify._testing.test_library() (libhsv_test.so)")
+    return fn
 
 
 def check(rc: int, what: str) -> int:

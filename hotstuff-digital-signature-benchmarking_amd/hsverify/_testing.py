@@ -1,7 +1,12 @@
-"""Test and measurement hooks of libhsv.so (not part of include/hsv.h).
+"""Test and measurement hooks (csrc/hsv_test_hooks.h), exported by
+libhsv_test.so only -- the product libhsv.so exports exactly include/hsv.h.
 
-Kept out of the public modules: each changes process-wide behaviour of the
-library for every thread, so only tests, bench.py and tools/ use them.
+libhsv_test.so is a second, independent instance of the library (same
+objects plus the hooks).  ``test_library()`` routes every hsverify call made
+inside it to that instance, so a test injects faults into, or changes the
+variant of, the very library its calls run on -- and nothing it does reaches
+the product instance other tests use.  The hook functions below require it
+(they enter it themselves where that is unambiguous).
 """
 from __future__ import annotations
 
@@ -17,20 +22,31 @@ INJECT_CANARY = 2        # a lane's workspace canary is overwritten mid-batch
 INJECT_FLIP_TABLES = 3   # one bit of table entries flipped
 
 
+@contextlib.contextmanager
+def test_library():
+    """Route hsverify calls to libhsv_test.so for the duration (re-entrant)."""
+    lib = _lib.load_test()
+    prev = _lib.set_override(lib)
+    try:
+        yield lib
+    finally:
+        _lib.set_override(prev)
+
+
 def set_lattice_bits(bits: int) -> int:
     """The lattice bound of the comb-path prepass (0 = default, 138; 133 sends
     the tests/golden/lattice_fallback.bin challenges down the full-length
     path).  Returns the previous bound."""
-    prev = _lib.load().hsv_set_lattice_bits(bits)
+    prev = _lib.hook("hsv_set_lattice_bits")(bits)
     if prev < 0:
         raise ValueError(f"lattice bound out of range: {bits}")
     return prev
 
 
 def inject_fault(mode: int) -> int:
-    """Corrupt what the following launches read back (INJECT_*; 0 = off).
-    Returns the previous mode."""
-    prev = _lib.load().hsv_test_inject_fault(mode)
+    """Corrupt what the calling thread's following launches read back
+    (INJECT_*; 0 = off; other threads are unaffected).  Returns the previous mode."""
+    prev = _lib.hook("hsv_test_inject_fault")(mode)
     if prev < 0:
         raise ValueError(f"unknown fault injection mode {mode}")
     return prev
@@ -38,11 +54,19 @@ def inject_fault(mode: int) -> int:
 
 @contextlib.contextmanager
 def injected_fault(mode: int):
-    prev = inject_fault(mode)
-    try:
-        yield
-    finally:
-        inject_fault(prev)
+    """test_library() with `mode` injected into this thread's launches."""
+    with test_library():
+        prev = inject_fault(mode)
+        try:
+            yield
+        finally:
+            inject_fault(prev)
+
+
+def corrupt_auto_committee() -> int:
+    """Zero the automatic committee cache's tables in HBM (test library);
+    returns the number of cached keys."""
+    return _lib.check(_lib.hook("hsv_test_corrupt_auto_committee")(), "hsv_test_corrupt_auto_committee")
 
 
 def host_call_stats() -> dict:
@@ -54,9 +78,9 @@ def host_call_stats() -> dict:
 
 
 def host_call_marks() -> list:
-    """Per-chunk host marks of the calling thread's last pipelined call, ms
-    from its start: staging buffer free, packed, copy enqueued, launch
-    enqueued (4 per chunk; empty for calls below the pipeline's size)."""
+    """Host timeline of the calling thread's last call, ms from its entry
+    (hsv_host_call_marks): HSV_MARK_* points for a latency call (see
+    latency_marks), four per chunk for a pipelined call."""
     buf = (ctypes.c_double * 256)()
     n = _lib.load().hsv_host_call_marks(buf, 256)
     return [round(buf[i], 4) for i in range(max(0, n))]
@@ -76,9 +100,8 @@ def lanesplit_check(words):
     import numpy as np
     w = np.ascontiguousarray(words, dtype=np.uint32)
     out = np.zeros(len(w), np.uint32)
-    lib = _lib.load()
-    rc = lib.hsv_test_lanesplit_check(ctypes.c_void_p(w.ctypes.data), ctypes.c_uint32(len(w)),
-                                      ctypes.c_void_p(out.ctypes.data))
+    rc = _lib.hook("hsv_test_lanesplit_check")(ctypes.c_void_p(w.ctypes.data), ctypes.c_uint32(len(w)),
+                                               ctypes.c_void_p(out.ctypes.data))
     if rc != 0:
         raise RuntimeError(f"hsv_test_lanesplit_check failed: hipError {rc}")
     return out

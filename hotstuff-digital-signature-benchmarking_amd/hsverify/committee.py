@@ -63,8 +63,10 @@ class Committee:
             "hsv_committee_verify_batch_packed")
         return OK if rc == 1 else Result(CryptoError("signature error"))
 
-    def verify_device(self, key_idx, sig, msg, flags, stream=None) -> None:
-        """Device tensors: key_idx (m,) int32, sig (m,64) u8, msg (m,32) or (32,), flags (m,) u8."""
+    def verify_device(self, key_idx, sig, msg, flags, stream=None, fault=None) -> None:
+        """Device tensors: key_idx (m,) int32, sig (m,64) u8, msg (m,32) or (32,), flags (m,) u8;
+        fault: optional per-call fault words (verifier.verify_device)."""
+        from .verifier import _fault_ptr
         import torch
         m = key_idx.shape[0]
         if stream is None:
@@ -72,7 +74,7 @@ class Committee:
         rc = self._lib.hsv_committee_verify_device(
             self._h, ctypes.c_void_p(key_idx.data_ptr()), ctypes.c_void_p(sig.data_ptr()), sig.stride(0),
             ctypes.c_void_p(msg.data_ptr()), 0 if msg.dim() == 1 else msg.stride(0), m,
-            ctypes.c_void_p(flags.data_ptr()), ctypes.c_void_p(stream))
+            ctypes.c_void_p(flags.data_ptr()), _fault_ptr(fault), ctypes.c_void_p(stream))
         _lib.check(rc, "hsv_committee_verify_device")
 
     def close(self) -> None:

@@ -78,11 +78,13 @@ def verify_transactions_fixed(txs: np.ndarray) -> np.ndarray:
 
 
 def verify_transactions_device(txs, offsets=None, tx_size: int = 0, n: int | None = None, flags=None,
-                               strict_bits=None, stream=None) -> None:
+                               strict_bits=None, stream=None, fault=None) -> None:
     """Enqueue verification of device-resident transactions (torch uint8 tensor
     ``txs``; ``offsets`` an int64 tensor of n+1 byte offsets, or None with
     ``tx_size`` for fixed-size transactions).  Outputs: ``flags`` (n,) uint8
-    and/or ``strict_bits`` (ceil(n/32),) int32.  No synchronisation."""
+    and/or ``strict_bits`` (ceil(n/32),) int32; ``fault`` optional per-call
+    fault words (verifier.verify_device).  No synchronisation."""
+    from .verifier import _fault_ptr
     import torch
 
     if n is None:
@@ -93,7 +95,8 @@ def verify_transactions_device(txs, offsets=None, tx_size: int = 0, n: int | Non
     rc = lib.hsv_verify_transactions_device(
         ctypes.c_void_p(txs.data_ptr()), ctypes.c_void_p(offsets.data_ptr()) if offsets is not None else None,
         tx_size, n, ctypes.c_void_p(flags.data_ptr()) if flags is not None else None,
-        ctypes.c_void_p(strict_bits.data_ptr()) if strict_bits is not None else None, ctypes.c_void_p(stream))
+        ctypes.c_void_p(strict_bits.data_ptr()) if strict_bits is not None else None, _fault_ptr(fault),
+        ctypes.c_void_p(stream))
     _lib.check(rc, "hsv_verify_transactions_device")
 
 

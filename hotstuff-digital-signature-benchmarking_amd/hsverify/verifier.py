@@ -44,17 +44,21 @@ def verify_flags(pk: np.ndarray, sig: np.ndarray, msg: np.ndarray) -> np.ndarray
     return out
 
 
-def verify_device(pk, sig, msg, flags=None, strict_bits=None, stream=None) -> None:
+def verify_device(pk, sig, msg, flags=None, strict_bits=None, stream=None, fault=None) -> None:
     """Enqueue verification of device tensors (uint8, contiguous rows).
 
     pk: (n,32), sig: (n,64), msg: (n,32) or (32,) shared; flags: (n,) uint8
     and/or strict_bits: (ceil(n/32),) int32 outputs.  ``stream`` is a raw
-    hipStream_t handle (int) -- default: torch's current stream.
+    hipStream_t handle (int) -- default: torch's current stream.  ``fault``
+    (optional): an int32 device tensor of >= 2 words owned by this call; the
+    library zeroes it on the stream and the kernels set it on a self-check
+    failure (read it with :func:`fault_bits` after synchronising).  Without
+    it the launches report into the per-device word (:func:`device_faults`).
     """
     import torch
 
     n = pk.shape[0]
-    for t in (sig, msg, flags, strict_bits):
+    for t in (sig, msg, flags, strict_bits, fault):
         if t is not None and t.device != pk.device:
             raise ValueError(f"all tensors must live on {pk.device}, got {t.device}")
     with torch.cuda.device(pk.device):  # the library launches on the inputs' device
@@ -67,8 +71,23 @@ def verify_device(pk, sig, msg, flags=None, strict_bits=None, stream=None) -> No
             ctypes.c_void_p(msg.data_ptr()), msg_stride, n,
             ctypes.c_void_p(flags.data_ptr()) if flags is not None else None,
             ctypes.c_void_p(strict_bits.data_ptr()) if strict_bits is not None else None,
-            ctypes.c_void_p(stream))
+            _fault_ptr(fault), ctypes.c_void_p(stream))
     _lib.check(rc, "hsv_verify_device_bits")
+
+
+def _fault_ptr(fault):
+    if fault is None:
+        return None
+    if fault.numel() * fault.element_size() < 8:
+        raise ValueError("a fault tensor needs two 32-bit words")
+    return ctypes.c_void_p(fault.data_ptr())
+
+
+def fault_bits(fault) -> int:
+    """Bits of a call's own fault words (after synchronising its stream):
+    1 = a final point failed the curve check, 2 = a workspace canary changed."""
+    w = fault.view(-1)[:2].cpu().tolist()
+    return (1 if w[0] else 0) | (2 if w[1] else 0)
 
 
 def device_faults(device: int = -1, clear: bool = True) -> int:
@@ -107,7 +126,8 @@ def measure_mad_peak() -> float:
 
 
 def set_variant(v: int) -> None:
-    _lib.check(_lib.load().hsv_set_variant(v), "hsv_set_variant")
+    """Test/measurement hook (libhsv_test.so / libhsv_all.so only)."""
+    _lib.check(_lib.hook("hsv_set_variant")(v), "hsv_set_variant")
 
 
 def get_variant() -> int:
@@ -116,15 +136,15 @@ def get_variant() -> int:
 
 def num_variants() -> int:
     """Size of the variant id space (not all ids are built: see variants())."""
-    return _lib.load().hsv_num_variants()
+    return _lib.hook("hsv_num_variants")()
 
 
 def variants() -> list:
     """Kernel variant ids built into the loaded library (product build: 19, 21)."""
-    lib = _lib.load()
-    n = lib.hsv_variant_list(None, 0)
+    fn = _lib.hook("hsv_variant_list")
+    n = fn(None, 0)
     buf = (ctypes.c_int * n)()
-    lib.hsv_variant_list(buf, n)
+    fn(buf, n)
     return list(buf)
 
 
@@ -135,4 +155,4 @@ def bind_device(device: int) -> int:
 
 def set_virtual_shards(k: int) -> None:
     """Test hook: split host batches of >= 2^16 items into k shards (0 = default)."""
-    _lib.check(_lib.load().hsv_set_virtual_shards(k), "hsv_set_virtual_shards")
+    _lib.check(_lib.hook("hsv_set_virtual_shards")(k), "hsv_set_virtual_shards")

@@ -36,6 +36,15 @@
 extern "C" {
 #endif
 
+/* Every function below is exported from libhsv.so; nothing else is (the
+ * library is built with -fvisibility=hidden and a version script, and
+ * tests/test_capi.py checks that its dynamic symbols are exactly these). */
+#if defined(__GNUC__) || defined(__clang__)
+#define HSV_API __attribute__((visibility("default")))
+#else
+#define HSV_API
+#endif
+
 /* ---- per-signature flag byte (hsv_verify / hsv_verify_device) ---------- */
 #define HSV_STRICT_OK 0x01u /* == ed25519-dalek PublicKey::verify_strict Ok   */
 #define HSV_EQ_OK 0x02u     /* PARSE_OK and [s]B == R + [k]A (cofactorless)    */
@@ -82,37 +91,37 @@ extern "C" {
  * Device-resident calls (hsv_*_device*) always run on the device that owns
  * their input pointers; a stream of another device is an error.
  * Returns < 0 for a device index out of range. */
-int hsv_init(int device);
+HSV_API int hsv_init(int device);
 /* The binding in effect: a device index, or -1 for "every device". */
-int hsv_bound_device(void);
+HSV_API int hsv_bound_device(void);
 /* Release all device buffers, streams and pinned staging memory. */
-void hsv_shutdown(void);
+HSV_API void hsv_shutdown(void);
 /* Number of visible HIP devices (0 when none). */
-int hsv_device_count(void);
+HSV_API int hsv_device_count(void);
 /* Human-readable description of the last error on the calling thread. */
-const char *hsv_last_error(void);
+HSV_API const char *hsv_last_error(void);
 /* Library version string. */
-const char *hsv_version(void);
+HSV_API const char *hsv_version(void);
 
 /* ---- verification, host buffers (synchronous) --------------------------- */
 /* Verify n independent triples.  pk: n*32 B, sig: n*64 B (R||s),
  * msg: n*32 B when msg_stride == 32, or one shared 32-B digest when
  * msg_stride == 0 (the QC case).  flags_out: n bytes (HSV_* bits above).
  * n == 0 is valid and does nothing. */
-int hsv_verify(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, size_t msg_stride,
+HSV_API int hsv_verify(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, size_t msg_stride,
                size_t n, uint8_t *flags_out);
 
 /* crypto::Signature::verify (crypto/src/lib.rs:204-208):
  * returns 1 = Ok, 0 = Err(CryptoError), < 0 = infrastructure error. */
-int hsv_verify_strict(const uint8_t digest[32], const uint8_t pk[32], const uint8_t sig[64]);
+HSV_API int hsv_verify_strict(const uint8_t digest[32], const uint8_t pk[32], const uint8_t sig[64]);
 
 /* crypto::Signature::verify_batch (crypto/src/lib.rs:210-223), votes as
  * parallel arrays pk[n*32], sig[n*64] over one shared digest:
  * returns 1 = Ok, 0 = Err, < 0 = infrastructure error.  n == 0 -> 1 (Ok). */
-int hsv_verify_batch(const uint8_t digest[32], const uint8_t *pk, const uint8_t *sig, size_t n);
+HSV_API int hsv_verify_batch(const uint8_t digest[32], const uint8_t *pk, const uint8_t *sig, size_t n);
 
 /* Same, votes packed as n 96-byte records pk(32)||R(32)||s(32). */
-int hsv_verify_batch_packed(const uint8_t digest[32], const uint8_t *votes, size_t n);
+HSV_API int hsv_verify_batch_packed(const uint8_t digest[32], const uint8_t *votes, size_t n);
 
 /* Automatic committee cache behind hsv_verify_batch[_packed] (on by default;
  * env HSV_AUTO_COMMITTEE=0 turns it off).  Consensus keys repeat every round
@@ -125,12 +134,16 @@ int hsv_verify_batch_packed(const uint8_t digest[32], const uint8_t *votes, size
  * cache miss, never an error; when a full cache keeps missing (a new epoch)
  * it is dropped and relearnt.  Strict batches of <= 4096 cached keys
  * (hsv_verify, hsv_verify_strict) use it too.  enable = 0 also drops it. */
-int hsv_set_auto_committee(int enable);
+HSV_API int hsv_set_auto_committee(int enable);
 /* Number of keys in the automatic cache (0 when none). */
-size_t hsv_auto_committee_size(void);
+HSV_API size_t hsv_auto_committee_size(void);
 /* Wait up to timeout_ms for a pending cache build to be published:
  * 1 = no build in flight, 0 = timed out.  (Warm-up and tests.) */
-int hsv_auto_committee_wait(int timeout_ms);
+HSV_API int hsv_auto_committee_wait(int timeout_ms);
+/* Number of cached-path launches whose device self-check failed since the
+ * process started.  Such a call is answered by the generic kernels instead,
+ * and the cache is dropped and relearnt (its tables are no longer trusted). */
+HSV_API uint64_t hsv_auto_committee_faults(void);
 
 /* ---- verification, device-resident buffers (stream-ordered, async) ------ */
 /* Inputs already in HBM (of any device: the call runs on the device owning
@@ -141,25 +154,36 @@ int hsv_auto_committee_wait(int timeout_ms);
  * Does not synchronise.  Batches above 2^22 items run as 2^22-item launches
  * alternating over `stream` and a library stream forked from and joined back
  * into `stream` by events: the call stays ordered on `stream` as one unit. */
-int hsv_verify_device(const uint8_t *d_pk, size_t pk_stride, const uint8_t *d_sig,
+HSV_API int hsv_verify_device(const uint8_t *d_pk, size_t pk_stride, const uint8_t *d_sig,
                       size_t sig_stride, const uint8_t *d_msg, size_t msg_stride, size_t n,
                       uint8_t *d_flags, void *stream);
 
 /* As hsv_verify_device, additionally packing STRICT_OK bits into
  * d_strict_bits[(n+31)/32] (bit i of word i/32 = item i).  Either output
- * pointer may be NULL. */
-int hsv_verify_device_bits(const uint8_t *d_pk, size_t pk_stride, const uint8_t *d_sig,
+ * pointer may be NULL.
+ * d_fault (optional): two device words owned by the caller.  The library
+ * zeroes them on `stream` before the call's launches and the kernels set
+ * d_fault[0] (a final point failed the curve self-check) and d_fault[1] (a
+ * workspace canary changed, i.e. memory the launch wrote was overwritten).
+ * Read them after synchronising `stream`: both zero means the flags are a
+ * verdict, anything else is an infrastructure error (HSV_ERR_DEVICE_FAULT on
+ * the host-buffer calls).  The words belong to this call alone, so concurrent
+ * callers on other streams never see or clear each other's faults.  With
+ * d_fault NULL the launches report into the per-device word read by
+ * hsv_device_faults. */
+HSV_API int hsv_verify_device_bits(const uint8_t *d_pk, size_t pk_stride, const uint8_t *d_sig,
                            size_t sig_stride, const uint8_t *d_msg, size_t msg_stride, size_t n,
-                           uint8_t *d_flags, uint32_t *d_strict_bits, void *stream);
+                           uint8_t *d_flags, uint32_t *d_strict_bits, uint32_t *d_fault, void *stream);
 
-/* Device self-check results of the device-resident calls on `device` (-1:
- * every device) since the last clear.  The stream-ordered calls cannot return
- * a kernel's outcome, so their kernels record it in a per-device word; read it
- * after synchronising the stream the calls ran on.  Returns 0 (no fault), the
- * fault bits (1: a final point failed the curve check, 2: a workspace canary
- * changed), or < 0 on error.  clear != 0 resets the word(s).  Host-buffer
- * calls report their own launches' faults as HSV_ERR_DEVICE_FAULT instead. */
-int hsv_device_faults(int device, int clear);
+/* Self-check results of the device-resident calls on `device` (-1: every
+ * device) that ran without a d_fault of their own, since the last clear.
+ * Read after synchronising the streams those calls ran on.  Returns 0 (no
+ * fault), the fault bits (1: curve check, 2: canary), or < 0 on error.
+ * clear != 0 reads and resets the word in one atomic exchange on the device,
+ * so a fault recorded by a launch still running on another stream is either
+ * returned now or kept for the next read, never lost.  Host-buffer calls
+ * report their own launches' faults as HSV_ERR_DEVICE_FAULT instead. */
+HSV_API int hsv_device_faults(int device, int clear);
 
 /* ---- committee key cache --------------------------- */
 /* Consensus keys are fixed per epoch (consensus/src/config.rs Committee).  A
@@ -170,24 +194,25 @@ int hsv_device_faults(int device, int clear);
  * through HSV_A_OK / HSV_SMALL_A exactly as the generic path does). */
 typedef struct hsv_committee hsv_committee;
 /* Build tables for n public keys (n*32 B). */
-int hsv_committee_create(const uint8_t *pks, size_t n, hsv_committee **out);
-void hsv_committee_destroy(hsv_committee *c);
-size_t hsv_committee_size(const hsv_committee *c);
+HSV_API int hsv_committee_create(const uint8_t *pks, size_t n, hsv_committee **out);
+HSV_API void hsv_committee_destroy(hsv_committee *c);
+HSV_API size_t hsv_committee_size(const hsv_committee *c);
 /* Index of pk in the committee, or -1. */
-int64_t hsv_committee_index(const hsv_committee *c, const uint8_t pk[32]);
+HSV_API int64_t hsv_committee_index(const hsv_committee *c, const uint8_t pk[32]);
 /* Votes by member index: key_idx[m], sig m*64 B, msg m*32 B (msg_stride 32)
  * or one shared digest (msg_stride 0); flags_out m bytes.  An index >= n
  * yields flags 0. */
-int hsv_committee_verify(hsv_committee *c, const uint32_t *key_idx, const uint8_t *sig,
+HSV_API int hsv_committee_verify(hsv_committee *c, const uint32_t *key_idx, const uint8_t *sig,
                          const uint8_t *msg, size_t msg_stride, size_t m, uint8_t *flags_out);
 /* crypto::Signature::verify_batch over votes packed pk||R||s: members use the
  * cached tables, any other key the generic kernel.  1 = Ok, 0 = Err, < 0 error. */
-int hsv_committee_verify_batch_packed(hsv_committee *c, const uint8_t digest[32], const uint8_t *votes,
+HSV_API int hsv_committee_verify_batch_packed(hsv_committee *c, const uint8_t digest[32], const uint8_t *votes,
                                       size_t m);
-/* Device-resident, stream-ordered form (device = the committee's). */
-int hsv_committee_verify_device(const hsv_committee *c, const uint32_t *d_key_idx, const uint8_t *d_sig,
+/* Device-resident, stream-ordered form (device = the committee's); d_fault
+ * (optional) as hsv_verify_device_bits. */
+HSV_API int hsv_committee_verify_device(const hsv_committee *c, const uint32_t *d_key_idx, const uint8_t *d_sig,
                                 size_t sig_stride, const uint8_t *d_msg, size_t msg_stride, size_t m,
-                                uint8_t *d_flags, void *stream);
+                                uint8_t *d_flags, uint32_t *d_fault, void *stream);
 
 /* ---- mempool transactions -------------------------- */
 /* A client transaction is  message || pk (32 B) || sig (64 B, R||s)  and its
@@ -201,18 +226,19 @@ int hsv_committee_verify_device(const hsv_committee *c, const uint32_t *d_key_id
 
 /* Ragged batch: transaction i is txs[offsets[i] .. offsets[i+1]) (n+1
  * offsets).  flags_out: n bytes. */
-int hsv_verify_transactions(const uint8_t *txs, const uint64_t *offsets, size_t n, uint8_t *flags_out);
+HSV_API int hsv_verify_transactions(const uint8_t *txs, const uint64_t *offsets, size_t n, uint8_t *flags_out);
 
 /* Fixed-size batch (the benchmark client's transactions all have the same
  * size, node/src/client.rs): transaction i is txs[i*tx_size .. (i+1)*tx_size). */
-int hsv_verify_transactions_fixed(const uint8_t *txs, size_t tx_size, size_t n, uint8_t *flags_out);
+HSV_API int hsv_verify_transactions_fixed(const uint8_t *txs, size_t tx_size, size_t n, uint8_t *flags_out);
 
 /* Device-resident, stream-ordered form.  d_offsets (n+1 entries, relative to
  * d_txs) or NULL for fixed-size transactions of tx_size bytes.  Any alignment
- * of d_txs.  Transactions shorter than 96 bytes get flags 0.  Outputs as
- * hsv_verify_device_bits (either may be NULL, not both). */
-int hsv_verify_transactions_device(const uint8_t *d_txs, const uint64_t *d_offsets, size_t tx_size, size_t n,
-                                   uint8_t *d_flags, uint32_t *d_strict_bits, void *stream);
+ * of d_txs.  Transactions shorter than 96 bytes get flags 0.  Outputs and
+ * d_fault as hsv_verify_device_bits (d_flags / d_strict_bits: either may be
+ * NULL, not both). */
+HSV_API int hsv_verify_transactions_device(const uint8_t *d_txs, const uint64_t *d_offsets, size_t tx_size, size_t n,
+                                   uint8_t *d_flags, uint32_t *d_strict_bits, uint32_t *d_fault, void *stream);
 
 /* ---- wire formats ---------------------------------- */
 /* Certificates verified straight from their bincode bytes (bincode 1.3
@@ -228,23 +254,23 @@ int hsv_verify_transactions_device(const uint8_t *d_txs, const uint64_t *d_offse
  * qc.digest() = SHA-512(hash || round_le)[..32] (messages.rs:201-207).
  * n_votes_out (optional): number of votes; pks_out (optional, 32 B per vote):
  * the decoded keys, in order. */
-int hsv_qc_verify_bincode(const uint8_t *buf, size_t len, size_t *n_votes_out, uint8_t *pks_out);
+HSV_API int hsv_qc_verify_bincode(const uint8_t *buf, size_t len, size_t *n_votes_out, uint8_t *pks_out);
 
 /* consensus::TC (messages.rs:281-285): round (u64) | votes
  * Vec<(PublicKey, Signature, Round)>.  Checks every vote with
  * Signature::verify over SHA-512(round_le || high_qc_round_le)[..32]
  * (messages.rs:306-313); 1 iff all pass.  flags_out (optional, one byte per
  * vote): the per-vote HSV_* flags. */
-int hsv_tc_verify_bincode(const uint8_t *buf, size_t len, size_t *n_votes_out, uint8_t *flags_out);
+HSV_API int hsv_tc_verify_bincode(const uint8_t *buf, size_t len, size_t *n_votes_out, uint8_t *flags_out);
 
 /* ---- signing (host CPU; not on the hot path) ---------------------------- */
 /* Public key for a 32-byte secret seed (dalek Keypair from SecretKey). */
-int hsv_public_key(const uint8_t seed[32], uint8_t pk_out[32]);
+HSV_API int hsv_public_key(const uint8_t seed[32], uint8_t pk_out[32]);
 /* RFC 8032 deterministic signature (Signature::new). */
-int hsv_sign(const uint8_t seed[32], const uint8_t *msg, size_t msg_len, uint8_t sig_out[64]);
+HSV_API int hsv_sign(const uint8_t seed[32], const uint8_t *msg, size_t msg_len, uint8_t sig_out[64]);
 /* Bulk: n seeds (n*32 B), n messages of msg_len bytes each; writes n public
  * keys and n signatures.  nthreads <= 0 picks min(hardware concurrency, 16). */
-int hsv_sign_many(const uint8_t *seeds, const uint8_t *msgs, size_t msg_len, size_t n,
+HSV_API int hsv_sign_many(const uint8_t *seeds, const uint8_t *msgs, size_t msg_len, size_t n,
                   uint8_t *pk_out, uint8_t *sig_out, int nthreads);
 
 /* Synthesis helper for the corrupted-input mixes (SURVEY 8(d) C3/C4 "mixed-
@@ -253,13 +279,35 @@ int hsv_sign_many(const uint8_t *seeds, const uint8_t *msgs, size_t msg_len, siz
  * a signature over msg whose challenge k is = 0 (mod 8) when accept != 0
  * (verify_strict accepts: cofactorless equation holds) or != 0 (mod 8) when
  * accept == 0 (rejected; a cofactored verifier would accept). */
-int hsv_sign_mixed_order(const uint8_t seed[32], const uint8_t *msg, size_t msg_len, int torsion, int accept,
+HSV_API int hsv_sign_mixed_order(const uint8_t seed[32], const uint8_t *msg, size_t msg_len, int torsion, int accept,
                          uint8_t pk_out[32], uint8_t sig_out[64]);
 
 /* ---- measurement helpers ------------------------------------------------ */
 /* Measured issue rate of v_mad_u64_u32 on the current device, in
  * multiply-accumulates per second (the roofline denominator). */
-double hsv_measure_mad_peak(void);
+HSV_API double hsv_measure_mad_peak(void);
+/* Kernel variant id the library runs (21: the product default). */
+HSV_API int hsv_get_variant(void);
+/* Host threads of the staging-copy pool, the calling thread excluded. */
+HSV_API int hsv_pack_threads(void);
+/* The calling thread's last host-buffer verification: host milliseconds spent
+ * packing into pinned staging, bytes copied host-to-device, wall milliseconds
+ * of the call (any pointer may be NULL). */
+HSV_API void hsv_host_call_stats(double *pack_ms, double *h2d_bytes, double *call_ms);
+/* Host timeline of the calling thread's last call, milliseconds from its
+ * entry.  For a latency call (one launch: a QC, a vote, a small batch) the
+ * HSV_MARK_* points below (a point the call did not pass reads -1); for a
+ * pipelined call four marks per chunk (staging buffer free, packed, copy
+ * enqueued, launch enqueued).  Writes min(count, cap) values to out (may be
+ * NULL) and returns the count. */
+#define HSV_MARK_LOOKUP 0  /* committee-cache lookup done                 */
+#define HSV_MARK_SLOT 1    /* staging slot leased                         */
+#define HSV_MARK_STAGED 2  /* inputs packed into pinned staging           */
+#define HSV_MARK_LAUNCH 3  /* kernel launch enqueued                      */
+#define HSV_MARK_SYNC 4    /* stream synchronisation returned             */
+#define HSV_MARK_DONE 5    /* flags copied out, self-check words read     */
+#define HSV_MARKS 6
+HSV_API int hsv_host_call_marks(double *out, int cap);
 
 #ifdef __cplusplus
 }

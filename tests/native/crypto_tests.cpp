@@ -220,16 +220,22 @@ static void install_host_route() {
   set_host_route(std::move(r));
 }
 
-// libhsv's fault injection hook (test only, not in hsv.h)
-extern "C" int hsv_test_inject_fault(int mode);
+#ifdef HSV_TEST_HOOKS
+// libhsv_test.so's fault injection hook (csrc/hsv_test_hooks.h; libhsv.so
+// exports no hook, so the --inject build links libhsv_test.so)
+#include "hsv_test_hooks.h"
+#endif
 
 int main(int argc, char **argv) {
   bool fallback = false;
   for (int i = 1; i < argc; ++i) {
     if (std::strcmp(argv[i], "--fallback") == 0) fallback = true;
     if (std::strcmp(argv[i], "--route") == 0) install_host_route();
-    // --inject MODE: every launch reads corrupted tables (csrc/hsv_verify_core.hpp kInject*)
+#ifdef HSV_TEST_HOOKS
+    // --inject MODE: every launch of this (the main) thread reads corrupted
+    // tables (csrc/hsv_verify_core.hpp kInject*)
     if (std::strcmp(argv[i], "--inject") == 0 && i + 1 < argc) hsv_test_inject_fault(std::atoi(argv[++i]));
+#endif
   }
   if (fallback) install_oracle_fallback();
   import_export_public_key();

@@ -10,21 +10,35 @@ from conftest import PKG, ROOT
 BIN = os.path.join(ROOT, "build", "crypto_tests")
 
 
+def _build(out, hooks):
+    """The port linked against libhsv.so, or (hooks) against libhsv_test.so
+    with the --inject option compiled in."""
+    libdir = os.path.join(PKG, "hsverify")
+    # the C oracle is linked in only as the --fallback stand-in for a host verifier
+    oracle_o = BIN + "_oracle.o"
+    if not os.path.exists(oracle_o):
+        subprocess.run(["gcc", "-O2", "-c", os.path.join(ROOT, "oracle", "ed25519_oracle.c"), "-o", oracle_o],
+                       check=True)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Wno-unknown-pragmas",
+                    "-I", os.path.join(ROOT, "include"), "-I", os.path.join(PKG, "csrc")]
+                   + (["-DHSV_TEST_HOOKS=1"] if hooks else [])
+                   + [os.path.join(ROOT, "tests", "native", "crypto_tests.cpp"), oracle_o,
+                      "-L", libdir, "-lhsv_test" if hooks else "-lhsv", f"-Wl,-rpath,{libdir}", "-lpthread",
+                      "-o", out], check=True)
+    return out
+
+
 @pytest.fixture(scope="module")
 def crypto_tests_bin():
     from hsverify import _lib
     _lib.load(require=True)  # libhsv.so must exist (built by __graft_entry__.build)
     os.makedirs(os.path.dirname(BIN), exist_ok=True)
-    libdir = os.path.join(PKG, "hsverify")
-    # the C oracle is linked in only as the --fallback stand-in for a host verifier
-    oracle_o = BIN + "_oracle.o"
-    subprocess.run(["gcc", "-O2", "-c", os.path.join(ROOT, "oracle", "ed25519_oracle.c"), "-o", oracle_o],
-                   check=True)
-    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Wno-unknown-pragmas",
-                    "-I", os.path.join(ROOT, "include"), "-I", os.path.join(PKG, "csrc"),
-                    os.path.join(ROOT, "tests", "native", "crypto_tests.cpp"), oracle_o,
-                    "-L", libdir, "-lhsv", f"-Wl,-rpath,{libdir}", "-lpthread", "-o", BIN], check=True)
-    return BIN
+    return _build(BIN, hooks=False)
+
+
+@pytest.fixture(scope="module")
+def crypto_tests_hooks_bin(crypto_tests_bin):
+    return _build(BIN + "_hooks", hooks=True)
 
 
 def test_cpp_mirror_raises_infrastructure_error_without_gpu(crypto_tests_bin):
@@ -91,7 +105,7 @@ def test_cpp_port_of_reference_crypto_tests(crypto_tests_bin, hsv):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", [1, 3])
-def test_cpp_mirror_corrupted_tables_are_infrastructure_errors(crypto_tests_bin, hsv, mode):
+def test_cpp_mirror_corrupted_tables_are_infrastructure_errors(crypto_tests_hooks_bin, hsv, mode):
     """Deterministic replacement of round 2's 8-process soak.
     The forged-vote acceptance came from table memory that read back as zeros
     between the table build and the window loop.  Fault injection reproduces
@@ -100,10 +114,10 @@ def test_cpp_mirror_corrupted_tables_are_infrastructure_errors(crypto_tests_bin,
     InfrastructureError -- never Ok, never Err -- and with the caller's
     fallback installed the fallback answers every call and the reference's
     tests pass."""
-    r = subprocess.run([crypto_tests_bin, "--inject", str(mode)], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([crypto_tests_hooks_bin, "--inject", str(mode)], capture_output=True, text=True, timeout=120)
     assert r.returncode != 0
     assert "InfrastructureError" in r.stderr and "self-check" in r.stderr, r.stderr
-    r = subprocess.run([crypto_tests_bin, "--inject", str(mode), "--fallback"], capture_output=True, text=True,
+    r = subprocess.run([crypto_tests_hooks_bin, "--inject", str(mode), "--fallback"], capture_output=True, text=True,
                        timeout=120)
     assert r.returncode == 0, r.stderr
     assert "all passed" in r.stdout

@@ -52,15 +52,17 @@ def test_virtual_shards_gather_matches_unsharded_and_oracle(mods, oracle_lib, sh
     """run_host's multi-device path: contiguous shards, one host thread and
     slot each, flags written into the caller's buffer at the shard offsets."""
     _, _, synth, verifier = mods
+    from hsverify import _testing
     n = (1 << 16) + 12345
     w = synth.independent_triples(n, seed=500 + shards, corrupt_frac=0.05)
-    verifier.set_virtual_shards(0)
-    whole = verifier.verify_flags(w.pk, w.sig, w.msg)
-    try:
-        verifier.set_virtual_shards(shards)
-        sharded = verifier.verify_flags(w.pk, w.sig, w.msg)
-    finally:
+    with _testing.test_library():
         verifier.set_virtual_shards(0)
+        whole = verifier.verify_flags(w.pk, w.sig, w.msg)
+        try:
+            verifier.set_virtual_shards(shards)
+            sharded = verifier.verify_flags(w.pk, w.sig, w.msg)
+        finally:
+            verifier.set_virtual_shards(0)
     assert (sharded == whole).all()
     assert (whole[w.accept] & o.STRICT_OK).all() and not (whole[~w.accept] & o.STRICT_OK).any()
     # oracle sample around every shard boundary
@@ -72,14 +74,16 @@ def test_virtual_shards_gather_matches_unsharded_and_oracle(mods, oracle_lib, sh
 def test_virtual_shards_transactions(mods, oracle_lib):
     from hsverify import mempool
     _, _, synth, verifier = mods
+    from hsverify import _testing
     n = (1 << 16) + 77
     w = synth.transactions(n, tx_size=200, seed=31)
-    whole = mempool.verify_transactions_fixed(w.txs)
-    try:
-        verifier.set_virtual_shards(4)
-        sharded = mempool.verify_transactions_fixed(w.txs)
-    finally:
-        verifier.set_virtual_shards(0)
+    with _testing.test_library():
+        whole = mempool.verify_transactions_fixed(w.txs)
+        try:
+            verifier.set_virtual_shards(4)
+            sharded = mempool.verify_transactions_fixed(w.txs)
+        finally:
+            verifier.set_virtual_shards(0)
     assert (sharded == whole).all()
     assert (whole[w.accept] & o.STRICT_OK).all() and not (whole[~w.accept] & o.STRICT_OK).any()
 

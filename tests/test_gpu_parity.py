@@ -25,16 +25,21 @@ def api(hsv):
 
 
 def test_golden_every_variant(api, golden):
+    """Every variant built into the library (the product's 19 and 21), switched
+    through the test library's hook (libhsv_test.so: the same objects)."""
     _, verifier, _ = api
-    default = verifier.get_variant()
-    try:
-        for v in verifier.variants():
-            verifier.set_variant(v)
-            got = verifier.verify_flags(golden["pk"], golden["sig"], golden["msg"])
-            bad = np.nonzero(got != golden["flags"])[0]
-            assert bad.size == 0, (v, [(golden["cases"][i], int(got[i]), int(golden["flags"][i])) for i in bad[:8]])
-    finally:
-        verifier.set_variant(default)
+    from hsverify import _testing
+    with _testing.test_library():
+        default = verifier.get_variant()
+        try:
+            for v in verifier.variants():
+                verifier.set_variant(v)
+                got = verifier.verify_flags(golden["pk"], golden["sig"], golden["msg"])
+                bad = np.nonzero(got != golden["flags"])[0]
+                assert bad.size == 0, (v, [(golden["cases"][i], int(got[i]), int(golden["flags"][i]))
+                                           for i in bad[:8]])
+        finally:
+            verifier.set_variant(default)
 
 
 def test_golden_row_form_chunks(api, golden):
@@ -92,33 +97,48 @@ def test_lattice_fallback_records_every_variant(api, fallback_records, bits):
     match the oracle's flags either way.  The automatic committee cache is off
     so the generic kernels run."""
     _, verifier, _ = api
-    from hsverify import _lib, _testing
-    lib = _lib.load()
+    from hsverify import _testing
+    with _testing.test_library() as lib:
+        fb = fallback_records
+        default = verifier.get_variant()
+        prev = _testing.set_lattice_bits(bits)
+        lib.hsv_set_auto_committee(0)
+        try:
+            for v in verifier.variants():
+                verifier.set_variant(v)
+                got = verifier.verify_flags(fb["pk"], fb["sig"], fb["msg"])
+                assert (got == fb["flags"]).all(), (v, np.nonzero(got != fb["flags"])[0][:8])
+                # mixed into a wave of ordinary records (the fallback lane diverges)
+                idx = np.arange(256) % len(fb["flags"])
+                got = verifier.verify_flags(fb["pk"][idx], fb["sig"][idx], fb["msg"][idx])
+                assert (got == fb["flags"][idx]).all(), v
+                # the pair form's range (3073 .. 2^13 items)
+                idx = np.arange(4096) % len(fb["flags"])
+                got = verifier.verify_flags(fb["pk"][idx], fb["sig"][idx], fb["msg"][idx])
+                assert (got == fb["flags"][idx]).all(), v
+                # past the pair form's cut-over: the point pass deals fallback batches first
+                idx = np.arange((1 << 13) + 64) % len(fb["flags"])
+                got = verifier.verify_flags(fb["pk"][idx], fb["sig"][idx], fb["msg"][idx])
+                assert (got == fb["flags"][idx]).all(), v
+        finally:
+            verifier.set_variant(default)
+            _testing.set_lattice_bits(prev)
+            lib.hsv_set_auto_committee(1)
+
+
+def test_lattice_fallback_records_product_library(api, fallback_records, hsv):
+    """The same records on the product library itself (default bound, default
+    variant), in the row, pair and point-pass ranges."""
+    _, verifier, _ = api
     fb = fallback_records
-    default = verifier.get_variant()
-    prev = _testing.set_lattice_bits(bits)
-    lib.hsv_set_auto_committee(0)
+    hsv.hsv_set_auto_committee(0)
     try:
-        for v in verifier.variants():
-            verifier.set_variant(v)
-            got = verifier.verify_flags(fb["pk"], fb["sig"], fb["msg"])
-            assert (got == fb["flags"]).all(), (v, np.nonzero(got != fb["flags"])[0][:8])
-            # mixed into a wave of ordinary records (the fallback lane diverges)
-            idx = np.arange(256) % len(fb["flags"])
+        for m in (len(fb["flags"]), 4096, (1 << 13) + 64):
+            idx = np.arange(m) % len(fb["flags"])
             got = verifier.verify_flags(fb["pk"][idx], fb["sig"][idx], fb["msg"][idx])
-            assert (got == fb["flags"][idx]).all(), v
-            # the pair form's range (3073 .. 2^13 items)
-            idx = np.arange(4096) % len(fb["flags"])
-            got = verifier.verify_flags(fb["pk"][idx], fb["sig"][idx], fb["msg"][idx])
-            assert (got == fb["flags"][idx]).all(), v
-            # past the pair form's cut-over: the point pass deals fallback batches first
-            idx = np.arange((1 << 13) + 64) % len(fb["flags"])
-            got = verifier.verify_flags(fb["pk"][idx], fb["sig"][idx], fb["msg"][idx])
-            assert (got == fb["flags"][idx]).all(), v
+            assert (got == fb["flags"][idx]).all(), m
     finally:
-        verifier.set_variant(default)
-        _testing.set_lattice_bits(prev)
-        lib.hsv_set_auto_committee(1)
+        hsv.hsv_set_auto_committee(1)
 
 
 # ---- the reference's own tests (crypto/src/tests/crypto_tests.rs) ---------

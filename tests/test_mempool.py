@@ -83,15 +83,16 @@ def test_tx_golden_ragged_host_api(hsv, tx_golden):
 
 @pytest.mark.gpu
 def test_tx_golden_every_variant(hsv, tx_golden):
-    from hsverify import mempool, verifier
-    default = verifier.get_variant()
-    try:
-        for v in verifier.variants():
-            verifier.set_variant(v)
-            got = mempool.verify_transactions(tx_golden["txs"])
-            assert (got == tx_golden["flags"]).all(), (v, np.nonzero(got != tx_golden["flags"])[0][:8])
-    finally:
-        verifier.set_variant(default)
+    from hsverify import _testing, mempool, verifier
+    with _testing.test_library():
+        default = verifier.get_variant()
+        try:
+            for v in verifier.variants():
+                verifier.set_variant(v)
+                got = mempool.verify_transactions(tx_golden["txs"])
+                assert (got == tx_golden["flags"]).all(), (v, np.nonzero(got != tx_golden["flags"])[0][:8])
+        finally:
+            verifier.set_variant(default)
 
 
 @pytest.mark.gpu
