@@ -74,6 +74,14 @@
 #define I_LSHR64(x) "v_lshrrev_b64 " x ", 26, " x "\n\t"
 #define I_LSHLADD64(x) "v_lshl_add_u64 " x ", " x ", 0, %8\n\t"
 #define I_MOV64(x) "v_mov_b64_e32 " x ", %8\n\t"
+// round 4: the f64 path's costs, and gfx950's three-input bit op
+#define I_FMA64(x) "v_fma_f64 " x ", " x ", %8, %8\n\t"
+#define I_ADDF64(x) "v_add_f64 " x ", " x ", %8\n\t"
+#define I_MULF64(x) "v_mul_f64 " x ", " x ", %8\n\t"
+#define I_BITOP3(x) "v_bitop3_b32 " x ", " x ", %8, %9 bitop3:0x96\n\t"
+#define I_MULHI(x) "v_mul_hi_u32 " x ", " x ", %8\n\t"
+#define I_ADDCO(x) "v_add_co_u32_e32 " x ", vcc, %8, " x "\n\t"
+#define I_ADDC(x) "v_addc_co_u32_e32 " x ", vcc, %8, " x ", vcc\n\t"
 
 K32(k_add, I_ADD)
 K32(k_sub, I_SUB)
@@ -102,6 +110,25 @@ K64(k_mad64, I_MAD64)
 K64(k_lshr64, I_LSHR64)
 K64(k_lshladd64, I_LSHLADD64)
 K64(k_mov64, I_MOV64)
+K64(k_fma64, I_FMA64)
+K64(k_addf64, I_ADDF64)
+K64(k_mulf64, I_MULF64)
+K32(k_bitop3, I_BITOP3)
+K32(k_mulhi, I_MULHI)
+
+// carry chains through VCC (v_add_co / v_addc_co: a 64-bit add is one of each)
+__global__ void __launch_bounds__(256) k_addco(uint32_t *sink, uint32_t seed) {
+  uint32_t t = threadIdx.x + blockIdx.x * blockDim.x + seed;
+  uint32_t x0 = t, x1 = t + 1, x2 = t + 2, x3 = t + 3, x4 = t + 4, x5 = t + 5, x6 = t + 6, x7 = t + 7;
+  const uint32_t a = t | 1u, b = t * 7u;
+  for (int it = 0; it < ITERS; ++it)
+    asm volatile(I_ADDCO("%0") I_ADDC("%1") I_ADDCO("%2") I_ADDC("%3") I_ADDCO("%4") I_ADDC("%5") I_ADDCO("%6")
+                     I_ADDC("%7")
+                 : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7)
+                 : "v"(a), "v"(b)
+                 : "vcc");
+  if ((x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7) == 0x12345678u) sink[0] = 1u;
+}
 
 // v_cndmask with VCC / an SGPR pair set once before the loop
 __global__ void __launch_bounds__(256) k_cndmask(uint32_t *sink, uint32_t seed) {
@@ -172,6 +199,8 @@ int main() {
       {"v_alignbit_b32", k_alignbit, 8},   {"v_perm_b32", k_perm, 8},           {"v_cndmask_b32_e32", k_cndmask, 8},
       {"v_cndmask_b32_e64", k_cndmask64, 8}, {"v_mad_u64_u32", k_mad64, 8},     {"v_lshrrev_b64", k_lshr64, 8},
       {"v_lshl_add_u64", k_lshladd64, 8},  {"v_mov_b64_e32", k_mov64, 8},
+      {"v_fma_f64", k_fma64, 8},           {"v_add_f64", k_addf64, 8},          {"v_mul_f64", k_mulf64, 8},
+      {"v_bitop3_b32", k_bitop3, 8},       {"v_mul_hi_u32", k_mulhi, 8},        {"v_add_co/v_addc_co (pairs)", k_addco, 8},
   };
   double base = 0;
   std::printf("device %s CUs=%d  (16 blocks x 256 per CU, 8 chains per lane)\n", prop.gcnArchName, ncu);
