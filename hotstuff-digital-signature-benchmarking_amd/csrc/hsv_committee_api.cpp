@@ -355,7 +355,9 @@ struct AutoCommittee {
   std::unordered_set<Key32, KeyHash> pending_set;
   bool building = false;
   uint64_t generation = 0;  // bumped by a reset; a build of an older generation is discarded
-  uint32_t miss_streak = 0;
+  // batches that missed a full cache in a row; written under mu on a miss,
+  // reset without the lock on a hit (the QC hot path takes no lock)
+  std::atomic<uint32_t> miss_streak{0};
   int failures = 0;
   std::thread worker;
   std::condition_variable idle;
@@ -496,8 +498,7 @@ std::shared_ptr<const AutoView> auto_lookup(const uint8_t *pk, size_t pk_stride,
   AutoCommittee &a = AC();
   if (missing.empty()) {
     if (v && v->dev.device != home_device()) return nullptr;  // cache lives on another device
-    std::lock_guard<std::mutex> lk(a.mu);
-    a.miss_streak = 0;
+    if (a.miss_streak.load(std::memory_order_relaxed)) a.miss_streak.store(0, std::memory_order_relaxed);
     return v;
   }
   if (n > kAutoMaxKeys) return nullptr;  // not a committee-sized batch
@@ -505,7 +506,7 @@ std::shared_ptr<const AutoView> auto_lookup(const uint8_t *pk, size_t pk_stride,
   missing.erase(std::unique(missing.begin(), missing.end()), missing.end());  // once per batch
   std::unique_lock<std::mutex> lk(a.mu);
   const uint32_t cached = v ? v->dev.n : 0;
-  if (cached + a.pending_set.size() >= kAutoMaxKeys && ++a.miss_streak >= kResetAfterMisses) {
+  if (cached + a.pending_set.size() >= kAutoMaxKeys && a.miss_streak.fetch_add(1) + 1 >= kResetAfterMisses) {
     // a full cache that keeps missing: a new epoch, relearn from scratch
     std::atomic_store(&a.view, std::shared_ptr<const AutoView>());
     a.seen.clear();
