@@ -751,6 +751,88 @@ int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, siz
   return HSV_OK;
 }
 
+// Large host batches, streamed (round 4; the default for variant 21): ONE
+// persistent launch over the whole batch (n <= kChunk), started before the
+// inputs are packed.  The pinned staging holds every record; the pack pool
+// packs it piece by piece (2^14 items, 2 or 1.5 MiB) and marks each piece
+// ready in a pinned word the kernel polls before it touches the piece; the
+// kernel reads the records and writes the flags through the staging's device
+// mapping (hsv_verify_stream_kernel).  No copy engine, no chunk launches and
+// their grid ends: the call costs one launch over the batch plus the first
+// piece's pack.  Pinned layout: records n*rec | shared digest | ready words |
+// flags n | self-check words (3: curve check, canary, input timeout).
+constexpr uint32_t kStreamPieceLog2 = 14;
+// A wave polls an unready piece at most this often (about 4 us a poll, so
+// ~2 s) before the launch gives up: the host packs every piece within
+// milliseconds, so a launch still waiting has lost its host thread.
+constexpr uint32_t kStreamMaxPolls = 1u << 19;
+
+int run_streamed(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, size_t pk_stride, const uint8_t *sig,
+                 size_t sig_stride, const uint8_t *msg, size_t msg_stride, size_t n, uint8_t *flags_out) {
+  const size_t rec = msg_stride ? 128 : 96;
+  const size_t piece = size_t(1) << kStreamPieceLog2;
+  const size_t npieces = (n + piece - 1) / piece;
+  const size_t h_dig = round_up(n * rec, kAlign);
+  const size_t h_ready = h_dig + kAlign;
+  const size_t h_flag = h_ready + round_up(npieces * 4, kAlign);
+  const size_t h_fault = h_flag + round_up(n, kAlign);
+  const size_t h_total = h_fault + kAlign;
+  int rc = slot_prepare(s, 0, 0);
+  if (rc != HSV_OK) return rc;
+  hipError_t e;
+  if (h_total > s.h_stream_cap) {
+    if (s.h_stream) (void)hipHostFree(s.h_stream);
+    s.h_stream = nullptr;
+    s.h_stream_cap = 0;
+    const size_t cap = round_up(h_total, size_t(1) << 20);
+    e = hipHostMalloc(&s.h_stream, cap, hipHostMallocCoherent | hipHostMallocMapped);
+    if (e != hipSuccess) return hip_fail("hipHostMalloc (streamed staging)", e);
+    s.h_stream_cap = cap;
+  }
+  rc = slot_workspaces(s, hsv_launch_stream_ws_bytes((uint32_t)n));
+  if (rc != HSV_OK) return rc;
+  void *hd = nullptr;
+  e = hipHostGetDevicePointer(&hd, s.h_stream, 0);
+  if (e != hipSuccess || !hd) return hip_fail("hipHostGetDevicePointer (streamed staging)", e);
+  uint8_t *h = s.h_stream, *d = static_cast<uint8_t *>(hd);
+  volatile uint32_t *ready = reinterpret_cast<volatile uint32_t *>(h + h_ready);
+  // nothing of an earlier call is in flight on this slot (its calls synchronise)
+  for (size_t p = 0; p < npieces; ++p) ready[p] = 0u;
+  std::memset(h + h_fault, 0, 16);
+  if (msg_stride == 0) std::memcpy(h + h_dig, msg, 32);
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  t_clock.marks.clear();
+  call_chunk_mark();
+  e = hsv_launch_verify_stream(d, (uint32_t)rec, msg_stride ? nullptr : d + h_dig, (uint32_t)n, kStreamPieceLog2,
+                               reinterpret_cast<const uint32_t *>(d + h_ready), d + h_flag, comb_b,
+                               reinterpret_cast<uint32_t *>(d + h_fault), kStreamMaxPolls, s.d_ws[0], s.ws_cap,
+                               s.stream);
+  if (e != hipSuccess) return hip_fail("streamed verify launch", e);
+  call_chunk_mark();
+  // the launch is queued: pack the pieces, in order of the pool's counter;
+  // each packed piece is published with a release store after the streaming
+  // stores' fence (pack_records), so the kernel never reads a half-packed piece
+  const auto t_pack = std::chrono::steady_clock::now();
+  PackPool::get().run((int)npieces, [&](int p) {
+    const size_t lo = (size_t)p * piece, hi = std::min(n, lo + piece);
+    pack_records(h, rec, pk, pk_stride, sig, sig_stride, msg, msg_stride, lo, hi);
+    std::atomic_thread_fence(std::memory_order_release);
+    ready[p] = 1u;
+  });
+  t_pack_ms += ms_since(t_pack);
+  call_chunk_mark();
+  e = hipStreamSynchronize(s.stream);
+  call_chunk_mark();
+  if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
+  uint32_t w[3];
+  std::memcpy(w, h + h_fault, sizeof(w));
+  if (w[2]) return fail(HSV_ERR_HIP, "streamed verify: the kernel waited too long for its inputs and aborted");
+  rc = check_faults(h + h_fault, "verify");
+  if (rc != HSV_OK) return rc;
+  std::memcpy(flags_out, h + h_flag, n);
+  return HSV_OK;
+}
+
 int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t *sig, size_t sig_stride,
                   const uint8_t *msg, size_t msg_stride, size_t n, uint8_t *flags_out) {
   static const bool no_pipe = std::getenv("HSV_NO_PIPELINE") != nullptr;        // measurement switch
@@ -768,6 +850,21 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
   Slot &s = lease.slot();
   call_mark(HSV_MARK_SLOT);
   const size_t pchunk = pipe_chunk();
+  // HSV_HOST_PIPE=chunked: round 3's copy pipeline instead (measurement switch)
+  static const bool chunked = [] {
+    const char *e = std::getenv("HSV_HOST_PIPE");
+    return e && std::strcmp(e, "chunked") == 0;
+  }();
+  if (!no_pipe && !chunked && v == 21 && n >= 2 * pchunk) {
+    for (size_t base = 0; base < n; base += kChunk) {
+      const size_t m = std::min(kChunk, n - base);
+      rc = run_streamed(s, v, comb_b, pk + base * pk_stride, pk_stride, sig + base * sig_stride, sig_stride,
+                        msg + base * msg_stride, msg_stride, m, flags_out + base);
+      if (rc != HSV_OK) return rc;
+    }
+    t_call_ms = ms_since(t_call);
+    return HSV_OK;
+  }
   if (!no_pipe && n >= 2 * pchunk) {
     for (size_t base = 0; base < n; base += kChunk) {
       const size_t m = std::min(kChunk, n - base);
@@ -970,6 +1067,9 @@ void hsv_shutdown(void) {
       s.ws_cap = 0;
       if (s.d_buf) (void)hipFree(s.d_buf);
       if (s.h_buf) (void)hipHostFree(s.h_buf);
+      if (s.h_stream) (void)hipHostFree(s.h_stream);
+      s.h_stream = nullptr;
+      s.h_stream_cap = 0;
       s.stream = s.stream2 = nullptr;
       s.d_buf = s.h_buf = nullptr;
       s.d_cap = s.h_cap = 0;

@@ -64,6 +64,11 @@ struct Slot {
   size_t d_cap = 0;
   uint8_t *h_buf = nullptr;
   size_t h_cap = 0;
+  // pinned staging of the streamed host path (run_streamed), allocated
+  // coherent: the running kernel reads pieces the host publishes after it
+  // started, so the GPU must not serve them from a cache
+  uint8_t *h_stream = nullptr;
+  size_t h_stream_cap = 0;
 };
 
 struct DevCtx {

@@ -47,6 +47,19 @@ hipError_t hsv_launch_verify_ws(int variant, const uint8_t *pk, uint64_t pk_stri
                                 uint8_t *flags_out, uint32_t *strict_bits, const uint32_t *comb_b, uint32_t *fault,
                                 void *ws, size_t ws_cap, hipStream_t stream);
 size_t hsv_launch_ws_bytes(int variant, uint32_t n);
+// Streamed host batch (variant 21, >= 2^18 items from host buffers): ONE
+// persistent launch over n records that the host is still packing.  recs:
+// device view of the pinned records (rec_bytes 128 = pk|R|s|digest, or 96 with
+// shared_msg the device view of one shared digest); piece p (2^piece_log2
+// items) may be read once ready[p] != 0 (host-written, pinned); flags_out:
+// device view of n pinned flag bytes; fault: 3 device-visible words the
+// caller zeroed (curve check, canary, input timeout: max_polls polls of an
+// unready piece abort the launch).  ws: hsv_launch_stream_ws_bytes(n) bytes.
+hipError_t hsv_launch_verify_stream(const uint8_t *recs, uint32_t rec_bytes, const uint8_t *shared_msg, uint32_t n,
+                                    uint32_t piece_log2, const uint32_t *ready, uint8_t *flags_out,
+                                    const uint32_t *comb_b, uint32_t *fault, uint32_t max_polls, void *ws,
+                                    size_t ws_cap, hipStream_t stream);
+size_t hsv_launch_stream_ws_bytes(uint32_t n);
 // Fault injection (tests only; hsv_kernels.hip): the mode of the launches the
 // calling thread issues (thread-scoped, so one test's injection never reaches
 // another thread's calls); hsvi_set_inject returns the previous mode, or -1.

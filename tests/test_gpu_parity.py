@@ -141,6 +141,40 @@ def test_lattice_fallback_records_product_library(api, fallback_records, hsv):
         hsv.hsv_set_auto_committee(1)
 
 
+def test_streamed_host_path_with_fallback_items(api, fallback_records, oracle_lib):
+    """Host batches of >= 2^18 items run as one streamed launch
+    (hsv_verify_stream_kernel: per-lane prepass, then the point pass or, for an
+    item without a short lattice pair, the full-length path inline).  With the
+    bound lowered to 133 every fixture record takes the inline full-length
+    path; they sit at random positions among ordinary records."""
+    _, verifier, synth = api
+    from hsverify import _testing
+    fb = fallback_records
+    n = (1 << 18) + 100
+    w = synth.independent_triples(n, seed=2718, corrupt_frac=0.05)
+    pos = np.sort(np.random.default_rng(5).choice(n, 3000, replace=False))
+    src = np.arange(pos.size) % len(fb["flags"])
+    pk, sig, msg = w.pk.copy(), w.sig.copy(), w.msg.copy()
+    pk[pos], sig[pos], msg[pos] = fb["pk"][src], fb["sig"][src], fb["msg"][src]
+    with _testing.test_library() as lib:
+        lib.hsv_set_auto_committee(0)
+        try:
+            for bits in (133, 0):
+                prev = _testing.set_lattice_bits(bits)
+                try:
+                    got = verifier.verify_flags(pk, sig, msg)
+                finally:
+                    _testing.set_lattice_bits(prev)
+                assert (got[pos] == fb["flags"][src]).all(), bits
+                rest = np.setdiff1d(np.arange(n), pos)
+                assert (got[rest][w.accept[rest]] & o.STRICT_OK).all()
+                assert not (got[rest][~w.accept[rest]] & o.STRICT_OK).any()
+                sample = np.sort(np.random.default_rng(6).choice(rest, 2048, replace=False))
+                assert (got[sample] == oracle_flags(oracle_lib, pk[sample], sig[sample], msg[sample])).all()
+        finally:
+            lib.hsv_set_auto_committee(1)
+
+
 # ---- the reference's own tests (crypto/src/tests/crypto_tests.rs) ---------
 def _keys(crypto):
     return [crypto.generate_keypair(lambda n, s=s: s) for s in o.reference_key_seeds()]
@@ -392,9 +426,9 @@ def test_c4_full_size_properties(api, oracle_lib):
 
 
 def test_host_api_pipelined_chunks_match_device_api(api, oracle_lib):
-    """Host batches of >= 2^18 items run as a two-stream pipeline of 2^17-item
-    chunks (hsv_capi.cpp run_on_device): an uneven tail chunk, every flag equal
-    to the device-resident launch, and an oracle-checked sample."""
+    """Host batches of >= 2^18 items run as one streamed launch over pieces of
+    2^14 items (hsv_capi.cpp run_streamed): an uneven last piece, every flag
+    equal to the device-resident launch, and an oracle-checked sample."""
     import torch
     _, verifier, synth = api
     n = (1 << 19) + (1 << 18) + 12345
@@ -412,10 +446,11 @@ def test_host_api_pipelined_chunks_match_device_api(api, oracle_lib):
 
 
 def test_host_api_pipeline_shared_digest_and_packed_votes(api, oracle_lib):
-    """The streamed host pipeline (hsv_capi.cpp run_pipelined: ramped chunks,
-    whole batch in HBM, two compute streams) with one shared digest (a huge
-    QC) and with packed 96-byte votes (hsv_verify_batch_packed's strided
-    records): flags equal the device-resident launch and an oracle sample."""
+    """The streamed host path (hsv_capi.cpp run_streamed: 96-byte records and
+    one shared digest, read through the pinned staging's device mapping) with
+    one shared digest (a huge QC) and with packed 96-byte votes
+    (hsv_verify_batch_packed's strided records): flags equal the
+    device-resident launch and an oracle sample."""
     import torch
     _, verifier, synth = api
     from hsverify import _lib
