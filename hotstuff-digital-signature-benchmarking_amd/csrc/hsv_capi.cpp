@@ -820,6 +820,7 @@ int run_streamed(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, size
     ready[p] = 1u;
   });
   t_pack_ms += ms_since(t_pack);
+  t_h2d_bytes += n * rec;  // read by the kernel over PCIe through the mapping
   call_chunk_mark();
   e = hipStreamSynchronize(s.stream);
   call_chunk_mark();

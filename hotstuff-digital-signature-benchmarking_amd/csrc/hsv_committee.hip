@@ -201,7 +201,7 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
                                   uint32_t m, const uint8_t *__restrict__ pks, const uint8_t *__restrict__ key_flags,
                                   uint32_t nkeys, const uint32_t *const *__restrict__ key_tables,
                                   const uint32_t *__restrict__ btable, uint8_t *__restrict__ flags_out,
-                                  uint32_t inject, uint32_t *__restrict__ fault) {
+                                  uint32_t inject, uint32_t *__restrict__ fault, uint32_t *__restrict__ done) {
   __shared__ uint32_t r_x[kFusedVotes][kFeLimbs], r_y[kFusedVotes][kFeLimbs], r_fl[kFusedVotes];
   __shared__ uint32_t k_rec[kFusedVotes][9], k_ready;
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
@@ -386,6 +386,15 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
   else fb = fault_bit(a_ok, r_ok, q) ? 1u : 0u;
   if (fb | ((rf >> 2) & 1u)) fault[0] = 1u;  // device self-check (hsv_kernels.hip report_faults)
   if (valid && g == 0u) flags_out[i0] = kvalid ? (uint8_t)f : (uint8_t)0;
+  if (done) {
+    // completion marker (HSV_QC_SYNC=marker): every wave of the block is past
+    // its reads (the R and hash waves before the barrier / k_ready), and this
+    // wave's flag and fault stores are released to the system before lane 0
+    // marks the block done, so the host may read the flags off pinned memory
+    // without waiting for the kernel's completion signal
+    __atomic_thread_fence(__ATOMIC_RELEASE);
+    if (lane == 0u) __hip_atomic_store(&done[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // Test hook (tests/test_lanesplit.py): the row forms of hsv_fe16x16.hpp
@@ -495,20 +504,26 @@ extern "C" hipError_t hsv_launch_comb_verify(const uint32_t *key_idx, const uint
                                              const uint8_t *msg, uint64_t msg_stride, uint32_t m,
                                              const uint8_t *pks, const uint8_t *key_flags, uint32_t nkeys,
                                              const uint32_t *const *key_tables, const uint32_t *btable,
-                                             uint8_t *flags_out, uint32_t *fault, hipStream_t stream) {
+                                             uint8_t *flags_out, uint32_t *fault, uint32_t *done,
+                                             hipStream_t stream) {
   if (m == 0) return hipSuccess;
   if (!fault) return hipErrorInvalidValue;
   const uint32_t inject = (uint32_t)hsvi_inject_mode();
   if (m <= kCombQuadMax) {  // latency form: four lanes per vote, R decompressed by the R waves
     hipLaunchKernelGGL(hsv::hsv_comb_verify_quad_fused_kernel, dim3((m + hsv::kFusedVotes - 1) / hsv::kFusedVotes),
                        dim3(hsv::kFusedThreads), 0, stream, key_idx, sig, sig_stride, msg, msg_stride, m, pks, key_flags, nkeys,
-                       key_tables, btable, flags_out, inject, fault);
+                       key_tables, btable, flags_out, inject, fault, done);
     return hipGetLastError();
   }
+  if (done) return hipErrorInvalidValue;  // markers: latency form only
   hipLaunchKernelGGL(hsv::hsv_comb_verify_kernel, dim3((m + 255u) / 256u), dim3(256), 0, stream, key_idx, sig,
                      sig_stride, msg, msg_stride, m, pks, key_flags, nkeys, key_tables, btable, flags_out, inject,
                      fault);
   return hipGetLastError();
+}
+
+extern "C" uint32_t hsv_comb_marker_blocks(uint32_t m) {
+  return m <= kCombQuadMax ? (m + hsv::kFusedVotes - 1) / hsv::kFusedVotes : 0u;
 }
 
 extern "C" uint64_t hsv_comb_table_bytes(void) { return hsv::kCombTableWords * 4ull; }

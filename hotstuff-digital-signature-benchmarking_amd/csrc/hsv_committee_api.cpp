@@ -97,7 +97,8 @@ int committee_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t
     const size_t msg_bytes = msg_stride ? k * 32 : 32;
     const size_t flag_off = msg_off + round_up(msg_bytes, kAlign);
     const size_t fault_off = flag_off + round_up(k, kAlign);
-    const size_t total = fault_off + kAlign;
+    const size_t done_off = fault_off + kAlign;  // completion markers (marker sync), one word per block
+    const size_t total = done_off + round_up((size_t)hsv_comb_marker_blocks((uint32_t)k) * 4 + 4, kAlign);
     rc = slot_prepare(s, total, total);
     if (rc != HSV_OK) return rc;
     uint8_t *h = s.h_buf;
@@ -115,6 +116,16 @@ int committee_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t
       return v ? (size_t)std::atoll(v) : kZeroCopyMax;
     }();
     const bool zero_copy = k <= zc_max && hipHostGetDevicePointer(&hd, h, 0) == hipSuccess && hd;
+    // HSV_QC_SYNC=marker (measurement switch): the zero-copy latency form marks
+    // each block done in pinned memory and the host spins on the markers
+    // instead of hipStreamSynchronize (see the kernel)
+    static const bool marker_sync = [] {
+      const char *v = std::getenv("HSV_QC_SYNC");
+      return v && std::strcmp(v, "marker") == 0;
+    }();
+    const uint32_t nmark = zero_copy && marker_sync ? hsv_comb_marker_blocks((uint32_t)k) : 0u;
+    volatile uint32_t *marks = reinterpret_cast<volatile uint32_t *>(h + done_off);
+    for (uint32_t b = 0; b < nmark; ++b) marks[b] = 0u;
     if (zero_copy) {
       dbuf = static_cast<uint8_t *>(hd);
     } else {
@@ -124,12 +135,31 @@ int committee_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t
     hipError_t e = hsv_launch_comb_verify(reinterpret_cast<const uint32_t *>(dbuf + idx_off), dbuf + sig_off, 64,
                                           dbuf + msg_off, msg_stride ? 32 : 0, (uint32_t)k, cd.d_pks, cd.d_kflags, cd.n,
                                           cd.d_tabptr, c.d_btable, dbuf + flag_off,
-                                          reinterpret_cast<uint32_t *>(dbuf + fault_off), s.stream);
+                                          reinterpret_cast<uint32_t *>(dbuf + fault_off),
+                                          nmark ? reinterpret_cast<uint32_t *>(dbuf + done_off) : nullptr, s.stream);
     if (e == hipSuccess && !zero_copy)
       e = hipMemcpyAsync(h + flag_off, s.d_buf + flag_off, fault_off + kFaultBytes - flag_off, hipMemcpyDeviceToHost,
                          s.stream);
     call_mark(HSV_MARK_LAUNCH);
-    const hipError_t es = hipStreamSynchronize(s.stream);  // nothing of this call stays in flight
+    hipError_t es = hipSuccess;
+    bool marked = false;
+    if (nmark && e == hipSuccess) {
+      // every block past its reads and its stores released: the flags are
+      // final, and nothing of this call reads the staging any more (the next
+      // call on this slot is ordered behind the kernel on the stream); a
+      // kernel that never marks (a device fault) falls back to the stream sync
+      const auto t0 = std::chrono::steady_clock::now();
+      for (uint32_t b = 0;;) {
+        while (b < nmark && marks[b] == 1u) ++b;
+        if (b == nmark) {
+          marked = true;
+          break;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
+      }
+      std::atomic_thread_fence(std::memory_order_acquire);
+    }
+    if (!marked) es = hipStreamSynchronize(s.stream);  // nothing of this call stays in flight
     call_mark(HSV_MARK_SYNC);
     if (e != hipSuccess) return hip_fail("committee verify launch", e);
     if (es != hipSuccess) return hip_fail("hipStreamSynchronize", es);
@@ -264,7 +294,8 @@ int hsv_committee_verify_device(const hsv_committee *cm, const uint32_t *d_key_i
   rc = call_fault_words(c, d_fault, s, &fault);
   if (rc != HSV_OK) return rc;
   const hipError_t e = hsv_launch_comb_verify(d_key_idx, d_sig, sig_stride, d_msg, msg_stride, (uint32_t)m, cm->dev.d_pks,
-                                              cm->dev.d_kflags, cm->dev.n, cm->dev.d_tabptr, c.d_btable, d_flags, fault, s);
+                                              cm->dev.d_kflags, cm->dev.n, cm->dev.d_tabptr, c.d_btable, d_flags, fault,
+                                              nullptr, s);
   return e == hipSuccess ? HSV_OK : hip_fail("committee verify launch", e);
 }
 

@@ -95,7 +95,12 @@ hipError_t hsv_launch_comb_build(const uint8_t *encs, uint32_t nkeys, uint32_t n
 hipError_t hsv_launch_comb_verify(const uint32_t *key_idx, const uint8_t *sig, uint64_t sig_stride,
                                   const uint8_t *msg, uint64_t msg_stride, uint32_t m, const uint8_t *pks,
                                   const uint8_t *key_flags, uint32_t nkeys, const uint32_t *const *key_tables,
-                                  const uint32_t *btable, uint8_t *flags_out, uint32_t *fault, hipStream_t stream);
+                                  const uint32_t *btable, uint8_t *flags_out, uint32_t *fault, uint32_t *done,
+                                  hipStream_t stream);
+// Completion markers of the latency form (done != NULL above, m votes): one
+// word per block, set to 1 by the block once its flags are released to the
+// system; 0 when m is above the latency form's range (no markers).
+uint32_t hsv_comb_marker_blocks(uint32_t m);
 uint64_t hsv_comb_table_bytes(void);
 uint64_t hsv_comb_tmp_bytes(uint32_t nkeys);
 // wide (16-bit digit) comb table of B, hsv_comb.hpp

@@ -32,6 +32,13 @@ q=d.get('qc_latency', {})
 for k, v in q.items():
     if isinstance(v, dict): print(k, v.get('p50_ms'), v.get('p99_ms'), v.get('max_ms'), v.get('tail', {}).get('phases_ms'))
 " ; fatal $rc $st ;;
+    qcab)
+      timeout -k 10 600 python -u tools/qc_ab.py --rounds 3 --reps 300 libhsv.so libhsv.so:HSV_QC_SYNC=marker \
+        > $OUT/${TAG}_qc_ab_marker.txt 2>&1; rc=$?
+      tail -3 $OUT/${TAG}_qc_ab_marker.txt; fatal $rc $st ;;
+    hostab)
+      timeout -k 10 600 python -u tools/host_api_ab.py --rounds 3 > $OUT/${TAG}_host_api_ab.txt 2>&1; rc=$?
+      tail -3 $OUT/${TAG}_host_api_ab.txt; fatal $rc $st ;;
     prof)
       cd /tmp && export TMPDIR=/tmp
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_prof -o bench -- \
