@@ -507,6 +507,8 @@ def mempool_bench(dev, n=1 << 20, tx_size=512, cpu_sample=1 << 17, nstreams=2):
            "outputs_identical_across_streams": all(bool(torch.equal(outs[0], o)) for o in outs[1:]),
            "honest_all_accepted": bool((f[w.accept] & 1).all()),
            "corrupted_all_rejected": bool(not (f[~w.accept] & 1).any())}
+    if cpu_sample <= 0:
+        return res
     lib = _oracle()
     m = min(cpu_sample, n)
     threads, _ = host_cores()

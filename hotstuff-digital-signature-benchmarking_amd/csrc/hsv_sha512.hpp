@@ -61,14 +61,38 @@ HSV_INL void sha512_init(uint64_t h[8]) {
   h[6] = 0x1f83d9abfb41bd6bull; h[7] = 0x5be0cd19137e2179ull;
 }
 
+// Three-input bit functions of the 32-bit halves.  gfx950's v_bitop3_b32
+// evaluates any 3-input function in one instruction (imm = its truth table
+// over A = 0xf0, B = 0xcc, C = 0xaa): x ^ y ^ z is 0x96, maj 0xe8, ch 0xca.
+// Without it the compiler forms v_bfi_b32 for ch but keeps the XOR pairs of
+// the four sigma functions and the majority as two or three instructions.
+// HSV_SHA_BITOP3=1 selects the v_bitop3 form.
+#ifndef HSV_SHA_BITOP3
+#define HSV_SHA_BITOP3 0
+#endif
+template <uint32_t IMM>
+HSV_INL uint64_t sha_bitop3(uint64_t x, uint64_t y, uint64_t z) {
+#if defined(__HIP_DEVICE_COMPILE__) && HSV_SHA_BITOP3
+  const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)x, (uint32_t)y, (uint32_t)z, IMM);
+  const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(x >> 32), (uint32_t)(y >> 32), (uint32_t)(z >> 32), IMM);
+  return ((uint64_t)hi << 32) | lo;
+#else
+  if constexpr (IMM == 0x96) return x ^ y ^ z;
+  if constexpr (IMM == 0xe8) return (x & y) ^ (x & z) ^ (y & z);
+  if constexpr (IMM == 0xca) return (x & y) ^ (~x & z);
+  return 0;
+#endif
+}
+HSV_INL uint64_t sha_xor3(uint64_t x, uint64_t y, uint64_t z) { return sha_bitop3<0x96>(x, y, z); }
+
 // One SHA-512 round with message word wj and round constant kj.
 HSV_INL void sha512_round(uint64_t &a, uint64_t &b, uint64_t &c, uint64_t &d, uint64_t &e, uint64_t &f,
                           uint64_t &g, uint64_t &hh, uint64_t wj, uint64_t kj) {
-  const uint64_t S1 = sha_rotr(e, 14) ^ sha_rotr(e, 18) ^ sha_rotr(e, 41);
-  const uint64_t ch = (e & f) ^ (~e & g);
+  const uint64_t S1 = sha_xor3(sha_rotr(e, 14), sha_rotr(e, 18), sha_rotr(e, 41));
+  const uint64_t ch = sha_bitop3<0xca>(e, f, g);  // (e & f) ^ (~e & g)
   const uint64_t t1 = hh + S1 + ch + kj + wj;
-  const uint64_t S0 = sha_rotr(a, 28) ^ sha_rotr(a, 34) ^ sha_rotr(a, 39);
-  const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
+  const uint64_t S0 = sha_xor3(sha_rotr(a, 28), sha_rotr(a, 34), sha_rotr(a, 39));
+  const uint64_t mj = sha_bitop3<0xe8>(a, b, c);  // (a & b) ^ (a & c) ^ (b & c)
   hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
 }
 
@@ -89,8 +113,8 @@ HSV_INL void sha512_compress(uint64_t h[8], uint64_t w[16]) {
     HSV_UNROLL
     for (int j = 0; j < 16; ++j) {
       const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
-      const uint64_t s0 = sha_rotr(w15, 1) ^ sha_rotr(w15, 8) ^ (w15 >> 7);
-      const uint64_t s1 = sha_rotr(w2, 19) ^ sha_rotr(w2, 61) ^ (w2 >> 6);
+      const uint64_t s0 = sha_xor3(sha_rotr(w15, 1), sha_rotr(w15, 8), w15 >> 7);
+      const uint64_t s1 = sha_xor3(sha_rotr(w2, 19), sha_rotr(w2, 61), w2 >> 6);
       const uint64_t wj = w[j] + s0 + w[(j + 9) & 15] + s1;
       w[j] = wj;
       sha512_round(a, b, c, d, e, f, g, hh, wj, kSha512K[blk * 16 + j]);

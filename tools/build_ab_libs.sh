@@ -5,7 +5,7 @@
 set -e
 cd "$(dirname "$0")/../hotstuff-digital-signature-benchmarking_amd"
 while [ $# -ge 2 ]; do
-  make -j8 BUILD=build_ab_$1 OUT=hsverify/libhsv_$1.so HSV_EXTRA_HIPFLAGS="$2" > /dev/null
+  make -j8 BUILD=build_ab_$1 OUT=hsverify/libhsv_$1.so OUT_TEST= HSV_EXTRA_HIPFLAGS="$2" > /dev/null
   shift 2
 done
 ls -la hsverify/libhsv_*.so

@@ -39,6 +39,10 @@ for k, v in q.items():
     hostab)
       timeout -k 10 600 python -u tools/host_api_ab.py --rounds 3 > $OUT/${TAG}_host_api_ab.txt 2>&1; rc=$?
       tail -3 $OUT/${TAG}_host_api_ab.txt; fatal $rc $st ;;
+    memab)
+      timeout -k 10 600 python -u tools/mempool_ab.py --rounds 3 libhsv.so libhsv_b3.so \
+        > $OUT/${TAG}_mempool_ab_bitop3.txt 2>&1; rc=$?
+      tail -3 $OUT/${TAG}_mempool_ab_bitop3.txt; fatal $rc $st ;;
     prof)
       cd /tmp && export TMPDIR=/tmp
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_prof -o bench -- \
