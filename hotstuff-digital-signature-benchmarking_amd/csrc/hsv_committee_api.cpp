@@ -116,12 +116,16 @@ int committee_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t
       return v ? (size_t)std::atoll(v) : kZeroCopyMax;
     }();
     const bool zero_copy = k <= zc_max && hipHostGetDevicePointer(&hd, h, 0) == hipSuccess && hd;
-    // HSV_QC_SYNC=marker (measurement switch): the zero-copy latency form marks
-    // each block done in pinned memory and the host spins on the markers
-    // instead of hipStreamSynchronize (see the kernel)
+    // The zero-copy latency form marks each block done in pinned memory and the
+    // host spins on the markers instead of hipStreamSynchronize (see the
+    // kernel): the flags are final once every block has released them, and
+    // the kernel's completion signal comes several microseconds later.  Same
+    // box, alternating processes (profiles/r04b_qc_ab_marker.txt): C1
+    // 0.0444 -> 0.0394 ms, C3 0.0587 -> 0.0559 ms, one verify_strict 0.0443 ->
+    // 0.0395 ms.  HSV_QC_SYNC=stream (measurement switch) restores the sync.
     static const bool marker_sync = [] {
       const char *v = std::getenv("HSV_QC_SYNC");
-      return v && std::strcmp(v, "marker") == 0;
+      return !(v && std::strcmp(v, "stream") == 0);
     }();
     const uint32_t nmark = zero_copy && marker_sync ? hsv_comb_marker_blocks((uint32_t)k) : 0u;
     volatile uint32_t *marks = reinterpret_cast<volatile uint32_t *>(h + done_off);

@@ -522,11 +522,19 @@ hsv_verify_hp_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const u
 // packing) the wave sets ctr->pad (abort), every wave leaves at its next
 // batch, and fault[2] tells the host the launch did not finish -- an error,
 // never a verdict and never a hang.
+// The poll is a RELAXED system-scope load: an acquire at system scope would
+// invalidate the XCD's L2 (buffer_inv sc0 sc1) at every batch, evicting the
+// B comb and the other waves' tables -- the first version read 12.1-13.1 ms
+// per 2^20 against 9.4 for the resident launch (profiles/r04b_host_api_ab.txt).
+// No acquire is needed: the records and the flag live in coherent (uncached,
+// fine-grained) pinned memory, the host publishes a piece only after its
+// streaming stores' fence, and the wave issues its record loads after the
+// flag's value decided the branch, at addresses it has not read before.
 __device__ __forceinline__ bool stream_piece_ready(const uint32_t *ready, uint32_t piece, HcCounters *ctr,
                                                    uint32_t max_polls) {
   for (uint32_t i = 0;; ++i) {
     const uint32_t v = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(ready + piece, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
+        __hip_atomic_load(ready + piece, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     if (v != 0u) return true;
     const uint32_t ab =
         __builtin_amdgcn_readfirstlane(__hip_atomic_load(&ctr->pad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -566,14 +574,35 @@ hsv_verify_stream_kernel(const uint8_t *__restrict__ recs, uint32_t rec_bytes, c
     const uint32_t idx = base + lane;
     const bool valid = idx < n;
     const uint32_t li = valid ? idx : n - 1u;
-    uint32_t pkw[8], sigw[16], msgw[8];
-    load_triple(recs, rec_bytes, recs + 32, rec_bytes, shared_msg ? shared_msg : recs + 96,
-                shared_msg ? 0u : rec_bytes, li, pkw, sigw, msgw);
-    uint32_t f;
-    if (prep_scalars<WA>(pkw, sigw, msgw, rec, nslots, lat_bits))
-      f = verify_one_full_comb<WA, false, CB>(pkw, sigw, msgw, comb_b, vt);  // no short lattice pair
-    else
-      f = verify_one_prepped<WA, CB>(pkw, sigw, rec, nslots, rec[18ull * nslots], comb_b, vt);
+    const uint8_t *msg_base = shared_msg ? shared_msg : recs + 96;
+    const uint32_t msg_stride = shared_msg ? 0u : rec_bytes;
+    uint32_t meta;
+    {
+      uint32_t pkw[8], sigw[16], msgw[8];
+      load_triple(recs, rec_bytes, recs + 32, rec_bytes, msg_base, msg_stride, li, pkw, sigw, msgw);
+      (void)prep_scalars<WA>(pkw, sigw, msgw, rec, nslots, lat_bits);
+      meta = rec[18ull * nslots];
+    }
+    // The two paths reload what they need from the records instead of keeping
+    // the prepass's 32 input words live: a divergent if/else runs both regions
+    // in turn, so a value the second region reads stays live through the
+    // first -- here through the whole point pass (round 4 first version: 301
+    // spilled VGPRs against 211 and a 30 % slower launch).
+    uint32_t f = 0;
+    if (!(meta & kPrepFallback)) {
+      uint32_t pkw[8], rw[8];
+      const uint4 *p = reinterpret_cast<const uint4 *>(recs + (uint64_t)li * rec_bytes);
+      const uint4 p0 = p[0], p1 = p[1], r0 = p[2], r1 = p[3];  // pk | R: the record's first 64 bytes
+      pkw[0] = p0.x; pkw[1] = p0.y; pkw[2] = p0.z; pkw[3] = p0.w;
+      pkw[4] = p1.x; pkw[5] = p1.y; pkw[6] = p1.z; pkw[7] = p1.w;
+      rw[0] = r0.x; rw[1] = r0.y; rw[2] = r0.z; rw[3] = r0.w;
+      rw[4] = r1.x; rw[5] = r1.y; rw[6] = r1.z; rw[7] = r1.w;
+      f = verify_one_prepped<WA, CB>(pkw, rw, rec, nslots, meta, comb_b, vt);
+    } else {  // no short lattice pair: the full-length path
+      uint32_t pkw[8], sigw[16], msgw[8];
+      load_triple(recs, rec_bytes, recs + 32, rec_bytes, msg_base, msg_stride, li, pkw, sigw, msgw);
+      f = verify_one_full_comb<WA, false, CB>(pkw, sigw, msgw, comb_b, vt);
+    }
     bad |= ((f & kFault) ? 1u : 0u) | (canary[slot] != nonce ? 2u : 0u);
     if (valid) flags_out[idx] = (uint8_t)f;
   }
