@@ -555,10 +555,17 @@ hsv_verify_stream_kernel(const uint8_t *__restrict__ recs, uint32_t rec_bytes, c
                          uint32_t *__restrict__ canary, uint32_t nonce, uint32_t inject, int lat_bits,
                          uint32_t max_polls, uint32_t *__restrict__ fault) {
   constexpr int kEnt = (1 << (WA - 1)) + 1;
+  // A wave's 64 records, copied from pinned memory in whole 1-KB runs (lane l
+  // reads 16-B chunks l, l + 64, ...): reading them lane by lane was 12 to 16
+  // scattered 16-B PCIe reads per item, request-rate bound.  Each wave owns
+  // its 8 KB of LDS (the waves take batches independently: no block barrier).
+  __shared__ uint4 stage[kBlock / 64][512];
+  uint4 *st = stage[threadIdx.x >> 6];
   const uint32_t slot = blockIdx.x * kBlock + threadIdx.x;
   GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)slot * vt_lane_uint4<WA>(), inject};
   uint32_t *rec = prep_ws + slot;  // word j at rec[j * nslots]: a wave's loads of one word are one access
   const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t rc16 = rec_bytes / 16u;  // 16-B chunks per record (8, or 6 with a shared digest)
   canary[slot] = nonce;
   uint32_t bad = 0;
   for (;;) {
@@ -573,38 +580,78 @@ hsv_verify_stream_kernel(const uint8_t *__restrict__ recs, uint32_t rec_bytes, c
     if (inject == kInjectCanary) canary[slot] = ~nonce;
     const uint32_t idx = base + lane;
     const bool valid = idx < n;
-    const uint32_t li = valid ? idx : n - 1u;
-    const uint8_t *msg_base = shared_msg ? shared_msg : recs + 96;
-    const uint32_t msg_stride = shared_msg ? 0u : rec_bytes;
+    const uint32_t li = (valid ? idx : n - 1u) - base;  // this lane's record in the wave's stage
+    {
+      const uint4 *src = reinterpret_cast<const uint4 *>(recs + (uint64_t)base * rec_bytes);
+      const uint32_t nch = (n - base < 64u ? n - base : 64u) * rc16;
+      for (uint32_t c = lane; c < 64u * rc16; c += 64u)
+        if (c < nch) st[c] = src[c];
+      __builtin_amdgcn_wave_barrier();
+    }
+    const uint4 *my = st + li * rc16;
+    // the digest: the record's last 32 bytes, or the one shared digest
+    auto load_msg = [&](uint32_t msgw[8]) {
+      uint4 m0, m1;
+      if (shared_msg) {
+        const uint4 *g = reinterpret_cast<const uint4 *>(shared_msg);
+        m0 = g[0];
+        m1 = g[1];
+      } else {
+        m0 = my[6];
+        m1 = my[7];
+      }
+      msgw[0] = m0.x; msgw[1] = m0.y; msgw[2] = m0.z; msgw[3] = m0.w;
+      msgw[4] = m1.x; msgw[5] = m1.y; msgw[6] = m1.z; msgw[7] = m1.w;
+    };
     uint32_t meta;
     {
       uint32_t pkw[8], sigw[16], msgw[8];
-      load_triple(recs, rec_bytes, recs + 32, rec_bytes, msg_base, msg_stride, li, pkw, sigw, msgw);
+      load_msg(msgw);
+      HSV_UNROLL
+      for (int q = 0; q < 2; ++q) {
+        const uint4 v = my[q];
+        pkw[4 * q] = v.x; pkw[4 * q + 1] = v.y; pkw[4 * q + 2] = v.z; pkw[4 * q + 3] = v.w;
+      }
+      HSV_UNROLL
+      for (int q = 0; q < 4; ++q) {
+        const uint4 v = my[2 + q];
+        sigw[4 * q] = v.x; sigw[4 * q + 1] = v.y; sigw[4 * q + 2] = v.z; sigw[4 * q + 3] = v.w;
+      }
       (void)prep_scalars<WA>(pkw, sigw, msgw, rec, nslots, lat_bits);
       meta = rec[18ull * nslots];
     }
-    // The two paths reload what they need from the records instead of keeping
-    // the prepass's 32 input words live: a divergent if/else runs both regions
-    // in turn, so a value the second region reads stays live through the
-    // first -- here through the whole point pass (round 4 first version: 301
-    // spilled VGPRs against 211 and a 30 % slower launch).
+    // The two paths read what they need from the stage again instead of
+    // keeping the prepass's input words live: a divergent if/else runs both
+    // regions in turn, so a value the second region reads stays live through
+    // the first -- here through the whole point pass.
     uint32_t f = 0;
     if (!(meta & kPrepFallback)) {
       uint32_t pkw[8], rw[8];
-      const uint4 *p = reinterpret_cast<const uint4 *>(recs + (uint64_t)li * rec_bytes);
-      const uint4 p0 = p[0], p1 = p[1], r0 = p[2], r1 = p[3];  // pk | R: the record's first 64 bytes
-      pkw[0] = p0.x; pkw[1] = p0.y; pkw[2] = p0.z; pkw[3] = p0.w;
-      pkw[4] = p1.x; pkw[5] = p1.y; pkw[6] = p1.z; pkw[7] = p1.w;
-      rw[0] = r0.x; rw[1] = r0.y; rw[2] = r0.z; rw[3] = r0.w;
-      rw[4] = r1.x; rw[5] = r1.y; rw[6] = r1.z; rw[7] = r1.w;
+      HSV_UNROLL
+      for (int q = 0; q < 2; ++q) {
+        const uint4 v = my[q], r = my[2 + q];  // pk | R: the record's first 64 bytes
+        pkw[4 * q] = v.x; pkw[4 * q + 1] = v.y; pkw[4 * q + 2] = v.z; pkw[4 * q + 3] = v.w;
+        rw[4 * q] = r.x; rw[4 * q + 1] = r.y; rw[4 * q + 2] = r.z; rw[4 * q + 3] = r.w;
+      }
       f = verify_one_prepped<WA, CB>(pkw, rw, rec, nslots, meta, comb_b, vt);
     } else {  // no short lattice pair: the full-length path
       uint32_t pkw[8], sigw[16], msgw[8];
-      load_triple(recs, rec_bytes, recs + 32, rec_bytes, msg_base, msg_stride, li, pkw, sigw, msgw);
+      load_msg(msgw);
+      HSV_UNROLL
+      for (int q = 0; q < 2; ++q) {
+        const uint4 v = my[q];
+        pkw[4 * q] = v.x; pkw[4 * q + 1] = v.y; pkw[4 * q + 2] = v.z; pkw[4 * q + 3] = v.w;
+      }
+      HSV_UNROLL
+      for (int q = 0; q < 4; ++q) {
+        const uint4 v = my[2 + q];
+        sigw[4 * q] = v.x; sigw[4 * q + 1] = v.y; sigw[4 * q + 2] = v.z; sigw[4 * q + 3] = v.w;
+      }
       f = verify_one_full_comb<WA, false, CB>(pkw, sigw, msgw, comb_b, vt);
     }
     bad |= ((f & kFault) ? 1u : 0u) | (canary[slot] != nonce ? 2u : 0u);
     if (valid) flags_out[idx] = (uint8_t)f;
+    __builtin_amdgcn_wave_barrier();  // every lane is done with the stage before the next batch's copy
   }
   report_faults(fault, bad);
   if (bad & 4u) fault[2] = 1u;

@@ -19,6 +19,10 @@ for st in $STAGES; do
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
         > $OUT/${TAG}_pytest_gpu.txt 2>&1; rc=$?
       tail -4 $OUT/${TAG}_pytest_gpu.txt; fatal $rc $st ;;
+    pysub)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$PYSUB" \
+        > $OUT/${TAG}_pytest_sub.txt 2>&1; rc=$?
+      tail -3 $OUT/${TAG}_pytest_sub.txt; fatal $rc $st ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/${TAG}_smoke.txt 2>&1; rc=$?
       tail -1 $OUT/${TAG}_smoke.txt; fatal $rc $st ;;
