@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Summarise tools/pmc_r04.sh: per-dispatch counter means per kernel.
 
-  python tools/pmc_r04_summary.py gpurun_out/TAG [out_dir]
-writes out_dir/TAG_pmc_mix.json (C4 point pass + prepass) and
-out_dir/TAG_qc_pmc.json (committee and generic QC kernels at C1 and C3).
+  python tools/pmc_r04_summary.py gpurun_out/TAG [out_prefix]
+writes OUT_pmc_mix.json (C4 point pass + prepass) and OUT_qc_pmc.json
+(committee and generic QC kernels at C1 and C3); out_prefix defaults to
+profiles/TAG.
 """
 import collections
 import csv
@@ -44,11 +45,12 @@ def per_kernel(pass_dir, min_grid=0):
 
 def main():
     root = sys.argv[1].rstrip("/")
-    dst = sys.argv[2] if len(sys.argv) > 2 else "profiles"
     tag = os.path.basename(root)
+    out = sys.argv[2] if len(sys.argv) > 2 else os.path.join("profiles", tag)
     mix = per_kernel(os.path.join(root, "mix"), min_grid=1024)
-    hp = mix.get("hsv_verify_hp_kernel", {})
-    pre = mix.get("hsv_prep_kernel", {})
+    pick = lambda d, name: next((v for k, v in d.items() if k.endswith(name)), {})
+    hp = pick(mix, "hsv_verify_hp_kernel")
+    pre = pick(mix, "hsv_prep_kernel")
     res = {"source": f"tools/pmc_r04.sh ({tag}/mix): rocprofv3 --kernel-trace --pmc over bench.py --steps 3 "
                      "--streams 1, C4 2^20 items per launch", "items": N, "per_dispatch_mean": mix}
     if hp:
@@ -67,7 +69,7 @@ def main():
         }
     if pre:
         res["prepass"] = {"valu_lane_instr_per_verify": pre["SQ_INSTS_VALU"] * 64 / N, "kernel_us_under_pmc": pre["_us"]}
-    with open(os.path.join(dst, f"{tag}_pmc_mix.json"), "w") as f:
+    with open(f"{out}_pmc_mix.json", "w") as f:
         json.dump(res, f, indent=1, default=float)
         f.write("\n")
     qc = {"source": f"tools/pmc_r04.sh ({tag}/qc3, qc667): tools/qc_kernel_profile.py under rocprofv3 --pmc, "
@@ -81,7 +83,7 @@ def main():
     for k in set(a) & set(b):
         diff[k] = {c: b[k][c] - a[k][c] for c in a[k] if c in b[k] and not c.startswith("_dispatches")}
     qc["c3_minus_c1"] = diff
-    with open(os.path.join(dst, f"{tag}_qc_pmc.json"), "w") as f:
+    with open(f"{out}_qc_pmc.json", "w") as f:
         json.dump(qc, f, indent=1, default=float)
         f.write("\n")
     print(json.dumps({"point_pass": res.get("point_pass"), "c3_minus_c1": diff}, indent=1, default=float))
