@@ -851,12 +851,16 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
   Slot &s = lease.slot();
   call_mark(HSV_MARK_SLOT);
   const size_t pchunk = pipe_chunk();
-  // HSV_HOST_PIPE=chunked: round 3's copy pipeline instead (measurement switch)
-  static const bool chunked = [] {
+  // HSV_HOST_PIPE=streamed: the one-launch streamed form (run_streamed) instead
+  // of the chunked copy pipeline (measurement switch).  Measured slower on
+  // MI355X: 11.7 against 9.9 ms per 2^20 (profiles/r04d_host_api_ab.txt),
+  // same VALU instruction count, VALUBusy 0.90 against 0.99 and a lower
+  // clock under the PCIe traffic (profiles/r04e_streampmc_summary.json).
+  static const bool streamed = [] {
     const char *e = std::getenv("HSV_HOST_PIPE");
-    return e && std::strcmp(e, "chunked") == 0;
+    return e && std::strcmp(e, "streamed") == 0;
   }();
-  if (!no_pipe && !chunked && v == 21 && n >= 2 * pchunk) {
+  if (!no_pipe && streamed && v == 21 && n >= 2 * pchunk) {
     for (size_t base = 0; base < n; base += kChunk) {
       const size_t m = std::min(kChunk, n - base);
       rc = run_streamed(s, v, comb_b, pk + base * pk_stride, pk_stride, sig + base * sig_stride, sig_stride,

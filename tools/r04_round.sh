@@ -47,6 +47,12 @@ for k, v in q.items():
       timeout -k 10 600 python -u tools/mempool_ab.py --rounds 3 libhsv.so libhsv_b3.so \
         > $OUT/${TAG}_mempool_ab_bitop3.txt 2>&1; rc=$?
       tail -3 $OUT/${TAG}_mempool_ab_bitop3.txt; fatal $rc $st ;;
+    streampmc)
+      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 180 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU \
+        SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS GRBM_GUI_ACTIVE \
+        --output-format csv -d $OUT/${TAG}_streampmc -o p -- python3 $R/tools/host_api_probe.py \
+        > $OUT/${TAG}_streampmc.txt 2>&1 ); rc=$?
+      tail -2 $OUT/${TAG}_streampmc.txt; fatal $rc $st ;;
     prof)
       cd /tmp && export TMPDIR=/tmp
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_prof -o bench -- \
