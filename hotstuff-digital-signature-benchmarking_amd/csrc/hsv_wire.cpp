@@ -33,7 +33,7 @@ extern "C" {
 int hsv_qc_verify_bincode(const uint8_t *buf, size_t len, size_t *n_votes_out, uint8_t *pks_out) {
   hsvh::CallScope call;  // the host timeline includes the parse
   if (!buf && len) return hsvi_set_error(HSV_ERR_INVALID_ARG, "null buffer");
-  hsvw::QcParsed qc;
+  thread_local hsvw::QcParsed qc;  // keeps its vote buffer from call to call
   std::string err;
   if (!hsvw::parse_qc(buf, len, qc, err)) return parse_error(err);
   if (n_votes_out) *n_votes_out = qc.n;
@@ -45,7 +45,7 @@ int hsv_qc_verify_bincode(const uint8_t *buf, size_t len, size_t *n_votes_out, u
 int hsv_tc_verify_bincode(const uint8_t *buf, size_t len, size_t *n_votes_out, uint8_t *flags_out) {
   hsvh::CallScope call;
   if (!buf && len) return hsvi_set_error(HSV_ERR_INVALID_ARG, "null buffer");
-  hsvw::TcParsed tc;
+  thread_local hsvw::TcParsed tc;
   std::string err;
   if (!hsvw::parse_tc(buf, len, tc, err)) return parse_error(err);
   if (n_votes_out) *n_votes_out = tc.n;

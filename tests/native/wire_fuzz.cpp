@@ -236,6 +236,68 @@ Bytes mutate(const Bytes &in, std::mt19937_64 &rng, const std::vector<Bytes> &po
   return b;
 }
 
+// An independent, character-at-a-time statement of the decoder's rules
+// (base64 0.13 standard: alphabet A-Z a-z 0-9 + /, at most two '=' and only
+// at the end of a whole-quad string, no length = 1 mod 4, zero trailing
+// bits), against which the parser's block decoder (16 characters at a time
+// with SSSE3 on x86-64) is checked verdict for verdict and byte for byte.
+bool ref_b64_decode(const std::string &t, Bytes &out) {
+  auto val = [](unsigned char c) -> int {
+    if (c >= 'A' && c <= 'Z') return c - 'A';
+    if (c >= 'a' && c <= 'z') return c - 'a' + 26;
+    if (c >= '0' && c <= '9') return c - '0' + 52;
+    if (c == '+') return 62;
+    if (c == '/') return 63;
+    return -1;
+  };
+  out.clear();
+  size_t end = t.size();
+  while (end > 0 && t[end - 1] == '=') --end;
+  const size_t pad = t.size() - end;
+  if (pad > 2 || (pad && t.size() % 4 != 0) || end % 4 == 1) return false;
+  uint32_t acc = 0;
+  int bits = 0;
+  for (size_t i = 0; i < end; ++i) {
+    const int v = val((unsigned char)t[i]);
+    if (v < 0) return false;
+    acc = (acc << 6) | (uint32_t)v;
+    bits += 6;
+    if (bits >= 8) {
+      bits -= 8;
+      out.push_back((uint8_t)(acc >> bits));
+      acc &= (1u << bits) - 1u;
+    }
+  }
+  return acc == 0;
+}
+
+void fuzz_base64_differential(std::mt19937_64 &rng, long iters) {
+  static const char *alpha = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  static const uint8_t odd[] = {'=', '-', '_', ' ', '\n', 0, 0x80, 0xff, '!', '@', '[', '`', '{', ':', '?', '*', '.'};
+  Bytes got, want;
+  for (long i = 0; i < iters; ++i) {
+    std::string t;
+    if (rng() % 2) {  // a canonical encoding (often a key's 44 characters), sometimes with one byte changed
+      Bytes raw(rng() % 4 ? 32 : rng() % 80);
+      for (auto &x : raw) x = (uint8_t)rng();
+      t = b64_encode(raw.data(), raw.size());
+      if (!t.empty() && rng() % 3 == 0) {
+        const size_t at = rng() % t.size();
+        t[at] = rng() % 2 ? (char)odd[rng() % sizeof(odd)] : alpha[rng() % 64];
+      }
+    } else {  // random alphabet strings up to 100 characters, some odd bytes, some padding
+      t.resize(rng() % 101);
+      for (auto &c : t) c = rng() % 40 ? alpha[rng() % 64] : (char)odd[rng() % sizeof(odd)];
+      if (!t.empty() && rng() % 4 == 0) t.back() = '=';
+      if (t.size() > 1 && rng() % 8 == 0) t[t.size() - 2] = '=';
+    }
+    const bool ok = hsvw::b64_decode(reinterpret_cast<const uint8_t *>(t.data()), t.size(), got);
+    const bool ok_ref = ref_b64_decode(t, want);
+    CHECK(ok == ok_ref, "base64 verdict %d against %d for a %zu-character string", ok, ok_ref, t.size());
+    if (ok && ok_ref) CHECK(got == want, "base64 bytes differ for a %zu-character string", t.size());
+  }
+}
+
 void fuzz_base64(std::mt19937_64 &rng, long iters) {
   static const char *sym = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/=-_ \n";
   std::vector<uint8_t> out;
@@ -274,6 +336,7 @@ int main(int argc, char **argv) {
   pool.push_back(Bytes());
   for (long i = 0; i < iters; ++i) parse_any(mutate(pool[rng() % pool.size()], rng, pool));
   fuzz_base64(rng, iters / 10);
+  fuzz_base64_differential(rng, iters);
   if (failures) {
     std::fprintf(stderr, "%d check(s) failed\n", failures);
     return 1;
