@@ -15,6 +15,7 @@
 //                          the additions, R decompressed by a second wave.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "hsv_comb.hpp"
@@ -161,14 +162,55 @@ constexpr bool kHashWave = HSV_COMB_HASH_WAVE != 0;
 constexpr uint32_t kHashWaveIdx = 1 + kFusedRWaves;
 constexpr int kFusedThreads = 64 * (1 + kFusedRWaves + (kHashWave ? 1 : 0));
 
+#ifdef HSV_QC_WAVE_CLOCKS
+// Measurement builds only (tools/qc_wave_clocks.py): lane 0 of every wave
+// stamps the 100 MHz constant clock at fixed points of its path -- 0 entry,
+// 1 past the entry barrier, 2 its own work done (comb: the s half), 3 the
+// comb wave past the k handover, 4 at the final barrier, 5 exit; slot 6 the
+// wave's place (XCC_ID << 32 | HW_ID: SIMD, CU, SH, SE), 7 / 8 the shader
+// clock (s_memtime) at entry / exit, so the tool can tell a slower clock from
+// shared SIMDs.
+constexpr uint32_t kQcClkWaves = 4096;
+constexpr int kQcClkSlots = 9;
+__device__ uint64_t g_qc_clk[kQcClkWaves][kQcClkSlots];
+#define HSV_QC_CLK(slot)                                                       \
+  do {                                                                         \
+    const uint32_t wi_ = blockIdx.x * (uint32_t)(kFusedThreads / 64) + wave;   \
+    if (lane == 0u && wi_ < kQcClkWaves) {                                     \
+      g_qc_clk[wi_][slot] = wall_clock64();                                    \
+      if (slot == 0) {                                                         \
+        g_qc_clk[wi_][7] = clock64();                                          \
+        g_qc_clk[wi_][6] = ((uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32) | \
+                           (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4); \
+      }                                                                        \
+      if (slot == 5) g_qc_clk[wi_][8] = clock64();                             \
+    }                                                                          \
+  } while (0)
+#else
+#define HSV_QC_CLK(slot) \
+  do {                   \
+  } while (0)
+#endif
+
+// The block's inputs are read once into LDS (HSV_COMB_STAGE_INPUTS, default
+// 1): on the zero-copy latency path the key indices, signatures and digests
+// sit in pinned host memory, which the GPU reads uncached over PCIe, so each
+// wave that loads a vote's words pays its own PCIe requests.  Per wave stamps
+// (tools/qc_wave_clocks.py, profiles/r04h_qcclk.txt) put every role of the
+// C3 kernel (167 blocks) 4.4-4.6 us behind C1 (one block) with one wave per
+// SIMD and the shader clock within 4 %: the reads, not the arithmetic, grow
+// with the block count.  0 (measurement builds): every wave reads its own.
+#ifndef HSV_COMB_STAGE_INPUTS
+#define HSV_COMB_STAGE_INPUTS 1
+#endif
+constexpr bool kStageInputs = HSV_COMB_STAGE_INPUTS != 0;
+
 // one vote's words: the key A, the signature (R, s) and the message digest M
-__device__ __forceinline__ void load_vote_words(const uint8_t *__restrict__ pks, uint32_t kk,
-                                                const uint8_t *__restrict__ sig, uint64_t sig_stride,
-                                                const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t i,
-                                                uint32_t pkw[8], uint32_t sigw[16], uint32_t msgw[8]) {
+// (sp / gp: the vote's signature and digest, in global memory or LDS)
+__device__ __forceinline__ void load_vote_words(const uint8_t *__restrict__ pks, uint32_t kk, const uint4 *sp,
+                                                const uint4 *gp, uint32_t pkw[8], uint32_t sigw[16],
+                                                uint32_t msgw[8]) {
   const uint4 *p = reinterpret_cast<const uint4 *>(pks + (uint64_t)kk * 32);
-  const uint4 *sp = reinterpret_cast<const uint4 *>(sig + (uint64_t)i * sig_stride);
-  const uint4 *gp = reinterpret_cast<const uint4 *>(msg + (uint64_t)i * msg_stride);
   const uint4 p0 = p[0], p1 = p[1];
   const uint4 s0 = sp[0], s1 = sp[1], s2 = sp[2], s3 = sp[3];
   const uint4 m0 = gp[0], m1 = gp[1];
@@ -204,12 +246,48 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
                                   uint32_t inject, uint32_t *__restrict__ fault, uint32_t *__restrict__ done) {
   __shared__ uint32_t r_x[kFusedVotes][kFeLimbs], r_y[kFusedVotes][kFeLimbs], r_fl[kFusedVotes];
   __shared__ uint32_t k_rec[kFusedVotes][9], k_ready;
+  __shared__ uint4 in_sig[kStageInputs ? kFusedVotes : 1][4], in_msg[kStageInputs ? kFusedVotes : 1][2];
+  __shared__ uint32_t in_kidx[kStageInputs ? kFusedVotes : 1];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint32_t base = blockIdx.x * kFusedVotes;
-  if constexpr (kHashWave) {
+  HSV_QC_CLK(0);
+  // vote v of the block reads vote min(base + v, m - 1): the last block's
+  // spare slots repeat the batch's last vote and write no flag
+  auto vote_of = [&](uint32_t v) { return base + v < m ? base + v : m - 1u; };
+  if constexpr (kStageInputs) {
+    if (wave == 0u) {  // one 16-byte read per lane: 4 per signature, 2 per digest, then the key indices
+      constexpr uint32_t V = kFusedVotes;
+      for (uint32_t t = lane; t < 7u * V; t += 64u) {
+        if (t < 4u * V) {
+          in_sig[t >> 2][t & 3u] = reinterpret_cast<const uint4 *>(sig + (uint64_t)vote_of(t >> 2) * sig_stride)[t & 3u];
+        } else if (t < 6u * V) {
+          const uint32_t v = (t - 4u * V) >> 1, c = t & 1u;
+          in_msg[v][c] = reinterpret_cast<const uint4 *>(msg + (uint64_t)vote_of(v) * msg_stride)[c];
+        } else {
+          in_kidx[t - 6u * V] = key_idx[vote_of(t - 6u * V)];
+        }
+      }
+    }
+  }
+  if constexpr (kHashWave || kStageInputs) {
     // LDS keeps the last block's flag: cleared before any wave can look
-    if (threadIdx.x == 0) k_ready = 0u;
+    if (kHashWave && threadIdx.x == 0) k_ready = 0u;
     __syncthreads();
+    HSV_QC_CLK(1);
+  }
+  auto vote_sig = [&](uint32_t v) -> const uint4 * {
+    if constexpr (kStageInputs) return in_sig[v];
+    else return reinterpret_cast<const uint4 *>(sig + (uint64_t)vote_of(v) * sig_stride);
+  };
+  auto vote_msg = [&](uint32_t v) -> const uint4 * {
+    if constexpr (kStageInputs) return in_msg[v];
+    else return reinterpret_cast<const uint4 *>(msg + (uint64_t)vote_of(v) * msg_stride);
+  };
+  auto vote_kidx = [&](uint32_t v) -> uint32_t {
+    if constexpr (kStageInputs) return in_kidx[v];
+    else return key_idx[vote_of(v)];
+  };
+  if constexpr (kHashWave) {
     if (wave == kHashWaveIdx) {
       // one lane per vote hashes (lanes 0..kFusedVotes-1); the rest of the
       // wave stays masked off (HSV_COMB_HASH_ALL_LANES: every lane, as the
@@ -222,11 +300,10 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
       const uint32_t vl = lane, g = 0u;
 #endif
       if (hashes) {
-        const uint32_t i = base + vl < m ? base + vl : m - 1u;
-        const uint32_t kidx = key_idx[i];
+        const uint32_t kidx = vote_kidx(vl);
         const uint32_t kk = kidx < nkeys ? kidx : 0u;
         uint32_t pkw[8], sigw[16], msgw[8], h[16], kr[9];
-        load_vote_words(pks, kk, sig, sig_stride, msg, msg_stride, i, pkw, sigw, msgw);
+        load_vote_words(pks, kk, vote_sig(vl), vote_msg(vl), pkw, sigw, msgw);
         sha512_96(sigw, pkw, msgw, h);
         const sc k = sc_reduce512(h);
         recode_add<9, 8, kCombPos>(k.v, 8, kr);
@@ -235,8 +312,11 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
           for (int w = 0; w < 9; ++w) k_rec[vl][w] = kr[w];
         }
       }
+      HSV_QC_CLK(2);
       __hip_atomic_store(&k_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      HSV_QC_CLK(4);
       __syncthreads();
+      HSV_QC_CLK(5);
       return;
     }
   }
@@ -246,8 +326,7 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
     const uint32_t row = lane >> 4;
     const uint32_t vr = (wave - 1u) * kRVotesPerWave + row / kRRows;  // this row's vote in the block
     if (vr < (uint32_t)kFusedVotes) {
-      const uint32_t i = base + vr < m ? base + vr : m - 1u;
-      const uint4 *sp = reinterpret_cast<const uint4 *>(sig + (uint64_t)i * sig_stride);
+      const uint4 *sp = vote_sig(vr);
       const uint4 s0 = sp[0], s1 = sp[1];
       const uint32_t rw[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
       fe rx, ry;
@@ -271,8 +350,7 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
     }
 #else
     if (lane < (uint32_t)kFusedVotes) {
-      const uint32_t i = base + lane < m ? base + lane : m - 1u;
-      const uint4 *sp = reinterpret_cast<const uint4 *>(sig + (uint64_t)i * sig_stride);
+      const uint4 *sp = vote_sig(lane);
       const uint4 s0 = sp[0], s1 = sp[1];
       const uint32_t rw[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
       fe rx, ry;
@@ -286,18 +364,20 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
       r_fl[lane] = r_ok | (small_r << 1);
     }
 #endif
+    HSV_QC_CLK(2);
+    HSV_QC_CLK(4);
     __syncthreads();
+    HSV_QC_CLK(5);
     return;
   }
   const uint32_t vl = lane / kCombLanes, g = lane % kCombLanes;
   const uint32_t i0 = base + vl;
   const bool valid = i0 < m;
-  const uint32_t i = valid ? i0 : m - 1u;
-  const uint32_t kidx = key_idx[i];
+  const uint32_t kidx = vote_kidx(vl);
   const bool kvalid = kidx < nkeys;
   const uint32_t kk = kvalid ? kidx : 0u;
   uint32_t pkw[8], sigw[16], msgw[8];
-  load_vote_words(pks, kk, sig, sig_stride, msg, msg_stride, i, pkw, sigw, msgw);
+  load_vote_words(pks, kk, vote_sig(vl), vote_msg(vl), pkw, sigw, msgw);
   const uint32_t s_ok = sc_is_canonical(sigw + 8);
 #ifdef HSV_TIMING_STUB_QUADPATH  // tools/qc_phase_probe.py only: wrong flags, the R waves' time alone
   ge_ext q = ge_identity();
@@ -318,8 +398,10 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
       q = ge_add_niels<true>(q, select_niels<8>(tpb, (uint32_t)sd & 0xffu));
       sd >>= 8;
     }
+    HSV_QC_CLK(2);
     while (__hip_atomic_load(&k_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
       __builtin_amdgcn_s_sleep(1);
+    HSV_QC_CLK(3);
     uint32_t kr[9];
     HSV_UNROLL
     for (int w = 0; w < 9; ++w) kr[w] = k_rec[vl][w];
@@ -360,6 +442,7 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
   // the self-check of Q needs nothing from the R waves: before the barrier
   uint32_t z_nonzero = 0, sane = 0;
   if constexpr (kRowChecks) sane = ge_is_sane_row(q, z_nonzero);
+  HSV_QC_CLK(4);
   __syncthreads();
   fe rx, ry;
   HSV_UNROLL
@@ -386,6 +469,7 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
   else fb = fault_bit(a_ok, r_ok, q) ? 1u : 0u;
   if (fb | ((rf >> 2) & 1u)) fault[0] = 1u;  // device self-check (hsv_kernels.hip report_faults)
   if (valid && g == 0u) flags_out[i0] = kvalid ? (uint8_t)f : (uint8_t)0;
+  HSV_QC_CLK(5);
   if (done) {
     // completion marker (HSV_QC_SYNC=marker): every wave of the block is past
     // its reads (the R and hash waves before the barrier / k_ready), and this
@@ -531,3 +615,18 @@ extern "C" uint64_t hsv_comb_tmp_bytes(uint32_t nkeys) {
   const uint64_t npad = (nkeys + 63u) / 64u * 64u;
   return npad * (uint64_t)hsv::kCombPos * hsv::kCombEnt * 8ull * 4ull;
 }
+
+#ifdef HSV_QC_WAVE_CLOCKS
+// Measurement builds only: copies the wave stamps of the last latency-form
+// launches (waves x 9 u64: six 100 MHz stamps, place, shader clock) to `out` and clears them; returns the
+// waves per block, or -1 on a HIP error.
+extern "C" __attribute__((visibility("default"))) int hsv_qc_wave_clocks(uint64_t *out, size_t waves) {
+  const size_t n = std::min<size_t>(waves, hsv::kQcClkWaves) * hsv::kQcClkSlots * sizeof(uint64_t);
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(hsv::g_qc_clk), n) != hipSuccess) return -1;
+  void *p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(hsv::g_qc_clk)) != hipSuccess) return -1;
+  if (hipMemset(p, 0, sizeof(hsv::g_qc_clk)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return -1;
+  return hsv::kFusedThreads / 64;
+}
+#endif

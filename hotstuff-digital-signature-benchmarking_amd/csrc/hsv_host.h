@@ -69,6 +69,7 @@ struct Slot {
   // started, so the GPU must not serve them from a cache
   uint8_t *h_stream = nullptr;
   size_t h_stream_cap = 0;
+  size_t pipe_warm_n = 0;  // items of the last completed pipelined call (HSV_PIPE_NOCOPY)
 };
 
 struct DevCtx {

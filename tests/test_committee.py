@@ -65,6 +65,29 @@ def test_qc_verify_batch_through_committee(mods):
         assert c.verify_batch(d, []).is_ok()
 
 
+def test_committee_index_first_member_wins_and_misses(mods):
+    """The member index (an open-addressing table since round 4): every key
+    maps to its first position, a repeated key keeps it, and keys that share
+    the 8-byte probe tag or differ in one bit miss."""
+    committee, _, synth, _ = mods
+    w = synth.qc_votes(1000, seed=3)
+    keys = np.concatenate([w.pk, w.pk[5:6], w.pk[:3]])
+    first = {}
+    for i, k in enumerate(keys):
+        first.setdefault(bytes(k), i)
+    with committee.Committee(keys) as c:
+        for k, i in first.items():
+            assert c.index(k) == i
+        for j in (0, 7, 300):
+            tail = bytearray(w.pk[j])
+            tail[20] ^= 0x40                     # same first 8 bytes (probe tag), different key
+            assert bytes(tail) in first or c.index(bytes(tail)) == -1
+            head = bytearray(w.pk[j])
+            head[0] ^= 1
+            assert bytes(head) in first or c.index(bytes(head)) == -1
+        assert c.index(bytes(32)) in (-1, first.get(bytes(32), -1))
+
+
 def test_invalid_member_index_yields_zero_flags(mods, golden):
     committee, _, _, _ = mods
     with committee.Committee(golden["pk"][:4]) as c:

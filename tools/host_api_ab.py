@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """A/B of the host-buffer call (hsv_verify from numpy arrays at 2^20 items,
 PCIe-inclusive) between environment settings, alternating fresh processes:
-the streamed launch (round 4, default) against round 3's chunked copy
-pipeline (HSV_HOST_PIPE=chunked).  Prints each run's median of 5 calls and
-the median per setting.
+by default the chunked copy pipeline against the same chunk schedule with
+the pack and the copies skipped on repeat calls (HSV_PIPE_NOCOPY=1, its GPU
+time alone); HSV_HOST_PIPE=streamed selects the streamed launch.  Prints each
+run's median of 5 calls and the median per setting.
 
 python tools/host_api_ab.py [--rounds 3] [SETTING ...]   (SETTING: NAME=VALUE,... or "default")
 """
@@ -37,7 +38,7 @@ print(json.dumps({{"ms": float(np.median(ts) * 1e3), "ok": ok, "marks": _testing
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("settings", nargs="*", default=["default", "HSV_HOST_PIPE=chunked"])
+    ap.add_argument("settings", nargs="*", default=["default", "HSV_PIPE_NOCOPY=1"])
     a = ap.parse_args()
     res = {s: [] for s in a.settings}
     for _ in range(a.rounds):
