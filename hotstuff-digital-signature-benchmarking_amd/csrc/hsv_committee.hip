@@ -192,16 +192,18 @@ __device__ uint64_t g_qc_clk[kQcClkWaves][kQcClkSlots];
   } while (0)
 #endif
 
-// The block's inputs are read once into LDS (HSV_COMB_STAGE_INPUTS, default
-// 1): on the zero-copy latency path the key indices, signatures and digests
-// sit in pinned host memory, which the GPU reads uncached over PCIe, so each
-// wave that loads a vote's words pays its own PCIe requests.  Per wave stamps
-// (tools/qc_wave_clocks.py, profiles/r04h_qcclk.txt) put every role of the
-// C3 kernel (167 blocks) 4.4-4.6 us behind C1 (one block) with one wave per
-// SIMD and the shader clock within 4 %: the reads, not the arithmetic, grow
-// with the block count.  0 (measurement builds): every wave reads its own.
+// HSV_COMB_STAGE_INPUTS=1 (measurement builds only): the block's inputs read
+// once into LDS by wave 0 before the entry barrier, instead of each wave
+// reading its own vote words from the pinned staging over PCIe.  Per-wave
+// stamps (tools/qc_wave_clocks.py, profiles/r04h_qcclk.txt) put every role of
+// the C3 kernel (167 blocks) 4.4-4.6 us behind C1 (one block), with one wave
+// per SIMD and the shader clock 4 % lower; staging was to test whether the
+// redundant PCIe reads cause it.  They do not: staged, C3 keeps the same
+// penalty, and the barrier ahead of every wave costs C1 3.5 us
+// (profiles/r04i_qc_ab_stage.txt: C1 / C3 0.0431 / 0.0584 against 0.0396 /
+// 0.0554 ms).
 #ifndef HSV_COMB_STAGE_INPUTS
-#define HSV_COMB_STAGE_INPUTS 1
+#define HSV_COMB_STAGE_INPUTS 0
 #endif
 constexpr bool kStageInputs = HSV_COMB_STAGE_INPUTS != 0;
 
