@@ -166,12 +166,13 @@ constexpr int kFusedThreads = 64 * (1 + kFusedRWaves + (kHashWave ? 1 : 0));
 // Measurement builds only (tools/qc_wave_clocks.py): lane 0 of every wave
 // stamps the 100 MHz constant clock at fixed points of its path -- 0 entry,
 // 1 past the entry barrier, 2 its own work done (comb: the s half), 3 the
-// comb wave past the k handover, 4 at the final barrier, 5 exit; slot 6 the
+// comb wave past the k handover (R and hash waves: their first loads landed), 4 at the final
+// barrier, 5 exit; slot 6 the
 // wave's place (XCC_ID << 32 | HW_ID: SIMD, CU, SH, SE), 7 / 8 the shader
 // clock (s_memtime) at entry / exit, so the tool can tell a slower clock from
 // shared SIMDs.
 constexpr uint32_t kQcClkWaves = 4096;
-constexpr int kQcClkSlots = 9;
+constexpr int kQcClkSlots = 10;  // slot 9: HSV_QC_WAVE_CLOCKS_TWICE
 __device__ uint64_t g_qc_clk[kQcClkWaves][kQcClkSlots];
 #define HSV_QC_CLK(slot)                                                       \
   do {                                                                         \
@@ -186,9 +187,18 @@ __device__ uint64_t g_qc_clk[kQcClkWaves][kQcClkSlots];
       if (slot == 5) g_qc_clk[wi_][8] = clock64();                             \
     }                                                                          \
   } while (0)
+// slot 3 of the R and hash waves: once the wave's first loads have landed
+#define HSV_QC_CLK_LOADED(slot)        \
+  do {                                 \
+    __builtin_amdgcn_s_waitcnt(0);     \
+    HSV_QC_CLK(slot);                  \
+  } while (0)
 #else
 #define HSV_QC_CLK(slot) \
   do {                   \
+  } while (0)
+#define HSV_QC_CLK_LOADED(slot) \
+  do {                          \
   } while (0)
 #endif
 
@@ -306,6 +316,7 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
         const uint32_t kk = kidx < nkeys ? kidx : 0u;
         uint32_t pkw[8], sigw[16], msgw[8], h[16], kr[9];
         load_vote_words(pks, kk, vote_sig(vl), vote_msg(vl), pkw, sigw, msgw);
+        HSV_QC_CLK_LOADED(3);
         sha512_96(sigw, pkw, msgw, h);
         const sc k = sc_reduce512(h);
         recode_add<9, 8, kCombPos>(k.v, 8, kr);
@@ -330,6 +341,7 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
     if (vr < (uint32_t)kFusedVotes) {
       const uint4 *sp = vote_sig(vr);
       const uint4 s0 = sp[0], s1 = sp[1];
+      HSV_QC_CLK_LOADED(3);
       const uint32_t rw[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
       fe rx, ry;
 #ifdef HSV_TIMING_STUB_RWAVE  // tools/qc_phase_probe.py only: wrong flags, the quad path's time alone
@@ -338,6 +350,16 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
       const uint32_t r_ok = 1u, small = 0u, nc = 0u;
 #else
       uint32_t small, nc = 0;
+#ifdef HSV_QC_WAVE_CLOCKS_TWICE  // measurement builds only: a second, warm-cache decompression
+      {
+        fe x2, y2;
+        uint32_t small2, nc2 = 0;
+        const uint32_t ok2 = ge_decompress_row(rw, x2, y2, small2, nc2, L);
+        HSV_QC_CLK(9);
+        nc |= (ok2 ^ ok2) | (x2.v[0] & 0u) | (small2 & 0u);  // keeps the first pass alive
+        asm volatile("" ::"v"(x2.v[0]), "v"(y2.v[0]), "v"(ok2), "v"(nc2));
+      }
+#endif
       const uint32_t r_ok = ge_decompress_row(rw, rx, ry, small, nc, L);
 #endif
       const uint32_t small_r = r_ok & small;
@@ -620,7 +642,8 @@ extern "C" uint64_t hsv_comb_tmp_bytes(uint32_t nkeys) {
 
 #ifdef HSV_QC_WAVE_CLOCKS
 // Measurement builds only: copies the wave stamps of the last latency-form
-// launches (waves x 9 u64: six 100 MHz stamps, place, shader clock) to `out` and clears them; returns the
+// launches (waves x 10 u64: six 100 MHz stamps, place, shader clock, one
+// spare stamp) to `out` and clears them; returns the
 // waves per block, or -1 on a HIP error.
 extern "C" __attribute__((visibility("default"))) int hsv_qc_wave_clocks(uint64_t *out, size_t waves) {
   const size_t n = std::min<size_t>(waves, hsv::kQcClkWaves) * hsv::kQcClkSlots * sizeof(uint64_t);

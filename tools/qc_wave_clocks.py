@@ -6,8 +6,11 @@ tools/build_ab_libs.sh qcclk "-DHSV_QC_WAVE_CLOCKS").
 Each wave's lane 0 stamps the 100 MHz constant clock (s_memrealtime) at
 0 entry, 1 past the entry barrier, 2 its own work done (comb wave: the s
 half; R waves: the decompression; hash wave: the hash), 3 the comb wave past
-the k handover, 4 at the final barrier, 5 exit; plus its place (XCC, SE, SH,
-CU, SIMD) and the shader clock at entry and exit.  For the drop-in C1 (3 votes,
+the k handover (R and hash waves: their first loads landed), 4 at the final
+barrier, 5 exit; plus its place (XCC, SE, SH,
+CU, SIMD) and the shader clock at entry and exit.  A -DHSV_QC_WAVE_CLOCKS_TWICE
+build decompresses R twice (slot 9 between the passes): the second pass runs
+with the code already in the instruction cache.  For the drop-in C1 (3 votes,
 1 block) and C3 (667 votes, 167 blocks) calls this reports, as medians over the
 reps: the spread of wave entries (dispatch ramp), every role's phase lengths,
 and the kernel span (first entry to last exit).
@@ -26,7 +29,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "hotstuff-digital-signature-benchmarking_amd"))
 
 TICK_US = 0.01  # 100 MHz
-SLOTS = 9
+SLOTS = 10
 
 
 def analyse(clk, nblocks, wpb):
@@ -58,6 +61,14 @@ def analyse(clk, nblocks, wpb):
         "comb_tail_us": float(np.median(comb[:, 5] - np.maximum(r[:, :, 4].max(axis=1), comb[:, 4]))) * TICK_US,
         "r_decompress_us": float(np.median(r[:, :, 2] - r[:, :, 0])) * TICK_US,
         "hash_us": float(np.median(hashw[:, 2] - hashw[:, 1])) * TICK_US,
+        "r_load_us": float(np.median(r[:, :, 3] - r[:, :, 0])) * TICK_US,
+        "r_alu_us": float(np.median(r[:, :, 2] - r[:, :, 3])) * TICK_US,
+        "r_first_pass_us": float(np.median(raw[:, 1:wpb - 1, 9].astype(np.int64) - t0 - r[:, :, 3])) * TICK_US
+        if raw[:, 1:wpb - 1, 9].any() else None,
+        "r_second_pass_us": float(np.median(r[:, :, 2] - (raw[:, 1:wpb - 1, 9].astype(np.int64) - t0))) * TICK_US
+        if raw[:, 1:wpb - 1, 9].any() else None,
+        "hash_load_us": float(np.median(hashw[:, 3] - hashw[:, 1])) * TICK_US,
+        "hash_alu_us": float(np.median(hashw[:, 2] - hashw[:, 3])) * TICK_US,
         "comb_life_us": float(np.median(comb[:, 5] - comb[:, 0])) * TICK_US,
         "comb_life_max_us": float((comb[:, 5] - comb[:, 0]).max()) * TICK_US,
         "last_exit_block": int(c[:, 0, 5].argmax()),
@@ -103,7 +114,8 @@ def main():
         keys = rows[0].keys()
         res[f"n{committee}_votes{w.n}"] = {
             "blocks": nblocks, "waves_per_block": wpb,
-            **{k: round(float(np.median([r[k] for r in rows])), 3) for k in keys},
+            **{k: (round(float(np.median([r[k] for r in rows])), 3) if rows[0][k] is not None else None)
+               for k in keys},
             "span_us_p90": round(float(np.percentile([r["span_us"] for r in rows], 90)), 3),
         }
         print(json.dumps({f"n{committee}_votes{w.n}": res[f"n{committee}_votes{w.n}"]}), flush=True)
