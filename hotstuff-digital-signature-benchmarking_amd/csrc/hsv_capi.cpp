@@ -243,12 +243,13 @@ int slot_stream2(Slot &s) {
   return e == hipSuccess ? HSV_OK : hip_fail("hipStreamCreate", e);
 }
 
-int slot_pipeline(Slot &s) {
+int slot_pipeline(Slot &s, int compute_streams) {
   int rc = slot_stream2(s);
   if (rc != HSV_OK) return rc;
   hipError_t e = hipSuccess;
   if (!s.copy) e = pipe_stream_create(&s.copy);
-  for (int i = 0; i < 4 && e == hipSuccess; ++i)
+  if (e == hipSuccess && compute_streams > 2 && !s.stream3) e = pipe_stream_create(&s.stream3);
+  for (int i = 0; i < 5 && e == hipSuccess; ++i)
     if (!s.ev[i]) e = hipEventCreateWithFlags(&s.ev[i], hipEventDisableTiming);
   return e == hipSuccess ? HSV_OK : hip_fail("creating the pipeline streams and events", e);
 }
@@ -577,20 +578,25 @@ size_t pipe_chunk() {  // HSV_PIPE_CHUNK_LOG2 (14..22): measurement switch
   return c;
 }
 
-// The slot's two launch workspaces (one per compute stream), grown to at
-// least `need` bytes each; kept across calls, so no launch allocates.
-int slot_workspaces(Slot &s, size_t need) {
-  if (need <= s.ws_cap) return HSV_OK;
+// The slot's launch workspaces (one per compute stream): the first `count`
+// exist and hold at least `need` bytes each; kept across calls, so no launch
+// allocates.
+int slot_workspaces(Slot &s, size_t need, int count) {
+  int have = 0;
+  while (have < 3 && s.d_ws[have]) ++have;
+  if (need <= s.ws_cap && count <= have) return HSV_OK;
+  const size_t cap = std::max(need, s.ws_cap);
+  const int n = std::max(count, have);
   for (uint8_t *&w : s.d_ws) {
     if (w) (void)hipFree(w);
     w = nullptr;
   }
   s.ws_cap = 0;
-  for (uint8_t *&w : s.d_ws) {
-    const hipError_t ea = hipMalloc(&w, need);
+  for (int i = 0; i < n; ++i) {
+    const hipError_t ea = hipMalloc(&s.d_ws[i], cap);
     if (ea != hipSuccess) return hip_fail("allocating the launch workspaces", ea);
   }
-  s.ws_cap = need;
+  s.ws_cap = cap;
   return HSV_OK;
 }
 
@@ -672,19 +678,29 @@ int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, siz
   const size_t h_fault = h_flag + round_up(n, kAlign);
   const size_t h_total = h_fault + kAlign;
   int rc = slot_prepare(s, d_total, h_total);
-  if (rc == HSV_OK) rc = slot_pipeline(s);
+  if (rc != HSV_OK) return rc;
+  // Launches alternate over two compute streams.  A chunk's memset and
+  // prepass (~0.1 ms) run beside only the other stream's point pass, a 2^17
+  // grid that fills two thirds of the GPU's lanes (rocprofv3 kernel trace,
+  // profiles/r04l_host_kernel_trace_summary.txt); a third stream
+  // (HSV_PIPE_STREAMS=3, measurement switch) fills that gap but measured
+  // slower: 10.27 against 10.04 ms per 2^20, and 9.62 against 9.32 ms with
+  // the copies skipped (profiles/r04m_host_streams_ab.txt, r04i_host_nocopy.txt).
+  static const int nstreams = env_int("HSV_PIPE_STREAMS", 2) == 3 ? 3 : 2;
+  rc = slot_pipeline(s, nstreams);
   if (rc != HSV_OK) return rc;
   // one launch workspace per compute stream, kept by the slot: a pool
   // allocation per launch made the enqueue of each chunk wait ~1 ms for an
   // earlier chunk (tools/host_api_probe.py marks)
-  rc = slot_workspaces(s, hsv_launch_ws_bytes(v, (uint32_t)maxm));
+  rc = slot_workspaces(s, hsv_launch_ws_bytes(v, (uint32_t)maxm), nstreams);
   if (rc != HSV_OK) return rc;
-  hipStream_t comp[2] = {s.stream, s.stream2};
+  hipStream_t comp[3] = {s.stream, s.stream2, s.stream3};
   hipEvent_t staged[2] = {s.ev[0], s.ev[1]};
   auto drain = [&](int code) -> int {
     (void)hipStreamSynchronize(s.copy);
     (void)hipStreamSynchronize(s.stream);
     (void)hipStreamSynchronize(s.stream2);
+    if (s.stream3) (void)hipStreamSynchronize(s.stream3);
     return code;
   };
   uint8_t *d = s.d_buf;
@@ -732,21 +748,24 @@ int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, siz
       if (e != hipSuccess) return drain(hip_fail("hipMemcpyAsync H2D", e));
     }
     call_chunk_mark();
+    const int cs = (int)(k % (size_t)nstreams);  // this chunk's compute stream and workspace
     e = hipEventRecord(staged[b], s.copy);
-    if (e == hipSuccess) e = hipStreamWaitEvent(comp[b], staged[b], 0);
+    if (e == hipSuccess) e = hipStreamWaitEvent(comp[cs], staged[b], 0);
     if (e != hipSuccess) return drain(hip_fail("staging a chunk", e));
     used[b] = true;
     call_chunk_mark();
     t_h2d_bytes += m * rec;
     e = hsv_launch_verify_ws(v, dc, rec, dc + 32, rec, msg_stride ? dc + 96 : d + d_dig, msg_stride ? rec : 0,
                              (uint32_t)m, d + d_flag + base, nullptr, comb_b,
-                             reinterpret_cast<uint32_t *>(d + d_fault), s.d_ws[b], s.ws_cap, comp[b]);
+                             reinterpret_cast<uint32_t *>(d + d_fault), s.d_ws[cs], s.ws_cap, comp[cs]);
     if (e != hipSuccess) return drain(hip_fail("verify kernel launch", e));
     call_chunk_mark();
   }
-  // join: the flags come back once both compute streams are done
-  e = hipEventRecord(s.ev[3], s.stream2);
-  if (e == hipSuccess) e = hipStreamWaitEvent(s.stream, s.ev[3], 0);
+  // join: the flags come back once every compute stream is done
+  for (int j = 1; j < nstreams && e == hipSuccess; ++j) {
+    e = hipEventRecord(s.ev[2 + j], comp[j]);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s.stream, s.ev[2 + j], 0);
+  }
   if (e == hipSuccess)
     e = hipMemcpyAsync(s.h_buf + h_flag, d + d_flag, d_total - d_flag, hipMemcpyDeviceToHost, s.stream);
   if (e != hipSuccess) return drain(hip_fail("hipMemcpyAsync D2H", e));
@@ -798,7 +817,7 @@ int run_streamed(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, size
     if (e != hipSuccess) return hip_fail("hipHostMalloc (streamed staging)", e);
     s.h_stream_cap = cap;
   }
-  rc = slot_workspaces(s, hsv_launch_stream_ws_bytes((uint32_t)n));
+  rc = slot_workspaces(s, hsv_launch_stream_ws_bytes((uint32_t)n), 1);
   if (rc != HSV_OK) return rc;
   void *hd = nullptr;
   e = hipHostGetDevicePointer(&hd, s.h_stream, 0);
@@ -935,7 +954,7 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
       // mapping, so no copy launches sit on the latency path
       uint8_t *dh = static_cast<uint8_t *>(hd);
       // the launch workspace the slot keeps: no pool allocation on the latency path
-      rc = slot_workspaces(s, hsv_launch_ws_bytes(v, (uint32_t)m));
+      rc = slot_workspaces(s, hsv_launch_ws_bytes(v, (uint32_t)m), 1);
       if (rc != HSV_OK) return rc;
       e = hsv_launch_verify_ws(v, dh + pk_off, 32, dh + sig_off, 64, dh + msg_off, msg_stride ? 32 : 0, (uint32_t)m,
                                dh + flag_off, nullptr, comb_b, reinterpret_cast<uint32_t *>(dh + fault_off), s.d_ws[0],
@@ -1051,6 +1070,7 @@ void hsv_shutdown(void) {
     for (auto &sp : c->slots) {
       if (sp->stream) (void)hipStreamSynchronize(sp->stream);
       if (sp->stream2) (void)hipStreamSynchronize(sp->stream2);
+      if (sp->stream3) (void)hipStreamSynchronize(sp->stream3);
       if (sp->copy) (void)hipStreamSynchronize(sp->copy);
     }
     for (hipStream_t st : c->side_all) (void)hipStreamSynchronize(st);
@@ -1068,6 +1088,7 @@ void hsv_shutdown(void) {
       Slot &s = *sp;
       if (s.stream) (void)hipStreamDestroy(s.stream);
       if (s.stream2) (void)hipStreamDestroy(s.stream2);
+      if (s.stream3) (void)hipStreamDestroy(s.stream3);
       if (s.copy) (void)hipStreamDestroy(s.copy);
       for (hipEvent_t &ev : s.ev) {
         if (ev) (void)hipEventDestroy(ev);
@@ -1084,7 +1105,7 @@ void hsv_shutdown(void) {
       if (s.h_stream) (void)hipHostFree(s.h_stream);
       s.h_stream = nullptr;
       s.h_stream_cap = 0;
-      s.stream = s.stream2 = nullptr;
+      s.stream = s.stream2 = s.stream3 = nullptr;
       s.d_buf = s.h_buf = nullptr;
       s.d_cap = s.h_cap = 0;
     }

@@ -55,10 +55,11 @@ inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 struct Slot {
   std::mutex mu;
   hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;  // second compute stream of large host batches
+  hipStream_t stream2 = nullptr;  // second and third compute streams of large host batches
+  hipStream_t stream3 = nullptr;
   hipStream_t copy = nullptr;     // host-to-device stream of large host batches
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // staged[2], joined[2] (run_pipelined)
-  uint8_t *d_ws[2] = {nullptr, nullptr};  // launch workspaces of the two compute streams (run_pipelined)
+  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // staged[2], unused, joined[2] (run_pipelined)
+  uint8_t *d_ws[3] = {nullptr, nullptr, nullptr};  // launch workspaces of the compute streams (run_pipelined)
   size_t ws_cap = 0;
   uint8_t *d_buf = nullptr;
   size_t d_cap = 0;
@@ -130,7 +131,7 @@ class SlotLease {
 // Stream and buffers of a slot (current device must be c.device).
 int slot_prepare(Slot &s, size_t dev_bytes, size_t host_bytes);
 int slot_stream2(Slot &s);
-int slot_pipeline(Slot &s);  // stream2, the copy stream and the events of run_pipelined
+int slot_pipeline(Slot &s, int compute_streams);  // stream2 (stream3), the copy stream, the events of run_pipelined
 
 // Device self-check words (hsv_kernels.hip report_faults): two words per
 // launch, zeroed before it; non-zero after it -> HSV_ERR_DEVICE_FAULT.
