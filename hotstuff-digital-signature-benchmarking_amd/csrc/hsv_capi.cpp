@@ -729,9 +729,13 @@ int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, siz
     call_chunk_mark();
     uint8_t *dc = d + base * rec;  // chunk k's records in HBM
     // Items as records pk | R || s (| digest), so any item range is one
-    // contiguous copy.  A full-size first chunk (HSV_PIPE_FIRST_LOG2) goes in
-    // four pieces, each copied as soon as it is packed.
-    const size_t pieces = nocopy ? 0 : k == 0 && m >= pipe_chunk() ? 4 : 1;
+    // contiguous copy.  HSV_PIPE_FIRST_PIECES (1..8, measurement switch)
+    // sends the first chunk in pieces, each copied as soon as it is packed;
+    // four pieces measured no faster than one (10.59 against 10.52 ms per
+    // 2^20, profiles/r04o_host_pieces_ab.txt): the pool's extra hand-offs
+    // cost what the overlap saves.
+    static const size_t first_pieces = (size_t)std::max(1, std::min(8, env_int("HSV_PIPE_FIRST_PIECES", 1)));
+    const size_t pieces = nocopy ? 0 : k == 0 && m >= first_pieces * 4096 ? first_pieces : 1;
     for (size_t q = 0; q < pieces; ++q) {
       const size_t lo0 = m * q / pieces, hi0 = m * (q + 1) / pieces;
       const auto t_pack = std::chrono::steady_clock::now();
