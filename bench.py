@@ -461,7 +461,7 @@ def qc_cpu(reps=5):
     return res
 
 
-def mempool_bench(dev, n=1 << 20, tx_size=512, cpu_sample=1 << 17, nstreams=2):
+def mempool_bench(dev, n=1 << 20, tx_size=512, cpu_sample=1 << 17, nstreams=2, streams=None):
     """Mempool transactions: n client transactions of
     tx_size bytes (the reference benchmark's default, benchmark/fabfile.py),
     resident in HBM; one step = digest records + verification
@@ -471,18 +471,28 @@ def mempool_bench(dev, n=1 << 20, tx_size=512, cpu_sample=1 << 17, nstreams=2):
     from hsverify import mempool, synth
     w = synth.transactions(n, tx_size=tx_size, seed=9)
     d = torch.from_numpy(w.txs.reshape(-1)).to(dev)
-    stream = torch.cuda.current_stream(dev)
-    # consecutive batches alternate over nstreams streams, as for the C4 line
-    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(max(1, nstreams) - 1)]
+    # Consecutive batches alternate over the C4 line's streams when given
+    # (main passes them), else over nstreams streams of their own.  Streams
+    # created later can land on a hardware queue an earlier stream already
+    # uses; two batches on one queue then run back to back instead of the
+    # next one starting in the previous grid's end.  In the round-4 trace the
+    # mempool line's three new streams used two queues, and a step took 10.0
+    # against 9.2 ms for the C4 line's three (profiles/r04p_mempool_trace.txt).
+    if streams is None:
+        stream = torch.cuda.current_stream(dev)
+        streams = [stream] + [torch.cuda.Stream(dev) for _ in range(max(1, nstreams) - 1)]
+    else:
+        streams = list(streams)
+        stream = streams[0]
     outs = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in streams]
     flags = outs[0]
     for j, s in enumerate(streams):
         mempool.verify_transactions_device(d, None, tx_size=tx_size, n=n, flags=outs[j], stream=s.cuda_stream)
     torch.cuda.synchronize(dev)
-    steps = 6
+    steps = 10  # as many batches per round as the C4 line's default --steps
     rounds_ms = []
     # three timed rounds of `steps` batches, the median reported: one round
-    # is ~60 ms, and one disturbed round once read 15.0 against 9.6-9.8 ms
+    # is ~100 ms, and one disturbed round once read 15.0 against 9.6-9.8 ms
     # (profiles/r03zz5_bench.json against r03zz6)
     for _ in range(3):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -844,7 +854,7 @@ def main():
         out["tc_latency"] = tc_latency(a.qc_reps, auto=True)
         _lib.load().hsv_set_auto_committee(1)
         out["committee_cache"] = committee_bench(a.qc_reps, dev)
-        out["mempool_tx"] = mempool_bench(dev, nstreams=nst)
+        out["mempool_tx"] = mempool_bench(dev, nstreams=nst, streams=streams)
         if world == 1 and not a.no_cpu_baseline:
             out["qc_cpu_baseline"] = qc_cpu()
     print(json.dumps(out), flush=True)
