@@ -159,6 +159,14 @@ constexpr int kFusedRWaves = (kFusedVotes + kRVotesPerWave - 1) / kRVotesPerWave
 #define HSV_COMB_HASH_WAVE 1
 #endif
 constexpr bool kHashWave = HSV_COMB_HASH_WAVE != 0;
+// HSV_COMB_SHA_COMPACT=1 (measurement builds only): the hash wave runs
+// SHA-512 with one 16-round body (sha512_compress_compact), half the code
+// fetched cold at each launch.  Measured no faster: the hash took 10.2 against
+// 9.7 us at C1 and 13.5 against 13.2 us at C3 (profiles/r04t_qcclk_*.txt).
+#ifndef HSV_COMB_SHA_COMPACT
+#define HSV_COMB_SHA_COMPACT 0
+#endif
+constexpr bool kShaCompact = HSV_COMB_SHA_COMPACT != 0;
 constexpr uint32_t kHashWaveIdx = 1 + kFusedRWaves;
 constexpr int kFusedThreads = 64 * (1 + kFusedRWaves + (kHashWave ? 1 : 0));
 
@@ -317,7 +325,7 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
         uint32_t pkw[8], sigw[16], msgw[8], h[16], kr[9];
         load_vote_words(pks, kk, vote_sig(vl), vote_msg(vl), pkw, sigw, msgw);
         HSV_QC_CLK_LOADED(3);
-        sha512_96(sigw, pkw, msgw, h);
+        sha512_96<kShaCompact>(sigw, pkw, msgw, h);
         const sc k = sc_reduce512(h);
         recode_add<9, 8, kCombPos>(k.v, 8, kr);
         if (g == 0u) {

@@ -124,6 +124,29 @@ HSV_INL void sha512_compress(uint64_t h[8], uint64_t w[16]) {
   h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
 }
 
+// The same compression with one 16-round body: five passes of 16 rounds,
+// each followed (but the last) by a separate extension of the schedule.  Same
+// instruction count, about half the code: the latency kernels' lone waves
+// execute it once, with every instruction fetched cold.
+HSV_INL void sha512_compress_compact(uint64_t h[8], uint64_t w[16]) {
+  uint64_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+  HSV_NOUNROLL
+  for (int blk = 0; blk < 5; ++blk) {
+    HSV_UNROLL
+    for (int j = 0; j < 16; ++j) sha512_round(a, b, c, d, e, f, g, hh, w[j], kSha512K[blk * 16 + j]);
+    if (blk == 4) break;
+    HSV_UNROLL
+    for (int j = 0; j < 16; ++j) {
+      const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+      const uint64_t s0 = sha_xor3(sha_rotr(w15, 1), sha_rotr(w15, 8), w15 >> 7);
+      const uint64_t s1 = sha_xor3(sha_rotr(w2, 19), sha_rotr(w2, 61), w2 >> 6);
+      w[j] = w[j] + s0 + w[(j + 9) & 15] + s1;
+    }
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d;
+  h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
 // Big-endian 64-bit word from two little-endian 32-bit loads of bytes b0..b7.
 HSV_INL uint64_t be64_from_le32(uint32_t lo_bytes, uint32_t hi_bytes) {
   return ((uint64_t)bswap32(lo_bytes) << 32) | bswap32(hi_bytes);
@@ -132,6 +155,7 @@ HSV_INL uint64_t be64_from_le32(uint32_t lo_bytes, uint32_t hi_bytes) {
 // SHA-512 over R(32) || A(32) || M(32), each given as 8 little-endian words.
 // Output: the 64-byte digest as 16 little-endian 32-bit limbs (the 512-bit
 // little-endian integer that Scalar::from_hash reduces).
+template <bool Compact = false>
 HSV_INL void sha512_96(const uint32_t r[8], const uint32_t a[8], const uint32_t m[8],
                        uint32_t out[16]) {
   uint64_t w[16];
@@ -150,7 +174,8 @@ HSV_INL void sha512_96(const uint32_t r[8], const uint32_t a[8], const uint32_t 
 #ifdef HSV_TIMING_STUB_SHA  // tools/phase_probe.py only: wrong results, timing share of SHA-512
   for (int i = 0; i < 8; ++i) h[i] ^= w[i] + w[i + 4];
 #else
-  sha512_compress(h, w);
+  if constexpr (Compact) sha512_compress_compact(h, w);
+  else sha512_compress(h, w);
 #endif
   HSV_UNROLL
   for (int i = 0; i < 8; ++i) {

@@ -159,6 +159,9 @@ int main(int argc, char **argv) {
       to_words(a, aw, 8);
       to_words(m, mw, 8);
       sha512_96(rw, aw, mw, h);
+      uint32_t hc[16];  // the one-body form of the latency kernels must agree
+      sha512_96<true>(rw, aw, mw, hc);
+      if (memcmp(h, hc, sizeof(h)) != 0) { fprintf(stderr, "sha512_compress_compact differs\n"); exit(4); }
       sc k = sc_reduce512(h);
       for (int i = 7; i >= 0; --i) printf("%08x", k.v[i]);
       printf("\n");
