@@ -568,6 +568,8 @@ namespace {
 // device, chunk by chunk.  Batches of at least 2 * pipe_chunk() items run as a
 // two-stage pipeline: two staging buffers and two streams, so the host packs
 // chunk i+1 and the DMA engine copies it while the kernels verify chunk i.
+std::atomic<bool> g_pipe_nocopy{false};  // set only through hsv_test_pipe_nocopy
+
 constexpr size_t kPipeChunkDefault = size_t(1) << 17;  // 16 MiB of inputs per pipelined chunk
 size_t pipe_chunk() {  // HSV_PIPE_CHUNK_LOG2 (14..22): measurement switch
   static const size_t c = [] {
@@ -710,12 +712,11 @@ int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, siz
   if (e == hipSuccess && msg_stride == 0) e = hipMemcpyAsync(d + d_dig, msg, 32, hipMemcpyHostToDevice, s.copy);
   if (e != hipSuccess) return drain(hip_fail("hipMemsetAsync", e));
   bool used[2] = {false, false};
-  // HSV_PIPE_NOCOPY=1 (measurement switch, tools/host_api_ab.py): a call of
-  // the same size as the slot's last one skips the pack and the copies and
+  // hsv_test_pipe_nocopy (libhsv_test.so only, tools/host_api_ab.py): a call
+  // of the same size as the slot's last one skips the pack and the copies and
   // verifies what the last call left in HBM -- the chunk schedule's GPU time
   // alone, for the same inputs called again
-  static const bool nocopy_env = env_int("HSV_PIPE_NOCOPY", 0) != 0;
-  const bool nocopy = nocopy_env && s.pipe_warm_n == n;
+  const bool nocopy = g_pipe_nocopy.load(std::memory_order_relaxed) && s.pipe_warm_n == n;
   s.pipe_warm_n = 0;
   t_clock.marks.clear();  // four marks per chunk instead of the HSV_MARK_* points
   for (size_t base = 0, k = 0, m = 0; k < sizes.size(); base += m, ++k) {
@@ -1058,6 +1059,8 @@ int hsvi_set_virtual_shards(int k) {
   G().virtual_shards = k;
   return HSV_OK;
 }
+
+int hsvi_set_pipe_nocopy(int on) { return hsvh::g_pipe_nocopy.exchange(on != 0) ? 1 : 0; }
 
 // Lifecycle call: must not run concurrently with verify calls (hsv.h).  It
 // still quiesces first -- every slot locked and drained, every side stream

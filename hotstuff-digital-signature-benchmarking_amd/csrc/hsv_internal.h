@@ -147,6 +147,7 @@ extern "C" {
 int hsvi_set_error(int code, const char *msg);
 // test hooks of hsv_capi.cpp (exported as hsv_set_* by libhsv_test.so only)
 int hsvi_set_virtual_shards(int k);
+int hsvi_set_pipe_nocopy(int on);  // hsv_test_pipe_nocopy (libhsv_test.so only)
 int hsvi_set_variant(int v);
 #ifdef __cplusplus
 }

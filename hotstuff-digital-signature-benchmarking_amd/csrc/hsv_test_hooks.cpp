@@ -20,5 +20,6 @@ int hsv_variant_list(int *out, int cap) { return hsvi_variant_list(out, cap); }
 int hsv_variant_available(int variant) { return hsvi_variant_available(variant); }
 int hsv_num_variants(void) { return hsvi_num_variants(); }
 int hsv_set_virtual_shards(int k) { return hsvi_set_virtual_shards(k); }
+int hsv_test_pipe_nocopy(int on) { return hsvi_set_pipe_nocopy(on); }
 
 }  // extern "C"

@@ -40,6 +40,12 @@ HSV_API int hsv_num_variants(void);
 /* Split host batches of >= 2^16 items into k shards on the bound device
  * (the multi-device gather path on a one-GPU box); 0 restores the default. */
 HSV_API int hsv_set_virtual_shards(int k);
+/* Measurement only (tools/host_api_ab.py): a pipelined host call of the same
+ * size as the slot's previous one skips the pack and the copies and verifies
+ * what that call left in HBM -- the chunk schedule's GPU time alone.  Its
+ * flags are the previous inputs' flags, so it never belongs in a product
+ * library.  Returns the previous setting. */
+HSV_API int hsv_test_pipe_nocopy(int on);
 
 #ifdef __cplusplus
 }

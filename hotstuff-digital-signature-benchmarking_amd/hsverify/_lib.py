@@ -26,7 +26,7 @@ TEST_LIB_PATH = os.path.join(_HERE, "libhsv_test.so")
 # Exported by libhsv_test.so / libhsv_all.so only, never by libhsv.so.
 HOOKS = ("hsv_test_inject_fault", "hsv_test_inject_mode", "hsv_test_corrupt_auto_committee",
          "hsv_test_lanesplit_check", "hsv_set_lattice_bits", "hsv_set_variant", "hsv_variant_list",
-         "hsv_variant_available", "hsv_num_variants", "hsv_set_virtual_shards")
+         "hsv_variant_available", "hsv_num_variants", "hsv_set_virtual_shards", "hsv_test_pipe_nocopy")
 
 # flag bits (include/hsv.h)
 STRICT_OK = 0x01
@@ -68,6 +68,7 @@ def _declare(lib):
         "hsv_init": (ctypes.c_int, [ctypes.c_int]),
         "hsv_bound_device": (ctypes.c_int, []),
         "hsv_set_virtual_shards": (ctypes.c_int, [ctypes.c_int]),
+        "hsv_test_pipe_nocopy": (ctypes.c_int, [ctypes.c_int]),
         "hsv_auto_committee_wait": (ctypes.c_int, [ctypes.c_int]),
         "hsv_auto_committee_faults": (ctypes.c_uint64, []),
         "hsv_variant_list": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),

@@ -69,6 +69,13 @@ def corrupt_auto_committee() -> int:
     return _lib.check(_lib.hook("hsv_test_corrupt_auto_committee")(), "hsv_test_corrupt_auto_committee")
 
 
+def pipe_nocopy(on: bool) -> bool:
+    """Measurement only (test library): pipelined host calls of the same size
+    as the slot's previous one skip the pack and the copies and verify what
+    that call left in HBM.  Returns the previous setting."""
+    return bool(_lib.hook("hsv_test_pipe_nocopy")(1 if on else 0))
+
+
 def host_call_stats() -> dict:
     """The calling thread's last host-buffer verification: pack time (host ms
     spent copying into pinned staging), bytes copied host-to-device, wall ms."""

@@ -2,8 +2,9 @@
 """A/B of the host-buffer call (hsv_verify from numpy arrays at 2^20 items,
 PCIe-inclusive) between environment settings, alternating fresh processes:
 by default the chunked copy pipeline against the same chunk schedule with
-the pack and the copies skipped on repeat calls (HSV_PIPE_NOCOPY=1, its GPU
-time alone); HSV_HOST_PIPE=streamed selects the streamed launch.  Prints each
+the pack and the copies skipped on repeat calls (HSV_PIPE_NOCOPY=1 here makes
+the child load libhsv_test.so and set hsv_test_pipe_nocopy: its GPU time
+alone); HSV_HOST_PIPE=streamed selects the streamed launch.  Prints each
 run's median of 5 calls and the median per setting.
 
 python tools/host_api_ab.py [--rounds 3] [SETTING ...]   (SETTING: NAME=VALUE,... or "default")
@@ -17,12 +18,16 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CHILD = r"""
-import json, sys, time
+import json, os, sys, time
 import numpy as np
 sys.path.insert(0, {root!r} + "/hotstuff-digital-signature-benchmarking_amd")
 from hsverify import _testing, synth, verifier
 n = 1 << 20
 w = synth.independent_triples(n, seed=5, corrupt_frac=0.05)
+if os.environ.get("HSV_PIPE_NOCOPY") == "1":  # the test library's no-copy hook
+    _ctx = _testing.test_library()
+    _ctx.__enter__()
+    _testing.pipe_nocopy(True)
 verifier.verify_flags(w.pk, w.sig, w.msg)
 ts = []
 for _ in range(5):
