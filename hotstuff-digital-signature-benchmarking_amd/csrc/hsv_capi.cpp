@@ -227,12 +227,15 @@ int slot_prepare(Slot &s, size_t dev_bytes, size_t host_bytes) {
   }
   if (host_bytes > s.h_cap) {
     if (s.h_buf) (void)hipHostFree(s.h_buf);
-    s.h_buf = nullptr;
+    s.h_buf = s.h_buf_dev = nullptr;
     s.h_cap = 0;
     const size_t cap = round_up(host_bytes, size_t(1) << 20);
     e = hipHostMalloc(&s.h_buf, cap, hipHostMallocDefault);
     if (e != hipSuccess) return hip_fail("hipHostMalloc", e);
     s.h_cap = cap;
+    // the zero-copy latency path needs the device address at every call
+    void *hd = nullptr;
+    if (hipHostGetDevicePointer(&hd, s.h_buf, 0) == hipSuccess) s.h_buf_dev = static_cast<uint8_t *>(hd);
   }
   return HSV_OK;
 }
@@ -953,7 +956,7 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
     call_mark(HSV_MARK_STAGED);
     hipError_t e;
     void *hd = nullptr;
-    if (!no_zero_copy && n <= kZeroCopyMax && hipHostGetDevicePointer(&hd, h, 0) == hipSuccess && hd) {
+    if (!no_zero_copy && n <= kZeroCopyMax && (hd = s.h_buf_dev) != nullptr) {
       // small batches (a QC of non-cached keys, a single vote): the kernels read
       // the pinned staging buffer and write the flags through its device
       // mapping, so no copy launches sit on the latency path
@@ -1113,7 +1116,7 @@ void hsv_shutdown(void) {
       s.h_stream = nullptr;
       s.h_stream_cap = 0;
       s.stream = s.stream2 = s.stream3 = nullptr;
-      s.d_buf = s.h_buf = nullptr;
+      s.d_buf = s.h_buf = s.h_buf_dev = nullptr;
       s.d_cap = s.h_cap = 0;
     }
     for (hipStream_t st : c->side_all) (void)hipStreamDestroy(st);

@@ -174,7 +174,7 @@ int committee_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t
       const char *v = std::getenv("HSV_COMMITTEE_ZC_MAX");
       return v ? (size_t)std::atoll(v) : kZeroCopyMax;
     }();
-    const bool zero_copy = k <= zc_max && hipHostGetDevicePointer(&hd, h, 0) == hipSuccess && hd;
+    const bool zero_copy = k <= zc_max && (hd = s.h_buf_dev) != nullptr;
     // The zero-copy latency form marks each block done in pinned memory and the
     // host spins on the markers instead of hipStreamSynchronize (see the
     // kernel): the flags are final once every block has released them, and

@@ -64,6 +64,7 @@ struct Slot {
   uint8_t *d_buf = nullptr;
   size_t d_cap = 0;
   uint8_t *h_buf = nullptr;
+  uint8_t *h_buf_dev = nullptr;  // h_buf's device address (zero-copy launches), looked up once
   size_t h_cap = 0;
   // pinned staging of the streamed host path (run_streamed), allocated
   // coherent: the running kernel reads pieces the host publishes after it
