@@ -471,8 +471,8 @@ def mempool_bench(dev, n=1 << 20, tx_size=512, cpu_sample=1 << 17, nstreams=2, s
     from hsverify import mempool, synth
     w = synth.transactions(n, tx_size=tx_size, seed=9)
     d = torch.from_numpy(w.txs.reshape(-1)).to(dev)
-    # Consecutive batches alternate over the C4 line's streams when given
-    # (main passes them), else over nstreams streams of their own.  Streams
+    # Consecutive batches alternate over the given streams (main passes the
+    # C4 line's first two), else over nstreams streams of their own.  Streams
     # created later can land on a hardware queue an earlier stream already
     # uses; two batches on one queue then run back to back instead of the
     # next one starting in the previous grid's end.  In the round-4 trace the
@@ -854,7 +854,11 @@ def main():
         out["tc_latency"] = tc_latency(a.qc_reps, auto=True)
         _lib.load().hsv_set_auto_committee(1)
         out["committee_cache"] = committee_bench(a.qc_reps, dev)
-        out["mempool_tx"] = mempool_bench(dev, nstreams=nst, streams=streams)
+        # two streams: the record kernels (message hash + prepass, 2.3x the C4
+        # prepass's work) fill the point passes' grid ends better with one
+        # batch in flight beside the next than with two (9.57 against 9.77 ms
+        # per 2^20, profiles/r04z_mempool_streams2.txt)
+        out["mempool_tx"] = mempool_bench(dev, nstreams=2, streams=streams[:2] if nst >= 2 else None)
         if world == 1 and not a.no_cpu_baseline:
             out["qc_cpu_baseline"] = qc_cpu()
     print(json.dumps(out), flush=True)

@@ -2,7 +2,7 @@
 """The mempool line on the C4 line's streams against streams of its own
 (bench.mempool_bench), in one process after a C4-style warm-up that creates
 three streams first: prints ms per 2^20 transactions for both, alternating.
-python tools/mempool_streams_ab.py [--rounds 3]"""
+python tools/mempool_streams_ab.py [--rounds 3] [--own 3]"""
 import argparse
 import json
 import os
@@ -16,6 +16,7 @@ sys.path.insert(0, os.path.join(ROOT, "hotstuff-digital-signature-benchmarking_a
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--own", type=int, default=3, help="streams of the mempool line's own")
     a = ap.parse_args()
     import torch
     import bench
@@ -23,7 +24,7 @@ def main():
     c4_streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(2)]
     for _ in range(a.rounds):
         shared = bench.mempool_bench(dev, cpu_sample=0, nstreams=3, streams=c4_streams)
-        own = bench.mempool_bench(dev, cpu_sample=0, nstreams=3)
+        own = bench.mempool_bench(dev, cpu_sample=0, nstreams=a.own)
         print(json.dumps({"c4_streams_ms": round(shared["ms_per_step"], 4), "own_streams_ms": round(own["ms_per_step"], 4),
                           "ok": shared["honest_all_accepted"] and own["corrupted_all_rejected"]}), flush=True)
     return 0
