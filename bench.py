@@ -473,11 +473,10 @@ def mempool_bench(dev, n=1 << 20, tx_size=512, cpu_sample=1 << 17, nstreams=2, s
     d = torch.from_numpy(w.txs.reshape(-1)).to(dev)
     # Consecutive batches alternate over the given streams (main passes the
     # C4 line's first two), else over nstreams streams of their own.  Streams
-    # created later can land on a hardware queue an earlier stream already
-    # uses; two batches on one queue then run back to back instead of the
-    # next one starting in the previous grid's end.  In the round-4 trace the
-    # mempool line's three new streams used two queues, and a step took 10.0
-    # against 9.2 ms for the C4 line's three (profiles/r04p_mempool_trace.txt).
+    # created later can share a hardware queue with an earlier one (seen in
+    # the round-4 traces, profiles/r04p_mempool_trace.txt); that did not change
+    # the line's rate (r04w), but reusing the C4 line's streams keeps the two
+    # lines' setups alike.
     if streams is None:
         stream = torch.cuda.current_stream(dev)
         streams = [stream] + [torch.cuda.Stream(dev) for _ in range(max(1, nstreams) - 1)]
