@@ -174,10 +174,10 @@ constexpr int kFusedThreads = 64 * (1 + kFusedRWaves + (kHashWave ? 1 : 0));
 // Measurement builds only (tools/qc_wave_clocks.py): lane 0 of every wave
 // stamps the 100 MHz constant clock at fixed points of its path -- 0 entry,
 // 1 past the entry barrier, 2 its own work done (comb: the s half), 3 the
-// comb wave past the k handover (R and hash waves: their first loads landed), 4 at the final
-// barrier, 5 exit; slot 6 the
-// wave's place (XCC_ID << 32 | HW_ID: SIMD, CU, SH, SE), 7 / 8 the shader
-// clock (s_memtime) at entry / exit, so the tool can tell a slower clock from
+// comb wave past the k handover (R and hash waves: their first loads
+// landed), 4 at the final barrier, 5 exit; slot 6 holds the wave's place
+// (XCC_ID << 32 | HW_ID: SIMD, CU, SH, SE), 7 / 8 the shader clock
+// (s_memtime) at entry / exit, so the tool can tell a slower clock from
 // shared SIMDs.
 constexpr uint32_t kQcClkWaves = 4096;
 constexpr int kQcClkSlots = 10;  // slot 9: HSV_QC_WAVE_CLOCKS_TWICE
