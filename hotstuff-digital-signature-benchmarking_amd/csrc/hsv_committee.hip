@@ -257,19 +257,23 @@ __device__ __forceinline__ uint64_t lane_digits(const uint32_t r[9], uint32_t g)
   return d;
 }
 
-__global__ void __launch_bounds__(kFusedThreads)
-hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__restrict__ sig,
-                                  uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride,
-                                  uint32_t m, const uint8_t *__restrict__ pks, const uint8_t *__restrict__ key_flags,
-                                  uint32_t nkeys, const uint32_t *const *__restrict__ key_tables,
-                                  const uint32_t *__restrict__ btable, uint8_t *__restrict__ flags_out,
-                                  uint32_t inject, uint32_t *__restrict__ fault, uint32_t *__restrict__ done) {
+// One block's votes [blk * kFusedVotes, ...) of the latency form; the
+// launched kernel below runs it for its blockIdx, the resident service
+// (hsv_comb_resident_kernel) for block 0 of each request.
+__device__ __forceinline__ void comb_quad_block(const uint32_t *__restrict__ key_idx, const uint8_t *__restrict__ sig,
+                                                uint64_t sig_stride, const uint8_t *__restrict__ msg,
+                                                uint64_t msg_stride, uint32_t m, const uint8_t *__restrict__ pks,
+                                                const uint8_t *__restrict__ key_flags, uint32_t nkeys,
+                                                const uint32_t *const *__restrict__ key_tables,
+                                                const uint32_t *__restrict__ btable, uint8_t *__restrict__ flags_out,
+                                                uint32_t inject, uint32_t *__restrict__ fault,
+                                                uint32_t *__restrict__ done, uint32_t blk) {
   __shared__ uint32_t r_x[kFusedVotes][kFeLimbs], r_y[kFusedVotes][kFeLimbs], r_fl[kFusedVotes];
   __shared__ uint32_t k_rec[kFusedVotes][9], k_ready;
   __shared__ uint4 in_sig[kStageInputs ? kFusedVotes : 1][4], in_msg[kStageInputs ? kFusedVotes : 1][2];
   __shared__ uint32_t in_kidx[kStageInputs ? kFusedVotes : 1];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  const uint32_t base = blockIdx.x * kFusedVotes;
+  const uint32_t base = blk * kFusedVotes;
   HSV_QC_CLK(0);
   // vote v of the block reads vote min(base + v, m - 1): the last block's
   // spare slots repeat the batch's last vote and write no flag
@@ -509,8 +513,101 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
     // marks the block done, so the host may read the flags off pinned memory
     // without waiting for the kernel's completion signal
     __atomic_thread_fence(__ATOMIC_RELEASE);
-    if (lane == 0u) __hip_atomic_store(&done[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0u) __hip_atomic_store(&done[blk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+}
+
+__global__ void __launch_bounds__(kFusedThreads)
+hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__restrict__ sig,
+                                  uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride,
+                                  uint32_t m, const uint8_t *__restrict__ pks, const uint8_t *__restrict__ key_flags,
+                                  uint32_t nkeys, const uint32_t *const *__restrict__ key_tables,
+                                  const uint32_t *__restrict__ btable, uint8_t *__restrict__ flags_out,
+                                  uint32_t inject, uint32_t *__restrict__ fault, uint32_t *__restrict__ done) {
+  comb_quad_block(key_idx, sig, sig_stride, msg, msg_stride, m, pks, key_flags, nkeys, key_tables, btable, flags_out,
+                  inject, fault, done, blockIdx.x);
+}
+
+// The resident latency service (HSV_QC_RESIDENT=1, csrc/hsv_committee_api.cpp):
+// one block that stays on its CU and answers requests of at most kFusedVotes
+// votes posted in coherent pinned memory, instead of a launch per request
+// (a launch with marker sync costs 5.95 us round trip against 1.54 us for a
+// resident wave, profiles/r04zz_resident_latency.txt).  Thread 0 polls the
+// doorbell with relaxed system-scope loads and s_sleep; the block runs the
+// request through comb_quad_block, and thread 0 releases the flags and sets
+// done = the request's sequence number.  It leaves on the stop word or after
+// idle_ticks (100 MHz) without a request, and clears `alive` as it goes, so
+// no grid outlives its process; the host relaunches it on the next request.
+// a relaxed system-scope load: a vector load, never the scalar cache, which
+// would keep an earlier request's header
+template <class T>
+__device__ __forceinline__ T req_load(T *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void __launch_bounds__(kFusedThreads) hsv_comb_resident_kernel(QcResidentReq *req, uint64_t idle_ticks) {
+  __shared__ uint32_t cmd_seq, cmd_stop, h_m, h_nkeys, h_inject;
+  __shared__ uint64_t h_msg_stride;
+  __shared__ const uint8_t *h_pks;
+  __shared__ const uint8_t *h_key_flags;
+  __shared__ const uint32_t *const *h_key_tables;
+  __shared__ const uint32_t *h_btable;
+  uint32_t last = 0;
+  if (threadIdx.x == 0) {
+    last = __hip_atomic_load(&req->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&req->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const uint64_t t0 = wall_clock64();
+      uint32_t sq = last, stop = 0;
+      for (;;) {
+        sq = __hip_atomic_load(&req->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        stop = __hip_atomic_load(&req->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (sq != last || stop) break;
+        if (wall_clock64() - t0 > idle_ticks) {
+          stop = 1u;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      cmd_seq = sq;
+      cmd_stop = stop;
+      last = sq;
+      if (!stop) {  // the request header, read once per request (the host wrote it before seq)
+        h_m = req_load(&req->m);
+        h_nkeys = req_load(&req->nkeys);
+        h_inject = req_load(&req->inject);
+        h_msg_stride = req_load(&req->msg_stride);
+        h_pks = (const uint8_t *)req_load((uint64_t *)&req->pks);
+        h_key_flags = (const uint8_t *)req_load((uint64_t *)&req->key_flags);
+        h_key_tables = (const uint32_t *const *)req_load((uint64_t *)&req->key_tables);
+        h_btable = (const uint32_t *)req_load((uint64_t *)&req->btable);
+      }
+    }
+    __syncthreads();
+    if (__builtin_amdgcn_readfirstlane(cmd_stop)) break;
+    // no cache line of an earlier request survives into this one: the same
+    // acquire a launch performs at its start
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    const uint32_t sq = __builtin_amdgcn_readfirstlane(cmd_seq);
+    // the header is uniform: in scalar registers, as a launch's arguments are
+    auto uni64 = [](uint64_t v) {
+      return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+             __builtin_amdgcn_readfirstlane((uint32_t)v);
+    };
+    comb_quad_block(req->key_idx, &req->sig[0][0], 64, &req->msg[0][0], uni64(h_msg_stride),
+                    __builtin_amdgcn_readfirstlane(h_m), (const uint8_t *)uni64((uint64_t)h_pks),
+                    (const uint8_t *)uni64((uint64_t)h_key_flags), __builtin_amdgcn_readfirstlane(h_nkeys),
+                    (const uint32_t *const *)uni64((uint64_t)h_key_tables), (const uint32_t *)uni64((uint64_t)h_btable),
+                    req->flags, __builtin_amdgcn_readfirstlane(h_inject), req->fault, nullptr, 0u);
+    __syncthreads();  // every wave past its reads of this request and (wave 0) its flag stores
+    if (threadIdx.x == 0) {
+      __atomic_thread_fence(__ATOMIC_RELEASE);
+      __hip_atomic_store(&req->done, sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(&req->alive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Test hook (tests/test_lanesplit.py): the row forms of hsv_fe16x16.hpp
@@ -637,6 +734,14 @@ extern "C" hipError_t hsv_launch_comb_verify(const uint32_t *key_idx, const uint
                      fault);
   return hipGetLastError();
 }
+
+extern "C" hipError_t hsv_launch_comb_resident(QcResidentReq *d_req, uint64_t idle_ticks, hipStream_t stream) {
+  if (!d_req) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(hsv::hsv_comb_resident_kernel, dim3(1), dim3(hsv::kFusedThreads), 0, stream, d_req, idle_ticks);
+  return hipGetLastError();
+}
+
+extern "C" uint32_t hsv_comb_resident_votes(void) { return (uint32_t)hsv::kFusedVotes; }
 
 extern "C" uint32_t hsv_comb_marker_blocks(uint32_t m) {
   return m <= kCombQuadMax ? (m + hsv::kFusedVotes - 1) / hsv::kFusedVotes : 0u;

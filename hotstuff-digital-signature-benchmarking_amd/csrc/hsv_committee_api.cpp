@@ -129,6 +129,164 @@ struct CommitteeDev {
   const uint32_t *const *d_tabptr = nullptr;
 };
 
+// ---- resident latency service (HSV_QC_RESIDENT=1, opt-in) --------------------------
+// One block of hsv_comb_resident_kernel stays on a CU of the home device and
+// answers requests of at most hsv_comb_resident_votes() votes posted in
+// coherent pinned memory: 1.54 us round trip against 5.95 us for a launch with
+// marker sync (profiles/r04zz_resident_latency.txt).  It holds that CU while it
+// runs, hence opt-in.  The kernel leaves on the stop word (hsv_shutdown, and an
+// atexit handler registered at the first start) or after kResidentIdle without
+// a request; the next request relaunches it.  A request unanswered within
+// kResidentWait ends the service for the process, and the call takes the
+// launch path, so the service can cost latency but never a verdict.
+constexpr uint64_t kResidentIdleTicks = 100000000ull;  // 1 s of the 100 MHz clock
+constexpr auto kResidentWait = std::chrono::milliseconds(50);
+constexpr int kResidentUnavailable = 1;
+
+struct ResidentQc {
+  std::mutex mu;
+  int device = -1;
+  QcResidentReq *h = nullptr;  // coherent pinned
+  QcResidentReq *d = nullptr;  // its device address
+  hipStream_t stream = nullptr;
+  uint32_t seq = 0;
+  bool broken = false;
+  bool atexit_registered = false;
+};
+
+ResidentQc &RQ() {
+  static ResidentQc r;
+  return r;
+}
+
+bool resident_enabled() {
+  static const bool on = [] {
+    const char *v = std::getenv("HSV_QC_RESIDENT");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+
+// stop the kernel and wait for its grid (mu held)
+void resident_stop_locked(ResidentQc &r) {
+  if (!r.h || !r.stream) return;
+  __atomic_store_n(&r.h->stop, 1u, __ATOMIC_RELEASE);
+  DeviceGuard guard(r.device);
+  (void)hipStreamSynchronize(r.stream);
+  __atomic_store_n(&r.h->stop, 0u, __ATOMIC_RELEASE);
+}
+
+void resident_atexit() {
+  ResidentQc &r = RQ();
+  std::lock_guard<std::mutex> lk(r.mu);
+  resident_stop_locked(r);
+}
+
+// the kernel running on `device` (mu held): HSV_OK or kResidentUnavailable
+int resident_ensure_locked(ResidentQc &r, int device) {
+  if (r.broken) return kResidentUnavailable;
+  if (r.h && r.device != device) return kResidentUnavailable;  // one device per process
+  if (!r.h) {
+    void *h = nullptr, *d = nullptr;
+    // default (non-coherent) pinned memory, as the launch path's staging: the
+    // kernel's per-request system-scope acquire drops stale lines, and its
+    // doorbell loads are system-scope atomics
+    if (hipHostMalloc(&h, sizeof(QcResidentReq), hipHostMallocDefault) != hipSuccess) {
+      r.broken = true;
+      return kResidentUnavailable;
+    }
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d ||
+        hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking) != hipSuccess) {
+      (void)hipHostFree(h);
+      r.broken = true;
+      return kResidentUnavailable;
+    }
+    std::memset(h, 0, sizeof(QcResidentReq));
+    r.h = static_cast<QcResidentReq *>(h);
+    r.d = static_cast<QcResidentReq *>(d);
+    r.device = device;
+    r.seq = 0;
+  }
+  if (__atomic_load_n(&r.h->alive, __ATOMIC_ACQUIRE) == 1u) return HSV_OK;
+  // not running (first use, or it left after an idle second): relaunch
+  (void)hipStreamSynchronize(r.stream);  // the previous grid has fully ended
+  __atomic_store_n(&r.h->stop, 0u, __ATOMIC_RELEASE);
+  if (hsv_launch_comb_resident(r.d, kResidentIdleTicks, r.stream) != hipSuccess) {
+    r.broken = true;
+    return kResidentUnavailable;
+  }
+  if (!r.atexit_registered) {  // after HIP's own: runs before the runtime tears down
+    std::atexit(resident_atexit);
+    r.atexit_registered = true;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  while (__atomic_load_n(&r.h->alive, __ATOMIC_ACQUIRE) != 1u)
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+      resident_stop_locked(r);
+      r.broken = true;
+      return kResidentUnavailable;
+    }
+  return HSV_OK;
+}
+
+// One request of at most hsv_comb_resident_votes() votes: HSV_OK, an error
+// (HSV_ERR_DEVICE_FAULT from the self-checks), or kResidentUnavailable (the
+// caller launches instead).
+int resident_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t *sig, size_t sig_stride,
+                 const uint8_t *msg, size_t msg_stride, size_t m, uint8_t *flags_out, const uint32_t *btable) {
+  ResidentQc &r = RQ();
+  std::lock_guard<std::mutex> lk(r.mu);
+  if (resident_ensure_locked(r, cd.device) != HSV_OK) return kResidentUnavailable;
+  QcResidentReq &q = *r.h;
+  q.m = (uint32_t)m;
+  q.nkeys = cd.n;
+  q.inject = (uint32_t)hsvi_inject_mode();
+  q.msg_stride = msg_stride ? 32 : 0;
+  q.pks = cd.d_pks;
+  q.key_flags = cd.d_kflags;
+  q.key_tables = cd.d_tabptr;
+  q.btable = btable;
+  for (size_t i = 0; i < m; ++i) {
+    q.key_idx[i] = key_idx[i];
+    std::memcpy(q.sig[i], sig + i * sig_stride, 64);
+    if (msg_stride) std::memcpy(q.msg[i], msg + i * msg_stride, 32);
+    q.flags[i] = 0;  // an unwritten flag reads as a rejection
+  }
+  if (!msg_stride) std::memcpy(q.msg[0], msg, 32);
+  std::memset(q.fault, 0, sizeof(q.fault));
+  call_mark(HSV_MARK_STAGED);
+  // One retry: the kernel may leave on its idle timer just as a request is
+  // posted (it read the doorbell before the store); then it is relaunched
+  // and the same request posted again under a new number.
+  for (int attempt = 0;; ++attempt) {
+    const uint32_t sq = ++r.seq == 0 ? ++r.seq : r.seq;  // never 0
+    __atomic_store_n(&q.seq, sq, __ATOMIC_RELEASE);      // everything above is visible first
+    call_mark(HSV_MARK_LAUNCH);
+    const auto t0 = std::chrono::steady_clock::now();
+    bool answered = true;
+    while (__atomic_load_n(&q.done, __ATOMIC_ACQUIRE) != sq)
+      if (std::chrono::steady_clock::now() - t0 > kResidentWait) {
+        answered = false;
+        break;
+      }
+    if (answered) break;
+    if (attempt == 0 && __atomic_load_n(&q.alive, __ATOMIC_ACQUIRE) == 0u &&
+        resident_ensure_locked(r, cd.device) == HSV_OK)
+      continue;
+    // no answer from a running kernel: end the service for this process,
+    // the launch path answers
+    resident_stop_locked(r);
+    r.broken = true;
+    return kResidentUnavailable;
+  }
+  call_mark(HSV_MARK_SYNC);
+  const int rc = check_faults(reinterpret_cast<const uint8_t *>(q.fault), "committee verify (resident)");
+  if (rc != HSV_OK) return rc;
+  std::memcpy(flags_out, q.flags, m);
+  call_mark(HSV_MARK_DONE);
+  return HSV_OK;
+}
+
 // Votes by member index on the committee's device, through a slot of that
 // device: the kernels read the pinned staging buffer directly for batches of
 // at most kZeroCopyMax votes (the latency path), otherwise via copies.
@@ -141,6 +299,10 @@ int committee_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t
   if (guard.status() != hipSuccess) return hip_fail("hipSetDevice", guard.status());
   rc = ensure_btable(c);  // also after an hsv_shutdown
   if (rc != HSV_OK) return rc;
+  if (resident_enabled() && m <= hsv_comb_resident_votes()) {
+    rc = resident_run(cd, key_idx, sig, sig_stride, msg, msg_stride, m, flags_out, c.d_btable);
+    if (rc != kResidentUnavailable) return rc;
+  }
   SlotLease lease(c);
   Slot &s = lease.slot();
   call_mark(HSV_MARK_SLOT);
@@ -697,6 +859,11 @@ int auto_committee_corrupt_tables() {
 }
 
 void auto_committee_shutdown() {
+  {
+    ResidentQc &r = RQ();
+    std::lock_guard<std::mutex> lk(r.mu);
+    resident_stop_locked(r);
+  }
   auto_reset(false);
   AutoCommittee &a = AC();
   std::lock_guard<std::mutex> lk(a.mu);

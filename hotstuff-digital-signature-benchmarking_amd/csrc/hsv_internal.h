@@ -86,9 +86,29 @@ double hsv_launch_mad_peak(int device_cus);
 #endif
 
 // ---- committee key cache (hsv_committee.hip) -----------------------------
+// Request block of the resident committee service (hsv_comb_resident_kernel,
+// csrc/hsv_committee.hip), in coherent pinned host memory: the host fills a
+// request and bumps `seq`; the kernel answers with `done` = seq.
+struct QcResidentReq {
+  uint32_t seq, stop, alive, done;       // doorbell, stop word, set while the kernel runs, completion
+  uint32_t m, nkeys, inject, pad0;       // votes (<= hsv_comb_resident_votes()), members, fault injection
+  uint64_t msg_stride;                   // 0: one shared digest in msg[0]; 32: a digest per vote
+  const uint8_t *pks;                    // the committee view's device arrays
+  const uint8_t *key_flags;
+  const uint32_t *const *key_tables;
+  const uint32_t *btable;
+  uint32_t key_idx[16];
+  uint32_t fault[8];                     // self-check words (the launched form's layout)
+  uint8_t flags[16];
+  uint8_t sig[16][64];                   // R || s per vote
+  uint8_t msg[16][32];
+};
+
 #ifdef __cplusplus
 extern "C" {
 #endif
+hipError_t hsv_launch_comb_resident(QcResidentReq *d_req, uint64_t idle_ticks, hipStream_t stream);
+uint32_t hsv_comb_resident_votes(void);  // votes one request may hold
 hipError_t hsv_launch_comb_build(const uint8_t *encs, uint32_t nkeys, uint32_t negate, uint32_t *tables,
                                  uint32_t *tmp, uint8_t *key_flags, hipStream_t stream);
 // key_tables[i]: device pointer to key i's comb table (hsv_comb_table_bytes)

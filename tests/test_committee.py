@@ -200,3 +200,50 @@ def test_auto_committee_behind_verify_batch(mods):
         lib.hsv_set_auto_committee(0)
         assert lib.hsv_auto_committee_size() == 0
         lib.hsv_set_auto_committee(1)
+
+
+RESIDENT_CHILD = r"""
+import sys
+sys.path.insert(0, {tests!r}); sys.path.insert(0, {pkg!r})
+import numpy as np
+import conftest
+from conftest import oracle_flags
+from hsverify import _lib, _testing, synth, verifier
+lib = _lib.load()
+oracle = conftest.oracle_lib.__wrapped__()
+lib.hsv_set_auto_committee(1)
+qc = synth.qc_votes(100, seed=5, corrupt_frac=0.3)      # one shared digest
+tc = synth.tc_votes(100, seed=6, corrupt_frac=0.3)      # a digest per vote
+for w in (qc, tc):
+    msg = np.broadcast_to(w.msg, (w.n, 32)) if w.msg.ndim == 1 else w.msg
+    packed = np.concatenate([w.pk, w.sig], axis=1).tobytes()
+    for _ in range(3):  # the keys recur in verify_batch calls: the automatic cache learns them
+        lib.hsv_verify_batch_packed(bytes(msg[0]), packed, w.n)
+    lib.hsv_auto_committee_wait(60000)
+    assert lib.hsv_auto_committee_size() > 0
+    used = 0
+    for k in (1, 2, 3, 4):
+        for i in range(0, w.n - k, 5):
+            got = verifier.verify_flags(w.pk[i:i + k], w.sig[i:i + k], msg[i:i + k] if w.msg.ndim == 2 else w.msg)
+            exp = oracle_flags(oracle, w.pk[i:i + k], w.sig[i:i + k], msg[i:i + k])
+            assert (got == exp).all(), (k, i, got, exp)
+            marks = _testing.host_call_marks()
+            used += marks[1] < 0 and marks[2] >= 0   # no slot lease (mark unset): the resident service answered
+    assert used > 0, "the resident service never answered"
+print("resident ok", used)
+"""
+
+
+def test_resident_service_in_a_child_process():
+    """The opt-in resident latency service (HSV_QC_RESIDENT=1, read once per
+    process): batches of 1-4 cached-key votes, with the corruption kinds of
+    synth.CORRUPTIONS, shared and per-vote digests, flag for flag against
+    the oracle; the host timeline shows the service (not a launch) answered."""
+    import os
+    import subprocess
+    import sys
+    from conftest import PKG
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, "-c", RESIDENT_CHILD.format(tests=here, pkg=PKG)], capture_output=True,
+                       text=True, timeout=300, env=dict(os.environ, HSV_QC_RESIDENT="1"))
+    assert r.returncode == 0 and "resident ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
