@@ -586,21 +586,13 @@ __global__ void __launch_bounds__(kFusedThreads) hsv_comb_resident_kernel(QcResi
       }
     }
     __syncthreads();
-    if (__builtin_amdgcn_readfirstlane(cmd_stop)) break;
-    // no cache line of an earlier request survives into this one: the same
-    // acquire a launch performs at its start
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    const uint32_t sq = __builtin_amdgcn_readfirstlane(cmd_seq);
-    // the header is uniform: in scalar registers, as a launch's arguments are
-    auto uni64 = [](uint64_t v) {
-      return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
-             __builtin_amdgcn_readfirstlane((uint32_t)v);
-    };
-    comb_quad_block(req->key_idx, &req->sig[0][0], 64, &req->msg[0][0], uni64(h_msg_stride),
-                    __builtin_amdgcn_readfirstlane(h_m), (const uint8_t *)uni64((uint64_t)h_pks),
-                    (const uint8_t *)uni64((uint64_t)h_key_flags), __builtin_amdgcn_readfirstlane(h_nkeys),
-                    (const uint32_t *const *)uni64((uint64_t)h_key_tables), (const uint32_t *)uni64((uint64_t)h_btable),
-                    req->flags, __builtin_amdgcn_readfirstlane(h_inject), req->fault, nullptr, 0u);
+    if (cmd_stop) break;
+    // no vector-cache line of an earlier request survives into this one (the
+    // request area is coherent host memory, which L2 does not keep)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const uint32_t sq = cmd_seq;
+    comb_quad_block(req->key_idx, &req->sig[0][0], 64, &req->msg[0][0], h_msg_stride, h_m, h_pks, h_key_flags,
+                    h_nkeys, h_key_tables, h_btable, req->flags, h_inject, req->fault, nullptr, 0u);
     __syncthreads();  // every wave past its reads of this request and (wave 0) its flag stores
     if (threadIdx.x == 0) {
       __atomic_thread_fence(__ATOMIC_RELEASE);

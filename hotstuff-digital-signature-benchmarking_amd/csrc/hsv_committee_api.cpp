@@ -188,10 +188,10 @@ int resident_ensure_locked(ResidentQc &r, int device) {
   if (r.h && r.device != device) return kResidentUnavailable;  // one device per process
   if (!r.h) {
     void *h = nullptr, *d = nullptr;
-    // default (non-coherent) pinned memory, as the launch path's staging: the
-    // kernel's per-request system-scope acquire drops stale lines, and its
-    // doorbell loads are system-scope atomics
-    if (hipHostMalloc(&h, sizeof(QcResidentReq), hipHostMallocDefault) != hipSuccess) {
+    // coherent pinned memory: the running kernel reads what the host writes
+    // after it started (a non-coherent area let it read a stale request
+    // header and fault, profiles/r04res_pytest_sub2.txt)
+    if (hipHostMalloc(&h, sizeof(QcResidentReq), hipHostMallocCoherent) != hipSuccess) {
       r.broken = true;
       return kResidentUnavailable;
     }
