@@ -759,4 +759,16 @@ extern "C" __attribute__((visibility("default"))) int hsv_qc_wave_clocks(uint64_
   if (hipMemset(p, 0, sizeof(hsv::g_qc_clk)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return -1;
   return hsv::kFusedThreads / 64;
 }
+
+// The same without synchronising the device (a resident block keeps running):
+// copies on a stream of its own, no clearing.
+extern "C" __attribute__((visibility("default"))) int hsv_qc_wave_clocks_nosync(uint64_t *out, size_t waves) {
+  const size_t n = std::min<size_t>(waves, hsv::kQcClkWaves) * hsv::kQcClkSlots * sizeof(uint64_t);
+  hipStream_t st = nullptr;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return -1;
+  hipError_t e = hipMemcpyFromSymbolAsync(out, HIP_SYMBOL(hsv::g_qc_clk), n, 0, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipStreamDestroy(st);
+  return e == hipSuccess ? hsv::kFusedThreads / 64 : -1;
+}
 #endif
