@@ -43,6 +43,41 @@ __global__ void __launch_bounds__(64) k_resident(uint32_t *cmd, uint32_t *done, 
   }
 }
 
+// The committee service's request shape without the verification: a block
+// of four waves, thread 0 polls, the block meets at a barrier, every wave
+// performs the agent-scope acquire, thread 0 releases and answers (the
+// resident service's per-request overhead).
+__global__ void __launch_bounds__(256) k_resident_block(uint32_t *cmd, uint32_t *done, uint64_t idle_ticks,
+                                                        int acquire) {
+  __shared__ uint32_t s_cmd, s_stop;
+  uint32_t last = 0;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const uint64_t t0 = wall_clock64();
+      uint32_t c = last, stop = 0;
+      for (;;) {
+        c = __hip_atomic_load(cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (c == kStop) { stop = 1; break; }
+        if (c != last) break;
+        if (wall_clock64() - t0 > idle_ticks) { stop = 1; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      s_cmd = c;
+      s_stop = stop;
+      last = c;
+    }
+    __syncthreads();
+    if (s_stop) break;
+    if (acquire) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const uint32_t c = s_cmd;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __atomic_thread_fence(__ATOMIC_RELEASE);
+      __hip_atomic_store(done, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 #define CK(x)                                                              \
   do {                                                                     \
     hipError_t e_ = (x);                                                   \
@@ -120,8 +155,40 @@ int main() {
     std::fprintf(stderr, "resident request timed out\n");
     return 4;
   }
-  std::printf("{\"launch_marker_p50_us\": %.2f, \"resident_round_trip_p50_us\": %.2f, \"reps\": %d}\n", p50(tl),
-              p50(tr), reps);
+  // the service's request shape: four waves, barrier, acquire (or not), release
+  double tb[2] = {0, 0};
+  for (int acq = 0; acq < 2; ++acq) {
+    *cmd = 0;
+    *done = 0;
+    hipLaunchKernelGGL(k_resident_block, dim3(1), dim3(256), 0, st, d, d + 16, (uint64_t)200000000ull, acq);
+    CK(hipGetLastError());
+    *cmd = 1;
+    if (!wait_for(done, 1u, std::chrono::microseconds(2000000))) {
+      *cmd = kStop;
+      (void)hipStreamSynchronize(st);
+      std::fprintf(stderr, "resident block never answered\n");
+      return 5;
+    }
+    std::vector<double> t;
+    bool good = true;
+    for (int i = 2; i <= reps + 51 && good; ++i) {
+      const auto t0 = clk::now();
+      *cmd = (uint32_t)i;
+      good = wait_for(done, (uint32_t)i, std::chrono::microseconds(100000));
+      const auto t1 = clk::now();
+      if (i > 51) t.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+    }
+    *cmd = kStop;
+    CK(hipStreamSynchronize(st));
+    if (!good) {
+      std::fprintf(stderr, "resident block request timed out\n");
+      return 6;
+    }
+    tb[acq] = p50(t);
+  }
+  std::printf("{\"launch_marker_p50_us\": %.2f, \"resident_round_trip_p50_us\": %.2f, "
+              "\"resident_block_p50_us\": %.2f, \"resident_block_acquire_p50_us\": %.2f, \"reps\": %d}\n",
+              p50(tl), p50(tr), tb[0], tb[1], reps);
   CK(hipStreamDestroy(st));
   CK(hipHostFree(h));
   return 0;
