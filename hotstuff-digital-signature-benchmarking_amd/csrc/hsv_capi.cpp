@@ -126,12 +126,8 @@ int ensure_init() {
     for (int s = 0; s < g.nslots; ++s) c->slots.emplace_back(new Slot());
     g.ctx.push_back(c);
   }
-  const int v = env_int("HSV_VARIANT", -1);
-  if (v >= 0 && hsvi_variant_available(v)) g.variant = v;
   const int d = env_int("HSV_DEVICE", kUnbound);
   if (g.bound.load() == kUnbound && d >= -1 && d < n) g.bound = d;
-  const int vs = env_int("HSV_VIRTUAL_SHARDS", 0);
-  if (vs > 0 && g.virtual_shards.load() == 0) g.virtual_shards = std::min(vs, 64);
   g.inited = true;
   return n > 0 ? HSV_OK : fail(HSV_ERR_NO_DEVICE, "no HIP device visible");
 }
@@ -199,14 +195,10 @@ SlotLease::SlotLease(DevCtx &c) {
 // took 10.9-11.0 ms against 10.1-10.3 ms at the greatest priority, with the
 // application's three-stream C4 line unchanged (8.89-8.92 ms per step;
 // tools/eager_streams_ab.sh, profiles/r03zm_eager_streams_ab.txt).
-// HSV_PIPE_PRIO=0 restores normal priority (measurement switch).
 hipError_t pipe_stream_create(hipStream_t *s) {
-  static const bool prio = env_int("HSV_PIPE_PRIO", 1) != 0;
-  if (prio) {
-    int least = 0, greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
-      return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
-  }
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
   return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
 }
 
@@ -216,6 +208,7 @@ int slot_prepare(Slot &s, size_t dev_bytes, size_t host_bytes) {
     e = pipe_stream_create(&s.stream);
     if (e != hipSuccess) return hip_fail("hipStreamCreate", e);
   }
+  if ((dev_bytes > s.d_cap && s.d_buf) || (host_bytes > s.h_cap && s.h_buf)) resident_quiesce();
   if (dev_bytes > s.d_cap) {
     if (s.d_buf) (void)hipFree(s.d_buf);
     s.d_buf = nullptr;
@@ -240,18 +233,40 @@ int slot_prepare(Slot &s, size_t dev_bytes, size_t host_bytes) {
   return HSV_OK;
 }
 
+int slot_sync_region(Slot &s, size_t bytes) {
+  if (bytes <= s.h_sync_cap) return HSV_OK;
+  if (s.h_sync) {
+    resident_quiesce();
+    (void)hipHostFree(s.h_sync);
+  }
+  s.h_sync = s.h_sync_dev = nullptr;
+  s.h_sync_cap = 0;
+  const size_t cap = round_up(bytes, size_t(64) << 10);
+  hipError_t e = hipHostMalloc(&s.h_sync, cap, hipHostMallocCoherent | hipHostMallocMapped);
+  if (e != hipSuccess) return hip_fail("hipHostMalloc (coherent sync region)", e);
+  void *hd = nullptr;
+  e = hipHostGetDevicePointer(&hd, s.h_sync, 0);
+  if (e != hipSuccess || !hd) {
+    (void)hipHostFree(s.h_sync);
+    s.h_sync = nullptr;
+    return hip_fail("hipHostGetDevicePointer (coherent sync region)", e);
+  }
+  s.h_sync_dev = static_cast<uint8_t *>(hd);
+  s.h_sync_cap = cap;
+  return HSV_OK;
+}
+
 int slot_stream2(Slot &s) {
   if (s.stream2) return HSV_OK;
   const hipError_t e = pipe_stream_create(&s.stream2);
   return e == hipSuccess ? HSV_OK : hip_fail("hipStreamCreate", e);
 }
 
-int slot_pipeline(Slot &s, int compute_streams) {
+int slot_pipeline(Slot &s) {
   int rc = slot_stream2(s);
   if (rc != HSV_OK) return rc;
   hipError_t e = hipSuccess;
   if (!s.copy) e = pipe_stream_create(&s.copy);
-  if (e == hipSuccess && compute_streams > 2 && !s.stream3) e = pipe_stream_create(&s.stream3);
   for (int i = 0; i < 5 && e == hipSuccess; ++i)
     if (!s.ev[i]) e = hipEventCreateWithFlags(&s.ev[i], hipEventDisableTiming);
   return e == hipSuccess ? HSV_OK : hip_fail("creating the pipeline streams and events", e);
@@ -568,20 +583,14 @@ int device_for_call(const void *d_ptr, void *stream, int *dev) {
 namespace {
 
 // Records at pk + i*pk_stride etc. (msg_stride 0 = shared), [0, n) on one
-// device, chunk by chunk.  Batches of at least 2 * pipe_chunk() items run as a
+// device, chunk by chunk.  Batches of at least 2 * kPipeChunk items run as a
 // two-stage pipeline: two staging buffers and two streams, so the host packs
 // chunk i+1 and the DMA engine copies it while the kernels verify chunk i.
 std::atomic<bool> g_pipe_nocopy{false};  // set only through hsv_test_pipe_nocopy
 
-constexpr size_t kPipeChunkDefault = size_t(1) << 17;  // 16 MiB of inputs per pipelined chunk
-size_t pipe_chunk() {  // HSV_PIPE_CHUNK_LOG2 (14..22): measurement switch
-  static const size_t c = [] {
-    const char *v = std::getenv("HSV_PIPE_CHUNK_LOG2");
-    const int l = v ? std::atoi(v) : 0;
-    return (l >= 14 && l <= 22) ? (size_t(1) << l) : kPipeChunkDefault;
-  }();
-  return c;
-}
+// 16 MiB of inputs per pipelined chunk (2^17 items): 10.10 ms per 2^20
+// against 10.25 for 2^16 and 10.31 for 2^18 (profiles/r03y_host_pipeline_schedules.txt)
+constexpr size_t kPipeChunk = size_t(1) << 17;
 
 // The slot's launch workspaces (one per compute stream): the first `count`
 // exist and hold at least `need` bytes each; kept across calls, so no launch
@@ -592,6 +601,7 @@ int slot_workspaces(Slot &s, size_t need, int count) {
   if (need <= s.ws_cap && count <= have) return HSV_OK;
   const size_t cap = std::max(need, s.ws_cap);
   const int n = std::max(count, have);
+  if (have) resident_quiesce();
   for (uint8_t *&w : s.d_ws) {
     if (w) (void)hipFree(w);
     w = nullptr;
@@ -605,35 +615,16 @@ int slot_workspaces(Slot &s, size_t need, int count) {
   return HSV_OK;
 }
 
-// Chunk sizes of a pipelined call over n items (n >= 2 pipe_chunk()).
+// Chunk sizes of a pipelined call over n items (n >= 2 kPipeChunk).
 // Nothing hides the first chunk's pack and copy, so it is half a chunk
 // (2^16 items: 10.73 ms per 2^20 against 10.99 for a full first chunk sent
-// in four pieces and 11.01 for 2^15, profiles/r03m_host_pipeline_probe.txt).
-// Measurement switches: HSV_PIPE_FIRST_LOG2 sets the first chunk;
-// HSV_PIPE_SIZES="a,b,..." gives the sizes in units of 2^14 items (the last
-// one repeats until the n items are covered).
+// in four pieces and 11.01 for 2^15, profiles/r03m_host_pipeline_probe.txt;
+// eight schedules measured within 10.02-10.12 ms,
+// profiles/r03y_host_pipeline_schedules.txt).
 std::vector<size_t> pipe_schedule(size_t n) {
-  const size_t pchunk = pipe_chunk();
-  static const size_t first_env = [] {
-    const int l = env_int("HSV_PIPE_FIRST_LOG2", 0);
-    return (l >= 12 && l <= 22) ? (size_t(1) << l) : size_t(0);
-  }();
-  static const std::vector<size_t> sizes_env = [] {
-    std::vector<size_t> v;
-    if (const char *e = std::getenv("HSV_PIPE_SIZES"))
-      for (const char *c = e; *c;) {
-        const long u = std::strtol(c, const_cast<char **>(&c), 10);
-        if (u > 0 && u <= 256) v.push_back(size_t(u) << 14);
-        while (*c == ',' || *c == ' ') ++c;
-        if (*c && (*c < '0' || *c > '9')) break;
-      }
-    return v;
-  }();
   std::vector<size_t> sizes;
   for (size_t base = 0, k = 0; base < n; ++k) {
-    size_t want;
-    if (!sizes_env.empty()) want = sizes_env[std::min(k, sizes_env.size() - 1)];
-    else want = k == 0 ? std::min(pchunk, first_env ? first_env : pchunk / 2) : pchunk;
+    const size_t want = k == 0 ? kPipeChunk / 2 : kPipeChunk;
     sizes.push_back(std::min(want, n - base));
     base += sizes.back();
   }
@@ -649,7 +640,7 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
-// Large host batches (n >= 2 pipe_chunk(), n <= kChunk): the inputs stream
+// Large host batches (n >= 2 kPipeChunk, n <= kChunk): the inputs stream
 // to HBM chunk by chunk while earlier chunks verify.
 //   * HBM holds the whole batch as records pk | R || s | digest (96 B with a
 //     shared digest, staged once), then all flags and the self-check words.
@@ -687,25 +678,24 @@ int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, siz
   // Launches alternate over two compute streams.  A chunk's memset and
   // prepass (~0.1 ms) run beside only the other stream's point pass, a 2^17
   // grid that fills two thirds of the GPU's lanes (rocprofv3 kernel trace,
-  // profiles/r04l_host_kernel_trace_summary.txt); a third stream
-  // (HSV_PIPE_STREAMS=3, measurement switch) fills that gap but measured
-  // slower: 10.27 against 10.04 ms per 2^20, and 9.62 against 9.32 ms with
-  // the copies skipped (profiles/r04m_host_streams_ab.txt, r04i_host_nocopy.txt).
-  static const int nstreams = env_int("HSV_PIPE_STREAMS", 2) == 3 ? 3 : 2;
-  rc = slot_pipeline(s, nstreams);
+  // profiles/r04l_host_kernel_trace_summary.txt); a third stream fills that
+  // gap but measured slower: 10.27 against 10.04 ms per 2^20, and 9.62
+  // against 9.32 ms with the copies skipped (profiles/r04m_host_streams_ab.txt,
+  // r04i_host_nocopy.txt).
+  constexpr int nstreams = 2;
+  rc = slot_pipeline(s);
   if (rc != HSV_OK) return rc;
   // one launch workspace per compute stream, kept by the slot: a pool
   // allocation per launch made the enqueue of each chunk wait ~1 ms for an
   // earlier chunk (tools/host_api_probe.py marks)
   rc = slot_workspaces(s, hsv_launch_ws_bytes(v, (uint32_t)maxm), nstreams);
   if (rc != HSV_OK) return rc;
-  hipStream_t comp[3] = {s.stream, s.stream2, s.stream3};
+  hipStream_t comp[nstreams] = {s.stream, s.stream2};
   hipEvent_t staged[2] = {s.ev[0], s.ev[1]};
   auto drain = [&](int code) -> int {
     (void)hipStreamSynchronize(s.copy);
     (void)hipStreamSynchronize(s.stream);
     (void)hipStreamSynchronize(s.stream2);
-    if (s.stream3) (void)hipStreamSynchronize(s.stream3);
     return code;
   };
   uint8_t *d = s.d_buf;
@@ -733,26 +723,21 @@ int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, siz
     call_chunk_mark();
     uint8_t *dc = d + base * rec;  // chunk k's records in HBM
     // Items as records pk | R || s (| digest), so any item range is one
-    // contiguous copy.  HSV_PIPE_FIRST_PIECES (1..8, measurement switch)
-    // sends the first chunk in pieces, each copied as soon as it is packed;
-    // four pieces measured no faster than one (10.59 against 10.52 ms per
-    // 2^20, profiles/r04o_host_pieces_ab.txt): the pool's extra hand-offs
-    // cost what the overlap saves.
-    static const size_t first_pieces = (size_t)std::max(1, std::min(8, env_int("HSV_PIPE_FIRST_PIECES", 1)));
-    const size_t pieces = nocopy ? 0 : k == 0 && m >= first_pieces * 4096 ? first_pieces : 1;
-    for (size_t q = 0; q < pieces; ++q) {
-      const size_t lo0 = m * q / pieces, hi0 = m * (q + 1) / pieces;
+    // contiguous copy.  (Sending the first chunk in four pieces, each copied
+    // as soon as it was packed, measured no faster: 10.59 against 10.52 ms
+    // per 2^20, profiles/r04o_host_pieces_ab.txt.)
+    if (!nocopy) {
       const auto t_pack = std::chrono::steady_clock::now();
-      const int nparts = (int)std::min<size_t>(64, ((hi0 - lo0) * rec + kPackPart - 1) / kPackPart);
+      const int nparts = (int)std::min<size_t>(64, (m * rec + kPackPart - 1) / kPackPart);
       auto part = [&](int p) {
-        const size_t lo = lo0 + (hi0 - lo0) * p / nparts, hi = lo0 + (hi0 - lo0) * (p + 1) / nparts;
+        const size_t lo = m * p / nparts, hi = m * (p + 1) / nparts;
         pack_records(h, rec, pk + base * pk_stride, pk_stride, sig + base * sig_stride, sig_stride,
                      msg + base * msg_stride, msg_stride, lo, hi);
       };
       if (nparts < 2) part(0);
       else PackPool::get().run(nparts, part);
       t_pack_ms += ms_since(t_pack);
-      e = hipMemcpyAsync(dc + lo0 * rec, h + lo0 * rec, (hi0 - lo0) * rec, hipMemcpyHostToDevice, s.copy);
+      e = hipMemcpyAsync(dc, h, m * rec, hipMemcpyHostToDevice, s.copy);
       if (e != hipSuccess) return drain(hip_fail("hipMemcpyAsync H2D", e));
     }
     call_chunk_mark();
@@ -786,94 +771,8 @@ int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, siz
   return HSV_OK;
 }
 
-// Large host batches, streamed (round 4; HSV_HOST_PIPE=streamed, measured
-// slower than run_pipelined): ONE
-// persistent launch over the whole batch (n <= kChunk), started before the
-// inputs are packed.  The pinned staging holds every record; the pack pool
-// packs it piece by piece (2^14 items, 2 or 1.5 MiB) and marks each piece
-// ready in a pinned word the kernel polls before it touches the piece; the
-// kernel reads the records and writes the flags through the staging's device
-// mapping (hsv_verify_stream_kernel).  No copy engine, no chunk launches and
-// their grid ends: the call costs one launch over the batch plus the first
-// piece's pack.  Pinned layout: records n*rec | shared digest | ready words |
-// flags n | self-check words (3: curve check, canary, input timeout).
-constexpr uint32_t kStreamPieceLog2 = 14;
-// A wave polls an unready piece at most this often (about 4 us a poll, so
-// ~2 s) before the launch gives up: the host packs every piece within
-// milliseconds, so a launch still waiting has lost its host thread.
-constexpr uint32_t kStreamMaxPolls = 1u << 19;
-
-int run_streamed(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, size_t pk_stride, const uint8_t *sig,
-                 size_t sig_stride, const uint8_t *msg, size_t msg_stride, size_t n, uint8_t *flags_out) {
-  const size_t rec = msg_stride ? 128 : 96;
-  const size_t piece = size_t(1) << kStreamPieceLog2;
-  const size_t npieces = (n + piece - 1) / piece;
-  const size_t h_dig = round_up(n * rec, kAlign);
-  const size_t h_ready = h_dig + kAlign;
-  const size_t h_flag = h_ready + round_up(npieces * 4, kAlign);
-  const size_t h_fault = h_flag + round_up(n, kAlign);
-  const size_t h_total = h_fault + kAlign;
-  int rc = slot_prepare(s, 0, 0);
-  if (rc != HSV_OK) return rc;
-  hipError_t e;
-  if (h_total > s.h_stream_cap) {
-    if (s.h_stream) (void)hipHostFree(s.h_stream);
-    s.h_stream = nullptr;
-    s.h_stream_cap = 0;
-    const size_t cap = round_up(h_total, size_t(1) << 20);
-    e = hipHostMalloc(&s.h_stream, cap, hipHostMallocCoherent | hipHostMallocMapped);
-    if (e != hipSuccess) return hip_fail("hipHostMalloc (streamed staging)", e);
-    s.h_stream_cap = cap;
-  }
-  rc = slot_workspaces(s, hsv_launch_stream_ws_bytes((uint32_t)n), 1);
-  if (rc != HSV_OK) return rc;
-  void *hd = nullptr;
-  e = hipHostGetDevicePointer(&hd, s.h_stream, 0);
-  if (e != hipSuccess || !hd) return hip_fail("hipHostGetDevicePointer (streamed staging)", e);
-  uint8_t *h = s.h_stream, *d = static_cast<uint8_t *>(hd);
-  volatile uint32_t *ready = reinterpret_cast<volatile uint32_t *>(h + h_ready);
-  // nothing of an earlier call is in flight on this slot (its calls synchronise)
-  for (size_t p = 0; p < npieces; ++p) ready[p] = 0u;
-  std::memset(h + h_fault, 0, 16);
-  if (msg_stride == 0) std::memcpy(h + h_dig, msg, 32);
-  std::atomic_thread_fence(std::memory_order_seq_cst);
-  t_clock.marks.clear();
-  call_chunk_mark();
-  e = hsv_launch_verify_stream(d, (uint32_t)rec, msg_stride ? nullptr : d + h_dig, (uint32_t)n, kStreamPieceLog2,
-                               reinterpret_cast<const uint32_t *>(d + h_ready), d + h_flag, comb_b,
-                               reinterpret_cast<uint32_t *>(d + h_fault), kStreamMaxPolls, s.d_ws[0], s.ws_cap,
-                               s.stream);
-  if (e != hipSuccess) return hip_fail("streamed verify launch", e);
-  call_chunk_mark();
-  // the launch is queued: pack the pieces, in order of the pool's counter;
-  // each packed piece is published with a release store after the streaming
-  // stores' fence (pack_records), so the kernel never reads a half-packed piece
-  const auto t_pack = std::chrono::steady_clock::now();
-  PackPool::get().run((int)npieces, [&](int p) {
-    const size_t lo = (size_t)p * piece, hi = std::min(n, lo + piece);
-    pack_records(h, rec, pk, pk_stride, sig, sig_stride, msg, msg_stride, lo, hi);
-    std::atomic_thread_fence(std::memory_order_release);
-    ready[p] = 1u;
-  });
-  t_pack_ms += ms_since(t_pack);
-  t_h2d_bytes += n * rec;  // read by the kernel over PCIe through the mapping
-  call_chunk_mark();
-  e = hipStreamSynchronize(s.stream);
-  call_chunk_mark();
-  if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
-  uint32_t w[3];
-  std::memcpy(w, h + h_fault, sizeof(w));
-  if (w[2]) return fail(HSV_ERR_HIP, "streamed verify: the kernel waited too long for its inputs and aborted");
-  rc = check_faults(h + h_fault, "verify");
-  if (rc != HSV_OK) return rc;
-  std::memcpy(flags_out, h + h_flag, n);
-  return HSV_OK;
-}
-
 int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t *sig, size_t sig_stride,
                   const uint8_t *msg, size_t msg_stride, size_t n, uint8_t *flags_out) {
-  static const bool no_pipe = std::getenv("HSV_NO_PIPELINE") != nullptr;        // measurement switch
-  static const bool no_zero_copy = std::getenv("HSV_NO_ZERO_COPY") != nullptr;  // measurement switch
   const auto t_call = std::chrono::steady_clock::now();
   t_pack_ms = 0;
   t_h2d_bytes = 0;
@@ -886,27 +785,7 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
   SlotLease lease(c);
   Slot &s = lease.slot();
   call_mark(HSV_MARK_SLOT);
-  const size_t pchunk = pipe_chunk();
-  // HSV_HOST_PIPE=streamed: the one-launch streamed form (run_streamed) instead
-  // of the chunked copy pipeline (measurement switch).  Measured slower on
-  // MI355X: 11.7 against 9.9 ms per 2^20 (profiles/r04d_host_api_ab.txt),
-  // same VALU instruction count, VALUBusy 0.90 against 0.99 and a lower
-  // clock under the PCIe traffic (profiles/r04e_streampmc_summary.json).
-  static const bool streamed = [] {
-    const char *e = std::getenv("HSV_HOST_PIPE");
-    return e && std::strcmp(e, "streamed") == 0;
-  }();
-  if (!no_pipe && streamed && v == 21 && n >= 2 * pchunk) {
-    for (size_t base = 0; base < n; base += kChunk) {
-      const size_t m = std::min(kChunk, n - base);
-      rc = run_streamed(s, v, comb_b, pk + base * pk_stride, pk_stride, sig + base * sig_stride, sig_stride,
-                        msg + base * msg_stride, msg_stride, m, flags_out + base);
-      if (rc != HSV_OK) return rc;
-    }
-    t_call_ms = ms_since(t_call);
-    return HSV_OK;
-  }
-  if (!no_pipe && n >= 2 * pchunk) {
+  if (n >= 2 * kPipeChunk) {  // the copy pipeline (HBM holds the whole batch)
     for (size_t base = 0; base < n; base += kChunk) {
       const size_t m = std::min(kChunk, n - base);
       rc = run_pipelined(s, v, comb_b, pk + base * pk_stride, pk_stride, sig + base * sig_stride, sig_stride,
@@ -916,7 +795,7 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
     t_call_ms = ms_since(t_call);
     return HSV_OK;
   }
-  // below the pipeline's size (or with HSV_NO_PIPELINE): one staging buffer,
+  // below the pipeline's size: one staging buffer,
   // chunk by chunk -- pk 32 | sig 64 | msg 32 (or one shared digest) | flags 1
   // | self-check words (kFaultBytes); the same layout in HBM
   const size_t chunk = std::min(n, kChunk);
@@ -956,7 +835,7 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
     call_mark(HSV_MARK_STAGED);
     hipError_t e;
     void *hd = nullptr;
-    if (!no_zero_copy && n <= kZeroCopyMax && (hd = s.h_buf_dev) != nullptr) {
+    if (n <= kZeroCopyMax && (hd = s.h_buf_dev) != nullptr) {
       // small batches (a QC of non-cached keys, a single vote): the kernels read
       // the pinned staging buffer and write the flags through its device
       // mapping, so no copy launches sit on the latency path
@@ -1080,7 +959,6 @@ void hsv_shutdown(void) {
     for (auto &sp : c->slots) {
       if (sp->stream) (void)hipStreamSynchronize(sp->stream);
       if (sp->stream2) (void)hipStreamSynchronize(sp->stream2);
-      if (sp->stream3) (void)hipStreamSynchronize(sp->stream3);
       if (sp->copy) (void)hipStreamSynchronize(sp->copy);
     }
     for (hipStream_t st : c->side_all) (void)hipStreamSynchronize(st);
@@ -1098,7 +976,6 @@ void hsv_shutdown(void) {
       Slot &s = *sp;
       if (s.stream) (void)hipStreamDestroy(s.stream);
       if (s.stream2) (void)hipStreamDestroy(s.stream2);
-      if (s.stream3) (void)hipStreamDestroy(s.stream3);
       if (s.copy) (void)hipStreamDestroy(s.copy);
       for (hipEvent_t &ev : s.ev) {
         if (ev) (void)hipEventDestroy(ev);
@@ -1112,10 +989,10 @@ void hsv_shutdown(void) {
       s.ws_cap = 0;
       if (s.d_buf) (void)hipFree(s.d_buf);
       if (s.h_buf) (void)hipHostFree(s.h_buf);
-      if (s.h_stream) (void)hipHostFree(s.h_stream);
-      s.h_stream = nullptr;
-      s.h_stream_cap = 0;
-      s.stream = s.stream2 = s.stream3 = nullptr;
+      if (s.h_sync) (void)hipHostFree(s.h_sync);
+      s.h_sync = s.h_sync_dev = nullptr;
+      s.h_sync_cap = 0;
+      s.stream = s.stream2 = nullptr;
       s.d_buf = s.h_buf = s.h_buf_dev = nullptr;
       s.d_cap = s.h_cap = 0;
     }
@@ -1137,7 +1014,9 @@ int hsv_device_count(void) {
 
 const char *hsv_last_error(void) { return t_last_error.c_str(); }
 
-const char *hsv_version(void) { return "hsv 0.2.0 (gfx950)"; }
+const char *hsv_version(void) { return "hsv 0.3.0 (gfx950)"; }
+
+int hsv_abi_version(void) { return HSV_ABI_VERSION; }
 
 // Measurement/test hook (exported by libhsv_test.so only): pick the kernel variant.
 int hsvi_set_variant(int v) {

@@ -210,20 +210,12 @@ __device__ uint64_t g_qc_clk[kQcClkWaves][kQcClkSlots];
   } while (0)
 #endif
 
-// HSV_COMB_STAGE_INPUTS=1 (measurement builds only): the block's inputs read
-// once into LDS by wave 0 before the entry barrier, instead of each wave
-// reading its own vote words from the pinned staging over PCIe.  Per-wave
-// stamps (tools/qc_wave_clocks.py, profiles/r04h_qcclk.txt) put every role of
-// the C3 kernel (167 blocks) 4.4-4.6 us behind C1 (one block), with one wave
-// per SIMD and the shader clock 4 % lower; staging was to test whether the
-// redundant PCIe reads cause it.  They do not: staged, C3 keeps the same
-// penalty, and the barrier ahead of every wave costs C1 3.5 us
-// (profiles/r04i_qc_ab_stage.txt: C1 / C3 0.0431 / 0.0584 against 0.0396 /
-// 0.0554 ms).
-#ifndef HSV_COMB_STAGE_INPUTS
-#define HSV_COMB_STAGE_INPUTS 0
-#endif
-constexpr bool kStageInputs = HSV_COMB_STAGE_INPUTS != 0;
+// Reading each block's inputs once into LDS before the entry barrier
+// (instead of each wave reading its own vote words from the pinned staging)
+// was measured and dropped in round 4: per-wave stamps put every role of the
+// C3 kernel 4.4-4.6 us behind C1 either way, and the barrier ahead of every
+// wave cost C1 3.5 us (profiles/r04i_qc_ab_stage.txt).  The resident service
+// does stage its request in LDS, read in one load by wave 0 (below).
 
 // one vote's words: the key A, the signature (R, s) and the message digest M
 // (sp / gp: the vote's signature and digest, in global memory or LDS)
@@ -270,47 +262,22 @@ __device__ __forceinline__ void comb_quad_block(const uint32_t *__restrict__ key
                                                 uint32_t *__restrict__ done, uint32_t blk) {
   __shared__ uint32_t r_x[kFusedVotes][kFeLimbs], r_y[kFusedVotes][kFeLimbs], r_fl[kFusedVotes];
   __shared__ uint32_t k_rec[kFusedVotes][9], k_ready;
-  __shared__ uint4 in_sig[kStageInputs ? kFusedVotes : 1][4], in_msg[kStageInputs ? kFusedVotes : 1][2];
-  __shared__ uint32_t in_kidx[kStageInputs ? kFusedVotes : 1];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint32_t base = blk * kFusedVotes;
   HSV_QC_CLK(0);
   // vote v of the block reads vote min(base + v, m - 1): the last block's
   // spare slots repeat the batch's last vote and write no flag
   auto vote_of = [&](uint32_t v) { return base + v < m ? base + v : m - 1u; };
-  if constexpr (kStageInputs) {
-    if (wave == 0u) {  // one 16-byte read per lane: 4 per signature, 2 per digest, then the key indices
-      constexpr uint32_t V = kFusedVotes;
-      for (uint32_t t = lane; t < 7u * V; t += 64u) {
-        if (t < 4u * V) {
-          in_sig[t >> 2][t & 3u] = reinterpret_cast<const uint4 *>(sig + (uint64_t)vote_of(t >> 2) * sig_stride)[t & 3u];
-        } else if (t < 6u * V) {
-          const uint32_t v = (t - 4u * V) >> 1, c = t & 1u;
-          in_msg[v][c] = reinterpret_cast<const uint4 *>(msg + (uint64_t)vote_of(v) * msg_stride)[c];
-        } else {
-          in_kidx[t - 6u * V] = key_idx[vote_of(t - 6u * V)];
-        }
-      }
-    }
-  }
-  if constexpr (kHashWave || kStageInputs) {
+  if constexpr (kHashWave) {
     // LDS keeps the last block's flag: cleared before any wave can look
-    if (kHashWave && threadIdx.x == 0) k_ready = 0u;
+    if (threadIdx.x == 0) k_ready = 0u;
     __syncthreads();
     HSV_QC_CLK(1);
   }
-  auto vote_sig = [&](uint32_t v) -> const uint4 * {
-    if constexpr (kStageInputs) return in_sig[v];
-    else return reinterpret_cast<const uint4 *>(sig + (uint64_t)vote_of(v) * sig_stride);
-  };
-  auto vote_msg = [&](uint32_t v) -> const uint4 * {
-    if constexpr (kStageInputs) return in_msg[v];
-    else return reinterpret_cast<const uint4 *>(msg + (uint64_t)vote_of(v) * msg_stride);
-  };
-  auto vote_kidx = [&](uint32_t v) -> uint32_t {
-    if constexpr (kStageInputs) return in_kidx[v];
-    else return key_idx[vote_of(v)];
-  };
+  // (the resident service passes key_idx / sig / msg pointing into its LDS copy of the request)
+  auto vote_sig = [&](uint32_t v) { return reinterpret_cast<const uint4 *>(sig + (uint64_t)vote_of(v) * sig_stride); };
+  auto vote_msg = [&](uint32_t v) { return reinterpret_cast<const uint4 *>(msg + (uint64_t)vote_of(v) * msg_stride); };
+  auto vote_kidx = [&](uint32_t v) -> uint32_t { return key_idx[vote_of(v)]; };
   if constexpr (kHashWave) {
     if (wave == kHashWaveIdx) {
       // one lane per vote hashes (lanes 0..kFusedVotes-1); the rest of the
@@ -529,41 +496,51 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
 }
 
 // The resident latency service (HSV_QC_RESIDENT=1, csrc/hsv_committee_api.cpp):
-// one block that stays on its CU and answers requests of at most kFusedVotes
-// votes posted in coherent pinned memory, instead of a launch per request
-// (a launch with marker sync costs 5.95 us round trip against 1.54 us for a
-// resident wave, profiles/r04zz_resident_latency.txt).  Thread 0 polls the
-// doorbell with relaxed system-scope loads and s_sleep; the block runs the
-// request through comb_quad_block, and thread 0 releases the flags and sets
-// done = the request's sequence number.  It leaves on the stop word or after
-// idle_ticks (100 MHz) without a request, and clears `alive` as it goes, so
-// no grid outlives its process; the host relaunches it on the next request.
-// a relaxed system-scope load: a vector load, never the scalar cache, which
-// would keep an earlier request's header
+// one block that stays on its CU and answers requests of at most
+// kResidentVotes votes posted in coherent pinned memory (QcResidentReq,
+// hsv_internal.h), instead of a launch per request: a block of this shape
+// answers a doorbell in 2.2 us against 5.8 us for a launch with marker sync
+// (profiles/r05a_aql_latency.txt, tools/resident_latency.hip).  Per request:
+//   * wave 0 polls the doorbell (relaxed system-scope loads, s_sleep between
+//     polls); on a new seq every lane performs a system-scope acquire, then
+//     the wave reads the whole request body in ONE vector load (64 lanes x 8
+//     bytes) into LDS.  Round 4's form read eight header words one by one
+//     with dependent LDS stores between them -- eight PCIe round trips, the
+//     ~10 us the service lost against a launch -- and its only acquire was
+//     an agent-scope fence after those reads;
+//   * the block validates the header before it dereferences anything: 1 <= m
+//     <= kResidentVotes, non-null committee arrays, 1 <= nkeys <= 2^20.  An
+//     invalid request is answered with fault[2] = 1 and no verification
+//     (HSV_ERR_DEVICE_FAULT on the host), never with a memory access;
+//   * the votes' key indices, signatures and digests are then read from LDS by
+//     comb_quad_block, and thread 0 answers done = seq after a release.
+// It leaves on the stop word or after idle_ticks (100 MHz) without a request,
+// and clears `alive` as it goes, so no grid outlives its process; the host
+// relaunches it on the next request.
 template <class T>
-__device__ __forceinline__ T req_load(T *p) {
+__device__ __forceinline__ T req_load(T *p) {  // a vector load, never the scalar cache
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+constexpr uint32_t kResidentMaxKeys = 1u << 20;  // hsv_committee_create's bound and above the auto cache's
+
 __global__ void __launch_bounds__(kFusedThreads) hsv_comb_resident_kernel(QcResidentReq *req, uint64_t idle_ticks) {
-  __shared__ uint32_t cmd_seq, cmd_stop, h_m, h_nkeys, h_inject;
-  __shared__ uint64_t h_msg_stride;
-  __shared__ const uint8_t *h_pks;
-  __shared__ const uint8_t *h_key_flags;
-  __shared__ const uint32_t *const *h_key_tables;
-  __shared__ const uint32_t *h_btable;
+  static_assert(sizeof(QcResidentBody) == 64 * 8, "one 8-byte word per lane");
+  __shared__ __attribute__((aligned(16))) uint64_t body[64];
+  __shared__ uint32_t cmd_seq, cmd_stop;
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   uint32_t last = 0;
-  if (threadIdx.x == 0) {
-    last = __hip_atomic_load(&req->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&req->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (wave == 0u) {
+    last = req_load(&req->seq);
+    if (lane == 0u) __hip_atomic_store(&req->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   for (;;) {
-    if (threadIdx.x == 0) {
+    if (wave == 0u) {
       const uint64_t t0 = wall_clock64();
       uint32_t sq = last, stop = 0;
-      for (;;) {
-        sq = __hip_atomic_load(&req->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        stop = __hip_atomic_load(&req->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      for (;;) {  // every lane polls the same word: one request per poll
+        sq = req_load(&req->seq);
+        stop = req_load(&req->stop);
         if (sq != last || stop) break;
         if (wall_clock64() - t0 > idle_ticks) {
           stop = 1u;
@@ -571,30 +548,32 @@ __global__ void __launch_bounds__(kFusedThreads) hsv_comb_resident_kernel(QcResi
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      cmd_seq = sq;
-      cmd_stop = stop;
       last = sq;
-      if (!stop) {  // the request header, read once per request (the host wrote it before seq)
-        h_m = req_load(&req->m);
-        h_nkeys = req_load(&req->nkeys);
-        h_inject = req_load(&req->inject);
-        h_msg_stride = req_load(&req->msg_stride);
-        h_pks = (const uint8_t *)req_load((uint64_t *)&req->pks);
-        h_key_flags = (const uint8_t *)req_load((uint64_t *)&req->key_flags);
-        h_key_tables = (const uint32_t *const *)req_load((uint64_t *)&req->key_tables);
-        h_btable = (const uint32_t *)req_load((uint64_t *)&req->btable);
+      if (!stop) {
+        // the body the host wrote before its release store of seq
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        body[lane] = req_load(reinterpret_cast<uint64_t *>(&req->body) + lane);
+      }
+      if (lane == 0u) {
+        cmd_seq = sq;
+        cmd_stop = stop;
       }
     }
     __syncthreads();
     if (cmd_stop) break;
-    // no vector-cache line of an earlier request survives into this one (the
-    // request area is coherent host memory, which L2 does not keep)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const uint32_t sq = cmd_seq;
-    comb_quad_block(req->key_idx, &req->sig[0][0], 64, &req->msg[0][0], h_msg_stride, h_m, h_pks, h_key_flags,
-                    h_nkeys, h_key_tables, h_btable, req->flags, h_inject, req->fault, nullptr, 0u);
-    __syncthreads();  // every wave past its reads of this request and (wave 0) its flag stores
+    const QcResidentBody &b = *reinterpret_cast<const QcResidentBody *>(body);
+    const uint32_t m = b.m, nkeys = b.nkeys;
+    const bool valid = m >= 1u && m <= (uint32_t)kResidentVotes && m <= (uint32_t)kFusedVotes && nkeys >= 1u &&
+                       nkeys <= kResidentMaxKeys && b.pks && b.key_flags && b.key_tables && b.btable;
+    if (valid) {  // block-uniform: every wave takes the same branch
+      comb_quad_block(b.key_idx, reinterpret_cast<const uint8_t *>(b.sig), 64,
+                      reinterpret_cast<const uint8_t *>(b.msg), b.msg_per_vote ? 32 : 0, m, b.pks, b.key_flags,
+                      nkeys, b.key_tables, b.btable, req->flags, b.inject, req->fault, nullptr, 0u);
+    }
+    __syncthreads();  // every wave past its reads of this request (LDS included) and its flag stores
     if (threadIdx.x == 0) {
+      if (!valid) __hip_atomic_store(&req->fault[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __atomic_thread_fence(__ATOMIC_RELEASE);
       __hip_atomic_store(&req->done, sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -733,7 +712,9 @@ extern "C" hipError_t hsv_launch_comb_resident(QcResidentReq *d_req, uint64_t id
   return hipGetLastError();
 }
 
-extern "C" uint32_t hsv_comb_resident_votes(void) { return (uint32_t)hsv::kFusedVotes; }
+extern "C" uint32_t hsv_comb_resident_votes(void) {
+  return (uint32_t)std::min<int>(hsv::kFusedVotes, kResidentVotes);
+}
 
 extern "C" uint32_t hsv_comb_marker_blocks(uint32_t m) {
   return m <= kCombQuadMax ? (m + hsv::kFusedVotes - 1) / hsv::kFusedVotes : 0u;

@@ -132,13 +132,19 @@ struct CommitteeDev {
 // ---- resident latency service (HSV_QC_RESIDENT=1, opt-in) --------------------------
 // One block of hsv_comb_resident_kernel stays on a CU of the home device and
 // answers requests of at most hsv_comb_resident_votes() votes posted in
-// coherent pinned memory: 1.54 us round trip against 5.95 us for a launch with
-// marker sync (profiles/r04zz_resident_latency.txt).  It holds that CU while it
-// runs, hence opt-in.  The kernel leaves on the stop word (hsv_shutdown, and an
-// atexit handler registered at the first start) or after kResidentIdle without
-// a request; the next request relaunches it.  A request unanswered within
-// kResidentWait ends the service for the process, and the call takes the
-// launch path, so the service can cost latency but never a verdict.
+// coherent pinned memory (QcResidentReq): 2.2 us round trip for a block of its
+// shape against 5.8 us for a launch with marker sync
+// (profiles/r05a_aql_latency.txt).  It holds that CU while it runs, hence
+// opt-in.  The kernel leaves on the stop word (hsv_shutdown, an atexit
+// handler registered at the first start, and resident_quiesce() before the
+// library frees device or pinned memory: on ROCm hipFree / hipHostFree wait
+// for every grid on the device, the resident one included) or after
+// kResidentIdle without a request; the next request relaunches it.  A request
+// unanswered within kResidentWait ends the service for the process, and the
+// call takes the launch path, so the service can cost latency but never a
+// verdict.  An application that synchronises the whole device
+// (hipDeviceSynchronize, torch.cuda.synchronize) waits for the idle exit, up to
+// kResidentIdle after the last request.
 constexpr uint64_t kResidentIdleTicks = 100000000ull;  // 1 s of the 100 MHz clock
 constexpr auto kResidentWait = std::chrono::milliseconds(50);
 constexpr int kResidentUnavailable = 1;
@@ -152,6 +158,7 @@ struct ResidentQc {
   uint32_t seq = 0;
   bool broken = false;
   bool atexit_registered = false;
+  uint64_t posted = 0, answered = 0;  // requests posted / answered (hsvi_resident_counts)
 };
 
 ResidentQc &RQ() {
@@ -230,29 +237,31 @@ int resident_ensure_locked(ResidentQc &r, int device) {
 }
 
 // One request of at most hsv_comb_resident_votes() votes: HSV_OK, an error
-// (HSV_ERR_DEVICE_FAULT from the self-checks), or kResidentUnavailable (the
-// caller launches instead).
+// (HSV_ERR_DEVICE_FAULT from the self-checks or the kernel's request check),
+// or kResidentUnavailable (the caller launches instead).
 int resident_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t *sig, size_t sig_stride,
                  const uint8_t *msg, size_t msg_stride, size_t m, uint8_t *flags_out, const uint32_t *btable) {
   ResidentQc &r = RQ();
   std::lock_guard<std::mutex> lk(r.mu);
   if (resident_ensure_locked(r, cd.device) != HSV_OK) return kResidentUnavailable;
   QcResidentReq &q = *r.h;
-  q.m = (uint32_t)m;
-  q.nkeys = cd.n;
-  q.inject = (uint32_t)hsvi_inject_mode();
-  q.msg_stride = msg_stride ? 32 : 0;
-  q.pks = cd.d_pks;
-  q.key_flags = cd.d_kflags;
-  q.key_tables = cd.d_tabptr;
-  q.btable = btable;
-  for (size_t i = 0; i < m; ++i) {
-    q.key_idx[i] = key_idx[i];
-    std::memcpy(q.sig[i], sig + i * sig_stride, 64);
-    if (msg_stride) std::memcpy(q.msg[i], msg + i * msg_stride, 32);
-    q.flags[i] = 0;  // an unwritten flag reads as a rejection
+  QcResidentBody &b = q.body;
+  b.m = (uint32_t)m;
+  b.nkeys = cd.n;
+  b.inject = (uint32_t)hsvi_inject_mode();
+  b.msg_per_vote = msg_stride ? 1u : 0u;
+  b.pks = cd.d_pks;
+  b.key_flags = cd.d_kflags;
+  b.key_tables = cd.d_tabptr;
+  b.btable = btable;
+  const size_t mm = std::min<size_t>(m, kResidentVotes);  // m > kResidentVotes is the kernel's to refuse
+  for (size_t i = 0; i < mm; ++i) {
+    b.key_idx[i] = key_idx[i];
+    std::memcpy(b.sig[i], sig + i * sig_stride, 64);
+    if (msg_stride) std::memcpy(b.msg[i], msg + i * msg_stride, 32);
   }
-  if (!msg_stride) std::memcpy(q.msg[0], msg, 32);
+  if (!msg_stride) std::memcpy(b.msg[0], msg, 32);
+  std::memset(q.flags, 0, sizeof(q.flags));  // an unwritten flag reads as a rejection
   std::memset(q.fault, 0, sizeof(q.fault));
   call_mark(HSV_MARK_STAGED);
   // One retry: the kernel may leave on its idle timer just as a request is
@@ -261,6 +270,7 @@ int resident_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t 
   for (int attempt = 0;; ++attempt) {
     const uint32_t sq = ++r.seq == 0 ? ++r.seq : r.seq;  // never 0
     __atomic_store_n(&q.seq, sq, __ATOMIC_RELEASE);      // everything above is visible first
+    ++r.posted;
     call_mark(HSV_MARK_LAUNCH);
     const auto t0 = std::chrono::steady_clock::now();
     bool answered = true;
@@ -279,13 +289,62 @@ int resident_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t 
     r.broken = true;
     return kResidentUnavailable;
   }
+  ++r.answered;
   call_mark(HSV_MARK_SYNC);
-  const int rc = check_faults(reinterpret_cast<const uint8_t *>(q.fault), "committee verify (resident)");
+  uint32_t fw[3];
+  std::memcpy(fw, q.fault, sizeof(fw));
+  if (fw[2])
+    return fail(HSV_ERR_DEVICE_FAULT, "committee verify (resident): the kernel refused the request header");
+  const int rc = check_faults(reinterpret_cast<const uint8_t *>(fw), "committee verify (resident)");
   if (rc != HSV_OK) return rc;
   std::memcpy(flags_out, q.flags, m);
   call_mark(HSV_MARK_DONE);
   return HSV_OK;
 }
+
+}  // namespace
+
+// Stop the resident kernel before the library frees device or pinned memory
+// (hipFree / hipHostFree wait for every grid on the device); the next request
+// relaunches it.  A no-op when the service never ran.
+void resident_quiesce() {
+  ResidentQc &r = RQ();
+  if (!r.h) return;  // unlocked peek: the service is only ever started, never unset
+  std::lock_guard<std::mutex> lk(r.mu);
+  if (__atomic_load_n(&r.h->alive, __ATOMIC_ACQUIRE) == 1u) resident_stop_locked(r);
+}
+
+void resident_counts(uint64_t *posted, uint64_t *answered) {
+  ResidentQc &r = RQ();
+  std::lock_guard<std::mutex> lk(r.mu);
+  if (posted) *posted = r.posted;
+  if (answered) *answered = r.answered;
+}
+
+// Test hook: one resident request whose header claims m votes (0 or above
+// the limit: the kernel must refuse it with HSV_ERR_DEVICE_FAULT, never read
+// through it); needs the automatic cache's committee (nkeys, tables).
+int resident_post_bad(uint32_t m) {
+  if (!resident_enabled()) return fail(HSV_ERR_INVALID_ARG, "HSV_QC_RESIDENT is off");
+  int rc = ensure_init();
+  if (rc != HSV_OK) return rc;
+  DevCtx &c = ctx(home_device());
+  DeviceGuard guard(c.device);
+  rc = ensure_btable(c);
+  if (rc != HSV_OK) return rc;
+  const uint32_t idx[1] = {0};
+  uint8_t sig[64] = {0}, msg[32] = {0}, flags[16];
+  CommitteeDev cd;
+  cd.device = c.device;
+  cd.n = 1;
+  cd.d_pks = reinterpret_cast<const uint8_t *>(c.d_btable);  // valid device memory, never read: m is refused
+  cd.d_kflags = cd.d_pks;
+  cd.d_tabptr = reinterpret_cast<const uint32_t *const *>(c.d_btable);
+  rc = resident_run(cd, idx, sig, 64, msg, 0, m, flags, c.d_btable);
+  return rc == kResidentUnavailable ? fail(HSV_ERR_HIP, "resident service unavailable") : rc;
+}
+
+namespace {
 
 // Votes by member index on the committee's device, through a slot of that
 // device: the kernels read the pinned staging buffer directly for batches of
@@ -314,8 +373,7 @@ int committee_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t
     const size_t msg_bytes = msg_stride ? k * 32 : 32;
     const size_t flag_off = msg_off + round_up(msg_bytes, kAlign);
     const size_t fault_off = flag_off + round_up(k, kAlign);
-    const size_t done_off = fault_off + kAlign;  // completion markers (marker sync), one word per block
-    const size_t total = done_off + round_up((size_t)hsv_comb_marker_blocks((uint32_t)k) * 4 + 4, kAlign);
+    const size_t total = fault_off + kAlign;
     rc = slot_prepare(s, total, total);
     if (rc != HSV_OK) return rc;
     uint8_t *h = s.h_buf;
@@ -326,42 +384,51 @@ int committee_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t
       for (size_t i = 0; i < k; ++i) std::memcpy(h + sig_off + i * 64, sig + (base + i) * sig_stride, 64);
     }
     std::memcpy(h + msg_off, msg + base * msg_stride, msg_bytes);
-    // unwritten flags read as rejections; self-check words start at zero
-    std::memset(h + flag_off, 0, k);
-    std::memset(h + fault_off, 0, kFaultBytes);
-    call_mark(HSV_MARK_STAGED);
-    void *hd = nullptr;
-    uint8_t *dbuf = s.d_buf;
-    static const size_t zc_max = [] {  // HSV_COMMITTEE_ZC_MAX: measurement switch
-      const char *v = std::getenv("HSV_COMMITTEE_ZC_MAX");
-      return v ? (size_t)std::atoll(v) : kZeroCopyMax;
-    }();
-    const bool zero_copy = k <= zc_max && (hd = s.h_buf_dev) != nullptr;
-    // The zero-copy latency form marks each block done in pinned memory and the
-    // host spins on the markers instead of hipStreamSynchronize (see the
-    // kernel): the flags are final once every block has released them, and
-    // the kernel's completion signal comes several microseconds later.  Same
-    // box, alternating processes (profiles/r04b_qc_ab_marker.txt): C1
-    // 0.0444 -> 0.0394 ms, C3 0.0587 -> 0.0559 ms, one verify_strict 0.0443 ->
-    // 0.0395 ms.  HSV_QC_SYNC=stream (measurement switch) restores the sync.
-    static const bool marker_sync = [] {
-      const char *v = std::getenv("HSV_QC_SYNC");
-      return !(v && std::strcmp(v, "stream") == 0);
-    }();
-    const uint32_t nmark = zero_copy && marker_sync ? hsv_comb_marker_blocks((uint32_t)k) : 0u;
-    volatile uint32_t *marks = reinterpret_cast<volatile uint32_t *>(h + done_off);
-    for (uint32_t b = 0; b < nmark; ++b) marks[b] = 0u;
+    // The zero-copy latency form (<= kZeroCopyMax votes) reads the inputs from
+    // the pinned staging through its device mapping (copying them to HBM first
+    // made C1 0.0444 -> 0.0498 ms and C3 0.0592 -> 0.0689 ms,
+    // profiles/r03zz7_qc_ab_zc.txt) and writes its flags, self-check words and
+    // one completion marker per block into the slot's coherent sync region;
+    // the host spins on the markers instead of hipStreamSynchronize: the flags
+    // are final once every block has released them, several microseconds
+    // before the kernel's completion signal (same box, alternating processes,
+    // profiles/r04b_qc_ab_marker.txt: C1 0.0444 -> 0.0394 ms, C3 0.0587 ->
+    // 0.0559 ms, one verify_strict 0.0443 -> 0.0395 ms).
+    const bool zero_copy = k <= kZeroCopyMax && s.h_buf_dev != nullptr;
+    uint8_t *flags_h, *flags_d, *fault_h, *fault_d;
+    uint32_t nmark = 0;
+    volatile uint32_t *marks = nullptr;
+    uint32_t *marks_d = nullptr;
     if (zero_copy) {
-      dbuf = static_cast<uint8_t *>(hd);
+      nmark = hsv_comb_marker_blocks((uint32_t)k);
+      const size_t sf = round_up(k, kAlign), sm = sf + kAlign, need = sm + round_up((size_t)nmark * 4 + 4, kAlign);
+      rc = slot_sync_region(s, need);
+      if (rc != HSV_OK) return rc;
+      flags_h = s.h_sync;
+      flags_d = s.h_sync_dev;
+      fault_h = s.h_sync + sf;
+      fault_d = s.h_sync_dev + sf;
+      marks = reinterpret_cast<volatile uint32_t *>(s.h_sync + sm);
+      marks_d = reinterpret_cast<uint32_t *>(s.h_sync_dev + sm);
+      for (uint32_t b = 0; b < nmark; ++b) marks[b] = 0u;
     } else {
-      const hipError_t e = hipMemcpyAsync(s.d_buf, h, fault_off + kFaultBytes, hipMemcpyHostToDevice, s.stream);
-      if (e != hipSuccess) return hip_fail("hipMemcpyAsync H2D", e);
+      flags_h = h + flag_off;
+      flags_d = s.d_buf + flag_off;
+      fault_h = h + fault_off;
+      fault_d = s.d_buf + fault_off;
     }
-    hipError_t e = hsv_launch_comb_verify(reinterpret_cast<const uint32_t *>(dbuf + idx_off), dbuf + sig_off, 64,
-                                          dbuf + msg_off, msg_stride ? 32 : 0, (uint32_t)k, cd.d_pks, cd.d_kflags, cd.n,
-                                          cd.d_tabptr, c.d_btable, dbuf + flag_off,
-                                          reinterpret_cast<uint32_t *>(dbuf + fault_off),
-                                          nmark ? reinterpret_cast<uint32_t *>(dbuf + done_off) : nullptr, s.stream);
+    // unwritten flags read as rejections; self-check words start at zero
+    std::memset(flags_h, 0, k);
+    std::memset(fault_h, 0, kFaultBytes);
+    call_mark(HSV_MARK_STAGED);
+    const uint8_t *dbuf = zero_copy ? s.h_buf_dev : s.d_buf;
+    hipError_t e = hipSuccess;
+    if (!zero_copy) e = hipMemcpyAsync(s.d_buf, h, fault_off + kFaultBytes, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess)
+      e = hsv_launch_comb_verify(reinterpret_cast<const uint32_t *>(dbuf + idx_off), dbuf + sig_off, 64,
+                                 dbuf + msg_off, msg_stride ? 32 : 0, (uint32_t)k, cd.d_pks, cd.d_kflags, cd.n,
+                                 cd.d_tabptr, c.d_btable, flags_d, reinterpret_cast<uint32_t *>(fault_d), marks_d,
+                                 s.stream);
     if (e == hipSuccess && !zero_copy)
       e = hipMemcpyAsync(h + flag_off, s.d_buf + flag_off, fault_off + kFaultBytes - flag_off, hipMemcpyDeviceToHost,
                          s.stream);
@@ -388,9 +455,9 @@ int committee_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t
     call_mark(HSV_MARK_SYNC);
     if (e != hipSuccess) return hip_fail("committee verify launch", e);
     if (es != hipSuccess) return hip_fail("hipStreamSynchronize", es);
-    rc = check_faults(h + fault_off, "committee verify");
+    rc = check_faults(fault_h, "committee verify");
     if (rc != HSV_OK) return rc;
-    std::memcpy(flags_out + base, h + flag_off, k);
+    std::memcpy(flags_out + base, flags_h, k);
     call_mark(HSV_MARK_DONE);
   }
   return HSV_OK;
@@ -478,6 +545,7 @@ int hsv_committee_create(const uint8_t *pks, size_t n, hsv_committee **out) {
 
 void hsv_committee_destroy(hsv_committee *cm) {
   if (!cm) return;
+  resident_quiesce();
   DeviceGuard guard(cm->dev.device);
   if (cm->d_pks) (void)hipFree(cm->d_pks);
   if (cm->d_kflags) (void)hipFree(cm->d_kflags);
@@ -585,6 +653,7 @@ struct AutoStore {  // append-only device storage, freed with the last view usin
   hipStream_t stream = nullptr;  // builds only
   std::vector<uint32_t *> blocks;
   ~AutoStore() {
+    resident_quiesce();
     DeviceGuard guard(device);
     if (stream) (void)hipStreamDestroy(stream);
     for (uint32_t *b : blocks) (void)hipFree(b);

@@ -55,8 +55,7 @@ inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 struct Slot {
   std::mutex mu;
   hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;  // second and third compute streams of large host batches
-  hipStream_t stream3 = nullptr;
+  hipStream_t stream2 = nullptr;  // second compute stream of large host batches
   hipStream_t copy = nullptr;     // host-to-device stream of large host batches
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // staged[2], unused, joined[2] (run_pipelined)
   uint8_t *d_ws[3] = {nullptr, nullptr, nullptr};  // launch workspaces of the compute streams (run_pipelined)
@@ -66,11 +65,14 @@ struct Slot {
   uint8_t *h_buf = nullptr;
   uint8_t *h_buf_dev = nullptr;  // h_buf's device address (zero-copy launches), looked up once
   size_t h_cap = 0;
-  // pinned staging of the streamed host path (run_streamed), allocated
-  // coherent: the running kernel reads pieces the host publishes after it
-  // started, so the GPU must not serve them from a cache
-  uint8_t *h_stream = nullptr;
-  size_t h_stream_cap = 0;
+  // flag bytes, self-check words and completion markers of the committee
+  // latency form (committee_run), in COHERENT pinned memory: the host reads
+  // them while the kernel may still be running (marker sync), so they must not
+  // sit in the GPU's L2 -- correctness does not rest on the release fence's
+  // write-back of non-coherent lines (round-4 advice)
+  uint8_t *h_sync = nullptr;
+  uint8_t *h_sync_dev = nullptr;
+  size_t h_sync_cap = 0;
   size_t pipe_warm_n = 0;  // items of the last completed pipelined call (HSV_PIPE_NOCOPY)
 };
 
@@ -132,7 +134,9 @@ class SlotLease {
 // Stream and buffers of a slot (current device must be c.device).
 int slot_prepare(Slot &s, size_t dev_bytes, size_t host_bytes);
 int slot_stream2(Slot &s);
-int slot_pipeline(Slot &s, int compute_streams);  // stream2 (stream3), the copy stream, the events of run_pipelined
+int slot_pipeline(Slot &s);  // stream2, the copy stream, the events of run_pipelined
+// the slot's coherent sync region (Slot::h_sync) of at least `bytes`
+int slot_sync_region(Slot &s, size_t bytes);
 
 // Device self-check words (hsv_kernels.hip report_faults): two words per
 // launch, zeroed before it; non-zero after it -> HSV_ERR_DEVICE_FAULT.
@@ -184,6 +188,10 @@ int auto_committee_corrupt_tables();  // zero the cached tables of the automatic
 int auto_committee_try(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, size_t msg_stride, size_t n,
                        uint8_t *flags_out);
 void auto_committee_shutdown();
+// resident latency service (HSV_QC_RESIDENT=1, hsv_committee_api.cpp)
+void resident_quiesce();  // stop its kernel before a hipFree / hipHostFree
+void resident_counts(uint64_t *posted, uint64_t *answered);
+int resident_post_bad(uint32_t m);  // test hook: a request the kernel must refuse
 
 // The generic host-buffer path (hsv_capi.cpp): records at the given strides.
 int run_host(const uint8_t *pk, size_t pk_stride, const uint8_t *sig, size_t sig_stride, const uint8_t *msg,

@@ -15,8 +15,9 @@ extern "C" {
 // process's first committee-cache allocations, accepted a forged vote in 8 of
 // 16 runs of tests/native/crypto_tests.cpp; with this pool, 0 of 16
 // (tools/forgery_debug.sh).  HSV_WS_POOL=default
-// selects the default pool again in the measurement build (ALL_VARIANTS=1)
-// only; the product library always uses its own pool.
+// selects the default pool again in the measurement build (ALL_VARIANTS=1,
+// libhsv_all.so) only; the product library always uses its own pool and reads
+// no such variable.
 hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream);
 void hsv_ws_trim(void);  // hsv_shutdown: release the pools' free blocks
 
@@ -47,19 +48,6 @@ hipError_t hsv_launch_verify_ws(int variant, const uint8_t *pk, uint64_t pk_stri
                                 uint8_t *flags_out, uint32_t *strict_bits, const uint32_t *comb_b, uint32_t *fault,
                                 void *ws, size_t ws_cap, hipStream_t stream);
 size_t hsv_launch_ws_bytes(int variant, uint32_t n);
-// Streamed host batch (variant 21, >= 2^18 items from host buffers): ONE
-// persistent launch over n records that the host is still packing.  recs:
-// device view of the pinned records (rec_bytes 128 = pk|R|s|digest, or 96 with
-// shared_msg the device view of one shared digest); piece p (2^piece_log2
-// items) may be read once ready[p] != 0 (host-written, pinned); flags_out:
-// device view of n pinned flag bytes; fault: 3 device-visible words the
-// caller zeroed (curve check, canary, input timeout: max_polls polls of an
-// unready piece abort the launch).  ws: hsv_launch_stream_ws_bytes(n) bytes.
-hipError_t hsv_launch_verify_stream(const uint8_t *recs, uint32_t rec_bytes, const uint8_t *shared_msg, uint32_t n,
-                                    uint32_t piece_log2, const uint32_t *ready, uint8_t *flags_out,
-                                    const uint32_t *comb_b, uint32_t *fault, uint32_t max_polls, void *ws,
-                                    size_t ws_cap, hipStream_t stream);
-size_t hsv_launch_stream_ws_bytes(uint32_t n);
 // Fault injection (tests only; hsv_kernels.hip): the mode of the launches the
 // calling thread issues (thread-scoped, so one test's injection never reaches
 // another thread's calls); hsvi_set_inject returns the previous mode, or -1.
@@ -87,28 +75,37 @@ double hsv_launch_mad_peak(int device_cus);
 
 // ---- committee key cache (hsv_committee.hip) -----------------------------
 // Request block of the resident committee service (hsv_comb_resident_kernel,
-// csrc/hsv_committee.hip), in coherent pinned host memory: the host fills a
-// request and bumps `seq`; the kernel answers with `done` = seq.
-struct QcResidentReq {
-  uint32_t seq, stop, alive, done;       // doorbell, stop word, set while the kernel runs, completion
-  uint32_t m, nkeys, inject, pad0;       // votes (<= hsv_comb_resident_votes()), members, fault injection
-  uint64_t msg_stride;                   // 0: one shared digest in msg[0]; 32: a digest per vote
+// csrc/hsv_committee.hip), in coherent pinned host memory.  The host fills
+// `body` and the answer words, then bumps `seq` with a release store; the
+// kernel sees the new seq, performs a system-scope acquire, reads the whole
+// body in ONE vector load (64 lanes x 8 bytes), validates it, and answers
+// with `done` = seq after a release.  kResidentVotes votes at most.
+constexpr int kResidentVotes = 4;
+struct QcResidentBody {                  // 512 bytes, word offsets fixed (the kernel reads it raw)
+  uint32_t m, nkeys, inject, msg_per_vote;  // votes (1..kResidentVotes), members, fault injection, 0/1
   const uint8_t *pks;                    // the committee view's device arrays
   const uint8_t *key_flags;
   const uint32_t *const *key_tables;
   const uint32_t *btable;
-  uint32_t key_idx[16];
-  uint32_t fault[8];                     // self-check words (the launched form's layout)
+  uint32_t key_idx[kResidentVotes];      // word 12
+  uint32_t sig[kResidentVotes][16];      // word 16: R || s per vote
+  uint32_t msg[kResidentVotes][8];       // word 80: one digest per vote, or the shared digest in msg[0]
+  uint32_t spare[16];
+};
+static_assert(sizeof(QcResidentBody) == 512, "one 64-lane x 8-byte load");
+struct QcResidentReq {
+  uint32_t seq, stop, alive, done;       // doorbell, stop word, set while the kernel runs, completion
+  uint32_t pad0[12];
+  QcResidentBody body;
+  uint32_t fault[8];                     // [0..1] self-check words (launched form's layout), [2] invalid request
   uint8_t flags[16];
-  uint8_t sig[16][64];                   // R || s per vote
-  uint8_t msg[16][32];
 };
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 hipError_t hsv_launch_comb_resident(QcResidentReq *d_req, uint64_t idle_ticks, hipStream_t stream);
-uint32_t hsv_comb_resident_votes(void);  // votes one request may hold
+uint32_t hsv_comb_resident_votes(void);  // votes one request may hold (0: no service in this build)
 hipError_t hsv_launch_comb_build(const uint8_t *encs, uint32_t nkeys, uint32_t negate, uint32_t *tables,
                                  uint32_t *tmp, uint8_t *key_flags, hipStream_t stream);
 // key_tables[i]: device pointer to key i's comb table (hsv_comb_table_bytes)

@@ -507,155 +507,11 @@ hsv_verify_hp_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const u
 }
 
 // ---- streamed host batches (round 4) ---------------------------------------
-// A host-buffer batch of >= 2^18 items as ONE persistent launch that starts
-// before its inputs are all there.  The host packs the records into pinned
-// staging piece by piece (2^14 items) and marks each packed piece ready in a
-// pinned word; the kernel reads the records through the staging buffer's
-// device mapping (no copy engine, no chunk launches) and a wave that draws a
-// batch of a piece not yet packed polls that piece's word.  Each lane runs the
-// scalar prepass of its item (prep_scalars, record in the lane's slot of
-// prep_ws) and then the point pass, or the full-length path when the lattice
-// gave no short pair; the flags go straight to pinned memory.  So the batch
-// has one grid end instead of one per chunk, and the GPU starts on the first
-// piece instead of the first chunk's copy.
-// The poll is bounded: after max_polls unanswered polls (the host stopped
-// packing) the wave sets ctr->pad (abort), every wave leaves at its next
-// batch, and fault[2] tells the host the launch did not finish -- an error,
-// never a verdict and never a hang.
-// The poll is a RELAXED system-scope load: an acquire at system scope would
-// invalidate the XCD's L2 (buffer_inv sc0 sc1) at every batch, evicting the
-// B comb and the other waves' tables -- the first version read 12.1-13.1 ms
-// per 2^20 against 9.4 for the resident launch (profiles/r04b_host_api_ab.txt).
-// No acquire is needed: the records and the flag live in coherent (uncached,
-// fine-grained) pinned memory, the host publishes a piece only after its
-// streaming stores' fence, and the wave issues its record loads after the
-// flag's value decided the branch, at addresses it has not read before.
-__device__ __forceinline__ bool stream_piece_ready(const uint32_t *ready, uint32_t piece, HcCounters *ctr,
-                                                   uint32_t max_polls) {
-  for (uint32_t i = 0;; ++i) {
-    const uint32_t v = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(ready + piece, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-    if (v != 0u) return true;
-    const uint32_t ab =
-        __builtin_amdgcn_readfirstlane(__hip_atomic_load(&ctr->pad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    if (ab != 0u || i >= max_polls) {
-      if ((threadIdx.x & 63u) == 0u) atomicExch(&ctr->pad, 1u);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(32);
-  }
-}
-
-template <int WA, int WAVES, int CB>
-__global__ void __launch_bounds__(kBlock, WAVES)
-hsv_verify_stream_kernel(const uint8_t *__restrict__ recs, uint32_t rec_bytes, const uint8_t *__restrict__ shared_msg,
-                         uint32_t n, uint32_t piece_log2, const uint32_t *ready, uint8_t *__restrict__ flags_out,
-                         uint32_t *__restrict__ prep_ws, uint32_t nslots, uint4 *__restrict__ vt_ws,
-                         const uint32_t *__restrict__ comb_b, HcCounters *__restrict__ ctr,
-                         uint32_t *__restrict__ canary, uint32_t nonce, uint32_t inject, int lat_bits,
-                         uint32_t max_polls, uint32_t *__restrict__ fault) {
-  constexpr int kEnt = (1 << (WA - 1)) + 1;
-  // A wave's 64 records, copied from pinned memory in whole 1-KB runs (lane l
-  // reads 16-B chunks l, l + 64, ...): reading them lane by lane was 12 to 16
-  // scattered 16-B PCIe reads per item, request-rate bound.  Each wave owns
-  // its 8 KB of LDS (the waves take batches independently: no block barrier).
-  __shared__ uint4 stage[kBlock / 64][512];
-  uint4 *st = stage[threadIdx.x >> 6];
-  const uint32_t slot = blockIdx.x * kBlock + threadIdx.x;
-  GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)slot * vt_lane_uint4<WA>(), inject};
-  uint32_t *rec = prep_ws + slot;  // word j at rec[j * nslots]: a wave's loads of one word are one access
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t rc16 = rec_bytes / 16u;  // 16-B chunks per record (8, or 6 with a shared digest)
-  canary[slot] = nonce;
-  uint32_t bad = 0;
-  for (;;) {
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&ctr->next, 64u);
-    base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
-    if (base >= n) break;
-    if (!stream_piece_ready(ready, base >> piece_log2, ctr, max_polls)) {
-      bad |= 4u;
-      break;
-    }
-    if (inject == kInjectCanary) canary[slot] = ~nonce;
-    const uint32_t idx = base + lane;
-    const bool valid = idx < n;
-    const uint32_t li = (valid ? idx : n - 1u) - base;  // this lane's record in the wave's stage
-    {
-      const uint4 *src = reinterpret_cast<const uint4 *>(recs + (uint64_t)base * rec_bytes);
-      const uint32_t nch = (n - base < 64u ? n - base : 64u) * rc16;
-      for (uint32_t c = lane; c < 64u * rc16; c += 64u)
-        if (c < nch) st[c] = src[c];
-      __builtin_amdgcn_wave_barrier();
-    }
-    const uint4 *my = st + li * rc16;
-    // the digest: the record's last 32 bytes, or the one shared digest
-    auto load_msg = [&](uint32_t msgw[8]) {
-      uint4 m0, m1;
-      if (shared_msg) {
-        const uint4 *g = reinterpret_cast<const uint4 *>(shared_msg);
-        m0 = g[0];
-        m1 = g[1];
-      } else {
-        m0 = my[6];
-        m1 = my[7];
-      }
-      msgw[0] = m0.x; msgw[1] = m0.y; msgw[2] = m0.z; msgw[3] = m0.w;
-      msgw[4] = m1.x; msgw[5] = m1.y; msgw[6] = m1.z; msgw[7] = m1.w;
-    };
-    uint32_t meta;
-    {
-      uint32_t pkw[8], sigw[16], msgw[8];
-      load_msg(msgw);
-      HSV_UNROLL
-      for (int q = 0; q < 2; ++q) {
-        const uint4 v = my[q];
-        pkw[4 * q] = v.x; pkw[4 * q + 1] = v.y; pkw[4 * q + 2] = v.z; pkw[4 * q + 3] = v.w;
-      }
-      HSV_UNROLL
-      for (int q = 0; q < 4; ++q) {
-        const uint4 v = my[2 + q];
-        sigw[4 * q] = v.x; sigw[4 * q + 1] = v.y; sigw[4 * q + 2] = v.z; sigw[4 * q + 3] = v.w;
-      }
-      (void)prep_scalars<WA>(pkw, sigw, msgw, rec, nslots, lat_bits);
-      meta = rec[18ull * nslots];
-    }
-    // The two paths read what they need from the stage again instead of
-    // keeping the prepass's input words live: a divergent if/else runs both
-    // regions in turn, so a value the second region reads stays live through
-    // the first -- here through the whole point pass.
-    uint32_t f = 0;
-    if (!(meta & kPrepFallback)) {
-      uint32_t pkw[8], rw[8];
-      HSV_UNROLL
-      for (int q = 0; q < 2; ++q) {
-        const uint4 v = my[q], r = my[2 + q];  // pk | R: the record's first 64 bytes
-        pkw[4 * q] = v.x; pkw[4 * q + 1] = v.y; pkw[4 * q + 2] = v.z; pkw[4 * q + 3] = v.w;
-        rw[4 * q] = r.x; rw[4 * q + 1] = r.y; rw[4 * q + 2] = r.z; rw[4 * q + 3] = r.w;
-      }
-      f = verify_one_prepped<WA, CB>(pkw, rw, rec, nslots, meta, comb_b, vt);
-    } else {  // no short lattice pair: the full-length path
-      uint32_t pkw[8], sigw[16], msgw[8];
-      load_msg(msgw);
-      HSV_UNROLL
-      for (int q = 0; q < 2; ++q) {
-        const uint4 v = my[q];
-        pkw[4 * q] = v.x; pkw[4 * q + 1] = v.y; pkw[4 * q + 2] = v.z; pkw[4 * q + 3] = v.w;
-      }
-      HSV_UNROLL
-      for (int q = 0; q < 4; ++q) {
-        const uint4 v = my[2 + q];
-        sigw[4 * q] = v.x; sigw[4 * q + 1] = v.y; sigw[4 * q + 2] = v.z; sigw[4 * q + 3] = v.w;
-      }
-      f = verify_one_full_comb<WA, false, CB>(pkw, sigw, msgw, comb_b, vt);
-    }
-    bad |= ((f & kFault) ? 1u : 0u) | (canary[slot] != nonce ? 2u : 0u);
-    if (valid) flags_out[idx] = (uint8_t)f;
-    __builtin_amdgcn_wave_barrier();  // every lane is done with the stage before the next batch's copy
-  }
-  report_faults(fault, bad);
-  if (bad & 4u) fault[2] = 1u;
-}
+// (Round 4 also had a streamed host form here: one persistent launch reading
+// the records through the pinned staging's device mapping while the host was
+// still packing them.  It measured slower than the chunked copy pipeline,
+// 11.7 against 9.9 ms per 2^20 (profiles/r04d_host_api_ab.txt), and was
+// removed from the library in round 5; it is in git history at 394d4d2.)
 
 // ---- latency form for small batches: two lanes per item ------------------
 // A lone wave issues one VALU instruction per 4 clocks whatever its lane
@@ -1342,59 +1198,6 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
   return e != hipSuccess ? e : ef;
 }
 
-// The streamed host-batch launch (hsv_verify_stream_kernel).  Workspace: the
-// per-lane tables | counters (256 B) | canaries | prepass records of every
-// lane slot (kPrepWords words each).  With ws_need set, only the size.
-template <int WA, int WAVES, int CB>
-hipError_t launch_stream(const uint8_t *recs, uint32_t rec_bytes, const uint8_t *shared_msg, uint32_t n,
-                         uint32_t piece_log2, const uint32_t *ready, uint8_t *flags_out, const uint32_t *comb_b,
-                         uint32_t *fault, uint32_t max_polls, void *ws_in, size_t ws_cap, hipStream_t stream,
-                         size_t *ws_need = nullptr) {
-  const void *kern = reinterpret_cast<const void *>(hsv::hsv_verify_stream_kernel<WA, WAVES, CB>);
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  static std::mutex mu;
-  static std::unordered_map<int, int> slots_per_dev;
-  int resident = 0;
-  {
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = slots_per_dev.find(dev);
-    if (it == slots_per_dev.end()) {
-      int bpc = 0, cus = 0;
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kern, hsv::kBlock, 0);
-      if (e != hipSuccess) return e;
-      e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      if (e != hipSuccess) return e;
-      it = slots_per_dev.emplace(dev, std::max(1, bpc) * std::max(1, cus)).first;
-    }
-    resident = it->second;
-  }
-  const uint32_t blocks_needed = (n + hsv::kBlock - 1) / hsv::kBlock;
-  const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(blocks_needed, (uint32_t)resident));
-  const size_t nslots = (size_t)grid * hsv::kBlock;
-  const size_t ws_bytes = nslots * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
-  const size_t canary_bytes = (nslots * sizeof(uint32_t) + 255) & ~(size_t)255;
-  const size_t prep_bytes = nslots * hsv::kPrepWords * sizeof(uint32_t);
-  const size_t need = ws_bytes + 256 + canary_bytes + prep_bytes;
-  if (ws_need) {
-    *ws_need = need;
-    return hipSuccess;
-  }
-  if (!ws_in || ws_cap < need || !fault || !comb_b) return hipErrorInvalidValue;
-  uint8_t *ws8 = static_cast<uint8_t *>(ws_in);
-  hsv::HcCounters *ctr = reinterpret_cast<hsv::HcCounters *>(ws8 + ws_bytes);
-  uint32_t *canary = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256);
-  uint32_t *prep = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256 + canary_bytes);
-  e = hipMemsetAsync(ctr, 0, sizeof(hsv::HcCounters), stream);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((hsv::hsv_verify_stream_kernel<WA, WAVES, CB>), dim3(grid), dim3(hsv::kBlock), 0, stream, recs,
-                     rec_bytes, shared_msg, n, piece_log2, ready, flags_out, prep, (uint32_t)nslots,
-                     reinterpret_cast<uint4 *>(ws_in), comb_b, ctr, canary, next_nonce(), t_inject, g_lat_bits.load(),
-                     max_polls, fault);
-  return hipGetLastError();
-}
-
 // Latency form (variant 21 below kPairMax items): one launch of the fused
 // kernel (prepass wave + two pair waves per 64 items).  Workspace: the pair
 // lanes' tables.  Round 1 ran the prepass and hsv_verify_pair_kernel as two
@@ -1441,25 +1244,14 @@ hipError_t launch_pair(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig
 // Row form (variant 21 at <= row_max() items): kRowItemsOf<RR> items per
 // block of four waves.  The workspace holds one full-length table and one canary per
 // row (the fallback path's tables; the row tables live in LDS).
-uint32_t row_max() {  // HSV_ROW_MAX: measurement switch (0: always the pair form)
-  static const uint32_t m = [] {
-    const char *v = std::getenv("HSV_ROW_MAX");
-    return v ? (uint32_t)std::atoi(v) : kRowMaxDefault;
-  }();
-  return m;
-}
+constexpr uint32_t row_max() { return kRowMaxDefault; }
 
-// Two rows per element up to row2_max() items (HSV_ROW2_MAX: measurement
-// switch, 0: one row per element): 3 items per block, so 768 items fill the
-// 256 CUs with one block each.
+// Two rows per element up to row2_max() items: 3 items per block, so 768
+// items fill the 256 CUs with one block each (0.169 / 0.205 ms at 64 items,
+// 0.175 / 0.210 at 768, 0.327 / 0.212 at 1024, two rows / one row,
+// profiles/r03zz4_row2_cutover.txt).
 constexpr uint32_t kRow2MaxDefault = 768;
-uint32_t row2_max() {
-  static const uint32_t m = [] {
-    const char *v = std::getenv("HSV_ROW2_MAX");
-    return v ? (uint32_t)std::atoi(v) : kRow2MaxDefault;
-  }();
-  return m;
-}
+constexpr uint32_t row2_max() { return kRow2MaxDefault; }
 
 template <int WA, int CB>
 hipError_t launch_row(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
@@ -1512,24 +1304,6 @@ extern "C" hipError_t hsv_launch_verify_ws(int variant, const uint8_t *pk, uint6
                               fault, stream, ws, ws_cap);
   return launch_hp<4, HSV_HP_WAVES, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits,
                                         comb_b, fault, stream, nullptr, ws, ws_cap);
-}
-
-extern "C" hipError_t hsv_launch_verify_stream(const uint8_t *recs, uint32_t rec_bytes, const uint8_t *shared_msg,
-                                               uint32_t n, uint32_t piece_log2, const uint32_t *ready,
-                                               uint8_t *flags_out, const uint32_t *comb_b, uint32_t *fault,
-                                               uint32_t max_polls, void *ws, size_t ws_cap, hipStream_t stream) {
-  if (n == 0) return hipSuccess;
-  if ((rec_bytes != 128u && rec_bytes != 96u) || (rec_bytes == 96u && !shared_msg) || piece_log2 < 6u)
-    return hipErrorInvalidValue;
-  return launch_stream<4, HSV_HP_WAVES, 16>(recs, rec_bytes, shared_msg, n, piece_log2, ready, flags_out, comb_b,
-                                             fault, max_polls, ws, ws_cap, stream);
-}
-
-extern "C" size_t hsv_launch_stream_ws_bytes(uint32_t n) {
-  size_t need = 0;
-  (void)launch_stream<4, HSV_HP_WAVES, 16>(nullptr, 128, nullptr, n, 14, nullptr, nullptr, nullptr, nullptr, 0,
-                                            nullptr, 0, nullptr, &need);
-  return need;
 }
 
 extern "C" size_t hsv_launch_ws_bytes(int variant, uint32_t n) {

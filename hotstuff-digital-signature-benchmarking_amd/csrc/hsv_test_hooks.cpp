@@ -21,5 +21,7 @@ int hsv_variant_available(int variant) { return hsvi_variant_available(variant);
 int hsv_num_variants(void) { return hsvi_num_variants(); }
 int hsv_set_virtual_shards(int k) { return hsvi_set_virtual_shards(k); }
 int hsv_test_pipe_nocopy(int on) { return hsvi_set_pipe_nocopy(on); }
+void hsv_test_resident_counts(uint64_t *posted, uint64_t *answered) { hsvh::resident_counts(posted, answered); }
+int hsv_test_resident_post_bad(uint32_t m) { return hsvh::resident_post_bad(m); }
 
 }  // extern "C"

@@ -46,6 +46,13 @@ HSV_API int hsv_set_virtual_shards(int k);
  * flags are the previous inputs' flags, so it never belongs in a product
  * library.  Returns the previous setting. */
 HSV_API int hsv_test_pipe_nocopy(int on);
+/* The resident latency service (HSV_QC_RESIDENT=1): requests posted to it and
+ * answered by it in this process so far (either pointer may be NULL). */
+HSV_API void hsv_test_resident_counts(uint64_t *posted, uint64_t *answered);
+/* Post one resident request whose header claims m votes (0, or above the
+ * service's limit): the kernel must refuse it, so the call returns
+ * HSV_ERR_DEVICE_FAULT without reading through the header. */
+HSV_API int hsv_test_resident_post_bad(uint32_t m);
 
 #ifdef __cplusplus
 }

@@ -26,7 +26,8 @@ TEST_LIB_PATH = os.path.join(_HERE, "libhsv_test.so")
 # Exported by libhsv_test.so / libhsv_all.so only, never by libhsv.so.
 HOOKS = ("hsv_test_inject_fault", "hsv_test_inject_mode", "hsv_test_corrupt_auto_committee",
          "hsv_test_lanesplit_check", "hsv_set_lattice_bits", "hsv_set_variant", "hsv_variant_list",
-         "hsv_variant_available", "hsv_num_variants", "hsv_set_virtual_shards", "hsv_test_pipe_nocopy")
+         "hsv_variant_available", "hsv_num_variants", "hsv_set_virtual_shards", "hsv_test_pipe_nocopy",
+         "hsv_test_resident_counts", "hsv_test_resident_post_bad")
 
 # flag bits (include/hsv.h)
 STRICT_OK = 0x01
@@ -69,6 +70,8 @@ def _declare(lib):
         "hsv_bound_device": (ctypes.c_int, []),
         "hsv_set_virtual_shards": (ctypes.c_int, [ctypes.c_int]),
         "hsv_test_pipe_nocopy": (ctypes.c_int, [ctypes.c_int]),
+        "hsv_test_resident_counts": (None, [ctypes.POINTER(ctypes.c_uint64)] * 2),
+        "hsv_test_resident_post_bad": (ctypes.c_int, [ctypes.c_uint32]),
         "hsv_auto_committee_wait": (ctypes.c_int, [ctypes.c_int]),
         "hsv_auto_committee_faults": (ctypes.c_uint64, []),
         "hsv_variant_list": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
@@ -77,6 +80,7 @@ def _declare(lib):
         "hsv_device_count": (ctypes.c_int, []),
         "hsv_last_error": (ctypes.c_char_p, []),
         "hsv_version": (ctypes.c_char_p, []),
+        "hsv_abi_version": (ctypes.c_int, []),
         "hsv_verify": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, sz, sz, c_u8p]),
         "hsv_verify_strict": (ctypes.c_int, [c_u8p, c_u8p, c_u8p]),
         "hsv_verify_batch": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, sz]),

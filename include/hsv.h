@@ -100,8 +100,15 @@ HSV_API void hsv_shutdown(void);
 HSV_API int hsv_device_count(void);
 /* Human-readable description of the last error on the calling thread. */
 HSV_API const char *hsv_last_error(void);
-/* Library version string. */
+/* Library version string, "hsv MAJOR.MINOR.PATCH (gfx950)".  0.3.0: the
+ * three device-API calls (hsv_verify_device_bits, hsv_committee_verify_device,
+ * hsv_verify_transactions_device) take the optional d_fault argument before
+ * `stream`; a caller built against 0.2.x headers must be rebuilt (check
+ * HSV_ABI_VERSION against hsv_abi_version() at startup). */
+#define HSV_ABI_VERSION 3
 HSV_API const char *hsv_version(void);
+/* The ABI generation this library implements (HSV_ABI_VERSION of its header). */
+HSV_API int hsv_abi_version(void);
 
 /* ---- verification, host buffers (synchronous) --------------------------- */
 /* Verify n independent triples.  pk: n*32 B, sig: n*64 B (R||s),

@@ -203,42 +203,100 @@ def test_auto_committee_behind_verify_batch(mods):
 
 
 RESIDENT_CHILD = r"""
-import sys
+import ctypes, sys, time
 sys.path.insert(0, {tests!r}); sys.path.insert(0, {pkg!r})
 import numpy as np
 import conftest
 from conftest import oracle_flags
 from hsverify import _lib, _testing, synth, verifier
-lib = _lib.load()
 oracle = conftest.oracle_lib.__wrapped__()
-lib.hsv_set_auto_committee(1)
-qc = synth.qc_votes(100, seed=5, corrupt_frac=0.3)      # one shared digest
-tc = synth.tc_votes(100, seed=6, corrupt_frac=0.3)      # a digest per vote
-for w in (qc, tc):
-    msg = np.broadcast_to(w.msg, (w.n, 32)) if w.msg.ndim == 1 else w.msg
-    packed = np.concatenate([w.pk, w.sig], axis=1).tobytes()
-    for _ in range(3):  # the keys recur in verify_batch calls: the automatic cache learns them
-        lib.hsv_verify_batch_packed(bytes(msg[0]), packed, w.n)
+ERR_FAULT = -7
+with _testing.test_library() as lib:   # the hooks count the service's answers
+    def counts():
+        p, a = ctypes.c_uint64(), ctypes.c_uint64()
+        lib.hsv_test_resident_counts(ctypes.byref(p), ctypes.byref(a))
+        return p.value, a.value
+
+    def resident_call(fn):
+        # fn's verification must be answered by the service: one request posted, one answered
+        p0, a0 = counts()
+        out = fn()
+        p1, a1 = counts()
+        assert (p1 - p0, a1 - a0) == (1, 1), ("not answered by the resident service", p1 - p0, a1 - a0)
+        return out
+
+    lib.hsv_set_auto_committee(1)
+    qc = synth.qc_votes(100, seed=5, corrupt_frac=0.3)      # one shared digest
+    tc = synth.tc_votes(100, seed=6, corrupt_frac=0.3)      # a digest per vote
+    calls = 0
+    for w in (qc, tc):
+        msg = np.broadcast_to(w.msg, (w.n, 32)) if w.msg.ndim == 1 else w.msg
+        packed = np.concatenate([w.pk, w.sig], axis=1).tobytes()
+        for _ in range(3):  # the keys recur in verify_batch calls: the automatic cache learns them
+            lib.hsv_verify_batch_packed(bytes(msg[0]), packed, w.n)
+        lib.hsv_auto_committee_wait(60000)
+        # every key of the batch, swapped-in corrupt ones included, recurred: all cached
+        assert lib.hsv_auto_committee_size() >= len(set(bytes(p) for p in w.pk))
+        for k in (1, 2, 3, 4):
+            for i in range(0, w.n - k, 5):
+                pk, sg = w.pk[i:i + k], w.sig[i:i + k]
+                mg = msg[i:i + k] if w.msg.ndim == 2 else w.msg
+                exp = oracle_flags(oracle, pk, sg, msg[i:i + k])
+                got = resident_call(lambda: verifier.verify_flags(pk, sg, mg))
+                assert (got == exp).all(), (k, i, got, exp)
+                calls += 1
+    # back-to-back requests that differ only in the shared digest, or in one byte of s:
+    # a stale body read would answer the second with the first one's verdict
+    good = qc.accept.nonzero()[0][:2]
+    pk, sg = bytes(qc.pk[good[0]]), bytes(qc.sig[good[0]])
+    d = bytes(qc.msg)
+    d2 = bytes([d[0] ^ 1]) + d[1:]
+    s2 = bytearray(sg); s2[40] ^= 0x10; s2 = bytes(s2)
+    for _ in range(20):
+        assert resident_call(lambda: lib.hsv_verify_strict(d, pk, sg)) == 1
+        assert resident_call(lambda: lib.hsv_verify_strict(d2, pk, sg)) == 0
+        assert resident_call(lambda: lib.hsv_verify_strict(d, pk, sg)) == 1
+        assert resident_call(lambda: lib.hsv_verify_strict(d, pk, s2)) == 0
+    # headers the kernel must refuse (m = 0, m above the limit): a device fault, never a memory access
+    for m in (0, 5, 0xffffffff):
+        assert lib.hsv_test_resident_post_bad(m) == ERR_FAULT, lib.hsv_last_error()
+    assert resident_call(lambda: lib.hsv_verify_strict(d, pk, sg)) == 1   # the service goes on
+    # after an idle exit (1 s) the next request relaunches the kernel and is answered by it
+    time.sleep(1.5)
+    assert resident_call(lambda: lib.hsv_verify_strict(d, pk, sg)) == 1
+    # corrupted cached tables under the service: its self-check fails, the view is dropped,
+    # and the generic kernels answer with the right verdict
+    f0 = lib.hsv_auto_committee_faults()
+    assert _testing.corrupt_auto_committee() > 0
+    assert resident_call(lambda: lib.hsv_verify_strict(d, pk, sg)) == 1
+    assert lib.hsv_auto_committee_faults() == f0 + 1
+    assert lib.hsv_auto_committee_size() == 0
+    # relearn, then free the cache while the service is alive: the frees stop the kernel
+    # first (hipFree waits for every grid), so the call returns at once, not after the idle second
+    packed = np.concatenate([qc.pk, qc.sig], axis=1).tobytes()
+    for _ in range(3):
+        lib.hsv_verify_batch_packed(d, packed, qc.n)
     lib.hsv_auto_committee_wait(60000)
-    assert lib.hsv_auto_committee_size() > 0
-    used = 0
-    for k in (1, 2, 3, 4):
-        for i in range(0, w.n - k, 5):
-            got = verifier.verify_flags(w.pk[i:i + k], w.sig[i:i + k], msg[i:i + k] if w.msg.ndim == 2 else w.msg)
-            exp = oracle_flags(oracle, w.pk[i:i + k], w.sig[i:i + k], msg[i:i + k])
-            assert (got == exp).all(), (k, i, got, exp)
-            marks = _testing.host_call_marks()
-            used += marks[1] < 0 and marks[2] >= 0   # no slot lease (mark unset): the resident service answered
-    assert used > 0, "the resident service never answered"
-print("resident ok", used)
+    assert resident_call(lambda: lib.hsv_verify_strict(d, pk, sg)) == 1
+    t0 = time.perf_counter()
+    lib.hsv_set_auto_committee(0)   # drops the view: its store's hipFree
+    dt = time.perf_counter() - t0
+    assert dt < 0.5, dt
+    lib.hsv_set_auto_committee(1)
+    print("resident ok", calls, counts())
 """
 
 
 def test_resident_service_in_a_child_process():
     """The opt-in resident latency service (HSV_QC_RESIDENT=1, read once per
-    process): batches of 1-4 cached-key votes, with the corruption kinds of
-    synth.CORRUPTIONS, shared and per-vote digests, flag for flag against
-    the oracle; the host timeline shows the service (not a launch) answered."""
+    process), through libhsv_test.so's request counters: every 1-4-vote
+    batch of cached keys is answered by the service (one request posted and
+    answered per call), flag for flag against the oracle over the corruption
+    kinds of synth.CORRUPTIONS, shared and per-vote digests; back-to-back
+    requests differing only in the digest or one byte of s; headers with m = 0
+    or above the limit refused as HSV_ERR_DEVICE_FAULT; a relaunch after the
+    idle exit; corrupted cached tables (the view dropped, the generic path
+    answers); a cache reset while the service is alive returns promptly."""
     import os
     import subprocess
     import sys

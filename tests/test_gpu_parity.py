@@ -44,7 +44,7 @@ def test_golden_every_variant(api, golden):
 
 
 def test_golden_row_form_chunks(api, golden):
-    """Batches at or below the row form's cut-over (HSV_ROW_MAX, default 3072)
+    """Batches at or below the row form's cut-over (row_max(), 3072 items)
     run hsv_verify_row_kernel: the golden records in chunks of 1000 (one row
     per element) and of 700 (at or below 768 items: two rows per element), and
     in ragged small batches (1, 5, 7, 13 items: partial blocks), every flag bit
@@ -143,10 +143,9 @@ def test_lattice_fallback_records_product_library(api, fallback_records, hsv):
 
 
 def test_host_pipeline_with_fallback_items(api, fallback_records, oracle_lib):
-    """Host batches of >= 2^18 items (the chunked copy pipeline, and with
-    HSV_HOST_PIPE=streamed the one-launch streamed form: per-lane prepass,
-    then the point pass or, for an item without a short lattice pair, the
-    full-length path inline).  With the bound lowered to 133 every fixture
+    """Host batches of >= 2^18 items (the chunked copy pipeline: per-chunk
+    prepass, then the point pass or, for an item without a short lattice
+    pair, the full-length path).  With the bound lowered to 133 every fixture
     record takes the full-length path; they sit at random positions among
     ordinary records."""
     _, verifier, synth = api
@@ -175,35 +174,6 @@ def test_host_pipeline_with_fallback_items(api, fallback_records, oracle_lib):
                 assert (got[sample] == oracle_flags(oracle_lib, pk[sample], sig[sample], msg[sample])).all()
         finally:
             lib.hsv_set_auto_committee(1)
-
-
-STREAMED_CHILD = r"""
-import sys
-sys.path.insert(0, {tests!r}); sys.path.insert(0, {pkg!r})
-import numpy as np, torch
-import conftest
-from conftest import oracle_flags
-import test_gpu_parity as t
-from hsverify import crypto, synth, verifier
-oracle = conftest.oracle_lib.__wrapped__()
-fb = conftest.fallback_records.__wrapped__()
-t.test_host_pipeline_with_fallback_items((crypto, verifier, synth), fb, oracle)
-t.test_host_api_pipelined_chunks_match_device_api((crypto, verifier, synth), oracle)
-t.test_host_api_pipeline_shared_digest_and_packed_votes((crypto, verifier, synth), oracle)
-print("streamed ok")
-"""
-
-
-def test_streamed_host_path_in_a_child_process():
-    """The streamed host form (HSV_HOST_PIPE=streamed, read once per process)
-    through the three host-pipeline tests above, in a child process."""
-    import subprocess
-    import sys
-    from conftest import PKG
-    here = os.path.dirname(os.path.abspath(__file__))
-    r = subprocess.run([sys.executable, "-c", STREAMED_CHILD.format(tests=here, pkg=PKG)], capture_output=True,
-                       text=True, timeout=600, env=dict(os.environ, HSV_HOST_PIPE="streamed"))
-    assert r.returncode == 0 and "streamed ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
 
 
 # ---- the reference's own tests (crypto/src/tests/crypto_tests.rs) ---------

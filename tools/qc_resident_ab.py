@@ -15,8 +15,16 @@ CHILD = r"""
 import json, sys
 sys.path.insert(0, {root!r}); sys.path.insert(0, {root!r} + "/hotstuff-digital-signature-benchmarking_amd")
 import bench
+import time
+import numpy as np
+from hsverify import synth
 r = bench.qc_latency({reps}, auto=True)
-print(json.dumps({{k: v["p50_ms"] for k, v in r.items() if isinstance(v, dict)}}))
+out = {{k: v["p50_ms"] for k, v in r.items() if isinstance(v, dict)}}
+lib = bench._oracle()   # the dalek port's single verify_strict, same process and box
+w = synth.qc_votes(4, seed=4)
+ts = bench._timed(lambda: lib.oracle_verify_flags(bytes(w.pk[0]), bytes(w.sig[0]), bytes(w.msg), 32), 200, warm=5)
+out["cpu_port_single_verify_strict"] = float(np.median(ts) * 1e3)
+print(json.dumps(out))
 """
 
 
