@@ -37,9 +37,18 @@ Reported beside it:
                    corrupted votes.
   tc_latency       C3 TC (667 timeouts, per-vote digests) through the batched
                    strict API and from bincode, 0 % and 5 % corrupted.
+  tc_dropin_sequential  C3 TC the way the unchanged caller verifies it: 667
+                   sequential hsv_verify_strict calls (TC::verify's loop).
+  resident         a child process with HSV_QC_RESIDENT=1: one verify_strict, a
+                   C1 QC and the sequential TC loop through the resident latency
+                   service, with the dalek port's single verify in the same process.
   qc_cpu_baseline  one host core: the C port of dalek verify_batch (Straus /
                    Pippenger MSM) for C1-C3 QCs and the sequential TC::verify loop.
   mempool_tx       2^20 client transactions of 512 B in HBM.
+
+stdout carries ONE compact JSON line (< 4 KB: the C4 line, roofline,
+cpu_baseline, and a `latency` object with every GPU latency next to the CPU
+port's); the full record (every rep's phases and tails) goes to --detail.
 """
 import argparse
 import ctypes
@@ -430,6 +439,49 @@ def tc_dropin_sequential(reps):
     return out
 
 
+def resident_child(reps, tc_reps):
+    """Runs in a child process with HSV_QC_RESIDENT=1 (the library reads it
+    once per process): one cached-key verify_strict and a C1 QC through the
+    resident latency service, the sequential TC loop through it, and the dalek
+    port's single verify_strict on one host core of the same process."""
+    from hsverify import _lib, _testing, synth
+    lib = _lib.load()
+    lib.hsv_set_auto_committee(1)
+    w = synth.qc_votes(4, seed=4)
+    pk0, sig0, d0 = bytes(w.pk[0]), bytes(w.sig[0]), bytes(w.msg)
+    packed = np.concatenate([w.pk, w.sig], 1).tobytes()
+    for _ in range(3):
+        lib.hsv_verify_batch_packed(d0, packed, w.n)
+    lib.hsv_auto_committee_wait(60000)
+    call = lambda: lib.hsv_verify_strict(d0, pk0, sig0)
+    assert call() == 1
+    res = {"single_verify_strict": _timed_lib(call, reps)}
+    marks = _testing.host_call_marks()
+    res["answered_by_service"] = bool(marks[1] < 0 <= marks[2])   # no slot lease: the service answered
+    call = lambda: lib.hsv_verify_batch_packed(d0, packed, w.n)
+    assert call() == 1
+    res["n4_votes3"] = _timed_lib(call, reps)
+    res["tc_dropin_sequential"] = tc_dropin_sequential(tc_reps)
+    orc = _oracle()
+    ts = _timed(lambda: orc.oracle_verify_flags(pk0, sig0, d0, 32), 200, warm=5)
+    res["cpu_port_single_verify_strict_p50_ms"] = float(np.median(ts) * 1e3)
+    return res
+
+
+def resident_leg(reps, tc_reps):
+    """resident_child in a fresh process (HSV_QC_RESIDENT=1); its JSON, or the error."""
+    env = dict(os.environ, HSV_QC_RESIDENT="1")
+    cmd = [sys.executable, os.path.abspath(__file__), "--resident-child", "--qc-reps", str(reps),
+           "--tc-seq-reps", str(tc_reps)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+        if r.returncode == 0:
+            return json.loads(r.stdout.strip().splitlines()[-1])
+        return {"error": f"rc {r.returncode}: {r.stderr[-500:]}"}
+    except (subprocess.SubprocessError, ValueError, IndexError) as e:
+        return {"error": str(e)}
+
+
 def committee_bench(reps, dev, n_votes=1 << 20):
     """Committee key cache: QC latency for C2/C3 through the
     cached tables, and throughput for 2^20 votes by a 1000-key committee."""
@@ -710,6 +762,17 @@ def compact(out):
                                            "cpu_p50": cpu("tc_n1000_votes667_clean_p50_ms")}
             lat["tc_c3_corrupt5pct_bincode"] = {"gpu": _pp(tl["n1000_votes667_corrupt5pct_bincode"], True),
                                                 "cpu_p50": cpu("tc_n1000_votes667_corrupt5pct_p50_ms")}
+        rs = out.get("resident", {})
+        if "single_verify_strict" in rs:
+            lat["resident_service"] = {
+                "verify_strict_single": _pp(rs["single_verify_strict"], True),
+                "qc_c1_3votes": _pp(rs["n4_votes3"], True),
+                "tc_c3_dropin_sequential": _pp(rs["tc_dropin_sequential"]),
+                "cpu_p50_same_process": _r(rs["cpu_port_single_verify_strict_p50_ms"]),
+                "answered_by_service": rs["answered_by_service"],
+                "what": "HSV_QC_RESIDENT=1 child process: requests to a resident block, no launch"}
+        elif rs:
+            lat["resident_service"] = {"error": str(rs.get("error"))[:200]}
         seq = out.get("tc_dropin_sequential")
         if seq:
             lat["tc_c3_dropin_sequential"] = {"gpu": _pp(seq), "gpu_call_p50": _r(seq["call_p50_ms"]),
@@ -758,6 +821,8 @@ def parse_args(argv=None):
                     help="file for the full record (every rep's phases, tails, probes); stdout gets the compact line")
     ap.add_argument("--tc-seq-reps", type=int, default=30,
                     help="repetitions of the 667-call sequential TC loop (tc_dropin_sequential)")
+    ap.add_argument("--resident-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-resident", action="store_true", help="skip the resident-service child leg")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only: launcher, shards, timing and gather without a GPU or verification")
     return ap.parse_args(argv)
@@ -820,6 +885,9 @@ def dry_run(a, world, rank, dist):
 
 def main():
     a = parse_args()
+    if a.resident_child:  # bench.py's own child (resident_leg): no ranks, one JSON line
+        print(json.dumps(resident_child(a.qc_reps, a.tc_seq_reps)), flush=True)
+        return
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and a.gpus is not None and a.gpus > 1:
         sys.exit(launch_ranks(a))
@@ -1013,6 +1081,8 @@ def main():
         out["qc_latency_generic"] = qc_latency(a.qc_reps, auto=False)
         out["tc_latency"] = tc_latency(a.qc_reps, auto=True)
         out["tc_dropin_sequential"] = tc_dropin_sequential(a.tc_seq_reps)
+        if not a.no_resident:
+            out["resident"] = resident_leg(a.qc_reps, a.tc_seq_reps)
         _lib.load().hsv_set_auto_committee(1)
         out["committee_cache"] = committee_bench(a.qc_reps, dev)
         # two streams: the record kernels (message hash + prepass, 2.3x the C4

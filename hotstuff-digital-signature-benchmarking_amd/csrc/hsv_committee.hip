@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 #include <type_traits>
 
 #include "hsv_comb.hpp"
@@ -218,11 +219,10 @@ __device__ uint64_t g_qc_clk[kQcClkWaves][kQcClkSlots];
 // does stage its request in LDS, read in one load by wave 0 (below).
 
 // one vote's words: the key A, the signature (R, s) and the message digest M
-// (sp / gp: the vote's signature and digest, in global memory or LDS)
-__device__ __forceinline__ void load_vote_words(const uint8_t *__restrict__ pks, uint32_t kk, const uint4 *sp,
-                                                const uint4 *gp, uint32_t pkw[8], uint32_t sigw[16],
-                                                uint32_t msgw[8]) {
-  const uint4 *p = reinterpret_cast<const uint4 *>(pks + (uint64_t)kk * 32);
+// (p / sp / gp: the vote's key encoding, signature and digest, in global
+// memory or LDS)
+__device__ __forceinline__ void load_vote_words(const uint4 *p, const uint4 *sp, const uint4 *gp, uint32_t pkw[8],
+                                                uint32_t sigw[16], uint32_t msgw[8]) {
   const uint4 p0 = p[0], p1 = p[1];
   const uint4 s0 = sp[0], s1 = sp[1], s2 = sp[2], s3 = sp[3];
   const uint4 m0 = gp[0], m1 = gp[1];
@@ -259,12 +259,16 @@ __device__ __forceinline__ void comb_quad_block(const uint32_t *__restrict__ key
                                                 const uint32_t *const *__restrict__ key_tables,
                                                 const uint32_t *__restrict__ btable, uint8_t *__restrict__ flags_out,
                                                 uint32_t inject, uint32_t *__restrict__ fault,
-                                                uint32_t *__restrict__ done, uint32_t blk) {
+                                                uint32_t *__restrict__ done, uint32_t blk,
+                                                const uint8_t *__restrict__ vote_pks = nullptr) {
   __shared__ uint32_t r_x[kFusedVotes][kFeLimbs], r_y[kFusedVotes][kFeLimbs], r_fl[kFusedVotes];
   __shared__ uint32_t k_rec[kFusedVotes][9], k_ready;
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint32_t base = blk * kFusedVotes;
   HSV_QC_CLK(0);
+#ifdef HSV_QC_WAVE_CLOCKS
+  const uint64_t call_t0 = wall_clock64(), call_s0 = clock64();  // block entry, for hsv_qc_call_stamps
+#endif
   // vote v of the block reads vote min(base + v, m - 1): the last block's
   // spare slots repeat the batch's last vote and write no flag
   auto vote_of = [&](uint32_t v) { return base + v < m ? base + v : m - 1u; };
@@ -278,6 +282,12 @@ __device__ __forceinline__ void comb_quad_block(const uint32_t *__restrict__ key
   auto vote_sig = [&](uint32_t v) { return reinterpret_cast<const uint4 *>(sig + (uint64_t)vote_of(v) * sig_stride); };
   auto vote_msg = [&](uint32_t v) { return reinterpret_cast<const uint4 *>(msg + (uint64_t)vote_of(v) * msg_stride); };
   auto vote_kidx = [&](uint32_t v) -> uint32_t { return key_idx[vote_of(v)]; };
+  // the key's encoding: the committee's copy in HBM, or (resident service)
+  // the request's copy in LDS -- the same bytes, the host found the member
+  // index by comparing all 32 of them
+  auto vote_pk = [&](uint32_t v, uint32_t kk) {
+    return reinterpret_cast<const uint4 *>(vote_pks ? vote_pks + 32ull * vote_of(v) : pks + (uint64_t)kk * 32);
+  };
   if constexpr (kHashWave) {
     if (wave == kHashWaveIdx) {
       // one lane per vote hashes (lanes 0..kFusedVotes-1); the rest of the
@@ -294,7 +304,7 @@ __device__ __forceinline__ void comb_quad_block(const uint32_t *__restrict__ key
         const uint32_t kidx = vote_kidx(vl);
         const uint32_t kk = kidx < nkeys ? kidx : 0u;
         uint32_t pkw[8], sigw[16], msgw[8], h[16], kr[9];
-        load_vote_words(pks, kk, vote_sig(vl), vote_msg(vl), pkw, sigw, msgw);
+        load_vote_words(vote_pk(vl, kk), vote_sig(vl), vote_msg(vl), pkw, sigw, msgw);
         HSV_QC_CLK_LOADED(3);
         sha512_96<kShaCompact>(sigw, pkw, msgw, h);
         const sc k = sc_reduce512(h);
@@ -380,7 +390,7 @@ __device__ __forceinline__ void comb_quad_block(const uint32_t *__restrict__ key
   const bool kvalid = kidx < nkeys;
   const uint32_t kk = kvalid ? kidx : 0u;
   uint32_t pkw[8], sigw[16], msgw[8];
-  load_vote_words(pks, kk, vote_sig(vl), vote_msg(vl), pkw, sigw, msgw);
+  load_vote_words(vote_pk(vl, kk), vote_sig(vl), vote_msg(vl), pkw, sigw, msgw);
   const uint32_t s_ok = sc_is_canonical(sigw + 8);
 #ifdef HSV_TIMING_STUB_QUADPATH  // tools/qc_phase_probe.py only: wrong flags, the R waves' time alone
   ge_ext q = ge_identity();
@@ -473,6 +483,19 @@ __device__ __forceinline__ void comb_quad_block(const uint32_t *__restrict__ key
   if (fb | ((rf >> 2) & 1u)) fault[0] = 1u;  // device self-check (hsv_kernels.hip report_faults)
   if (valid && g == 0u) flags_out[i0] = kvalid ? (uint8_t)f : (uint8_t)0;
   HSV_QC_CLK(5);
+#ifdef HSV_QC_WAVE_CLOCKS
+  // measurement builds: block 0's entry and end (100 MHz constant clock) and
+  // shader clock, next to the call's self-check words in pinned memory, so
+  // the host reads them after each call without a device-wide sync
+  // (tools/qc_tail_clocks.py); released with the flags below
+  if (blk == 0u && lane == 0u && done) {
+    uint64_t *st = reinterpret_cast<uint64_t *>(fault + 4);
+    st[0] = call_t0;
+    st[1] = wall_clock64();
+    st[2] = call_s0;
+    st[3] = clock64();
+  }
+#endif
   if (done) {
     // completion marker (HSV_QC_SYNC=marker): every wave of the block is past
     // its reads (the R and hash waves before the barrier / k_ready), and this
@@ -503,7 +526,7 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
 // (profiles/r05a_aql_latency.txt, tools/resident_latency.hip).  Per request:
 //   * wave 0 polls the doorbell (relaxed system-scope loads, s_sleep between
 //     polls); on a new seq every lane performs a system-scope acquire, then
-//     the wave reads the whole request body in ONE vector load (64 lanes x 8
+//     the wave reads the whole request body in ONE vector load (64 lanes x 16
 //     bytes) into LDS.  Round 4's form read eight header words one by one
 //     with dependent LDS stores between them -- eight PCIe round trips, the
 //     ~10 us the service lost against a launch -- and its only acquire was
@@ -512,8 +535,10 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
 //     <= kResidentVotes, non-null committee arrays, 1 <= nkeys <= 2^20.  An
 //     invalid request is answered with fault[2] = 1 and no verification
 //     (HSV_ERR_DEVICE_FAULT on the host), never with a memory access;
-//   * the votes' key indices, signatures and digests are then read from LDS by
-//     comb_quad_block, and thread 0 answers done = seq after a release.
+//   * the votes' key indices, key encodings, signatures and digests are then
+//     read from LDS by comb_quad_block (no PCIe or HBM read before the R
+//     waves' root chain and the hash wave's SHA-512 start), and thread 0
+//     answers done = seq after a release.
 // It leaves on the stop word or after idle_ticks (100 MHz) without a request,
 // and clears `alive` as it goes, so no grid outlives its process; the host
 // relaunches it on the next request.
@@ -525,8 +550,8 @@ __device__ __forceinline__ T req_load(T *p) {  // a vector load, never the scala
 constexpr uint32_t kResidentMaxKeys = 1u << 20;  // hsv_committee_create's bound and above the auto cache's
 
 __global__ void __launch_bounds__(kFusedThreads) hsv_comb_resident_kernel(QcResidentReq *req, uint64_t idle_ticks) {
-  static_assert(sizeof(QcResidentBody) == 64 * 8, "one 8-byte word per lane");
-  __shared__ __attribute__((aligned(16))) uint64_t body[64];
+  static_assert(sizeof(QcResidentBody) == 64 * 16, "16 bytes per lane");
+  __shared__ uint4 body[64];
   __shared__ uint32_t cmd_seq, cmd_stop;
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   uint32_t last = 0;
@@ -550,9 +575,11 @@ __global__ void __launch_bounds__(kFusedThreads) hsv_comb_resident_kernel(QcResi
       }
       last = sq;
       if (!stop) {
-        // the body the host wrote before its release store of seq
+        // the body the host wrote before its release store of seq: after the
+        // system-scope acquire no cache holds an older copy, so a plain
+        // 16-byte vector load per lane reads it (one instruction, one trip)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        body[lane] = req_load(reinterpret_cast<uint64_t *>(&req->body) + lane);
+        body[lane] = reinterpret_cast<const uint4 *>(&req->body)[lane];
       }
       if (lane == 0u) {
         cmd_seq = sq;
@@ -569,7 +596,8 @@ __global__ void __launch_bounds__(kFusedThreads) hsv_comb_resident_kernel(QcResi
     if (valid) {  // block-uniform: every wave takes the same branch
       comb_quad_block(b.key_idx, reinterpret_cast<const uint8_t *>(b.sig), 64,
                       reinterpret_cast<const uint8_t *>(b.msg), b.msg_per_vote ? 32 : 0, m, b.pks, b.key_flags,
-                      nkeys, b.key_tables, b.btable, req->flags, b.inject, req->fault, nullptr, 0u);
+                      nkeys, b.key_tables, b.btable, req->flags, b.inject, req->fault, nullptr, 0u,
+                      reinterpret_cast<const uint8_t *>(b.pk));
     }
     __syncthreads();  // every wave past its reads of this request (LDS included) and its flag stores
     if (threadIdx.x == 0) {
@@ -684,6 +712,10 @@ extern "C" hipError_t hsv_launch_comb_build(const uint8_t *encs, uint32_t nkeys,
 // batches up to this many votes take the four-lanes-per-vote form
 static constexpr uint32_t kCombQuadMax = 1u << 12;
 
+#ifdef HSV_QC_WAVE_CLOCKS
+static thread_local uint32_t *t_last_fault = nullptr;  // the calling thread's last latency-form launch
+#endif
+
 extern "C" hipError_t hsv_launch_comb_verify(const uint32_t *key_idx, const uint8_t *sig, uint64_t sig_stride,
                                              const uint8_t *msg, uint64_t msg_stride, uint32_t m,
                                              const uint8_t *pks, const uint8_t *key_flags, uint32_t nkeys,
@@ -692,6 +724,9 @@ extern "C" hipError_t hsv_launch_comb_verify(const uint32_t *key_idx, const uint
                                              hipStream_t stream) {
   if (m == 0) return hipSuccess;
   if (!fault) return hipErrorInvalidValue;
+#ifdef HSV_QC_WAVE_CLOCKS
+  t_last_fault = done ? fault : nullptr;
+#endif
   const uint32_t inject = (uint32_t)hsvi_inject_mode();
   if (m <= kCombQuadMax) {  // latency form: four lanes per vote, R decompressed by the R waves
     hipLaunchKernelGGL(hsv::hsv_comb_verify_quad_fused_kernel, dim3((m + hsv::kFusedVotes - 1) / hsv::kFusedVotes),
@@ -739,6 +774,17 @@ extern "C" __attribute__((visibility("default"))) int hsv_qc_wave_clocks(uint64_
   if (hipGetSymbolAddress(&p, HIP_SYMBOL(hsv::g_qc_clk)) != hipSuccess) return -1;
   if (hipMemset(p, 0, sizeof(hsv::g_qc_clk)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return -1;
   return hsv::kFusedThreads / 64;
+}
+
+// Block 0's stamps of the calling thread's last marker-synced committee call
+// (entry and end on the 100 MHz clock, shader clock at both): 4 words, read
+// from the call's pinned sync region.  0, or -1 when there was no such call.
+extern "C" __attribute__((visibility("default"))) int hsv_qc_call_stamps(uint64_t *out) {
+  if (!t_last_fault || !out) return -1;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, t_last_fault) != hipSuccess || !a.hostPointer) return -1;
+  std::memcpy(out, static_cast<const uint32_t *>(a.hostPointer) + 4, 4 * sizeof(uint64_t));
+  return 0;
 }
 
 // The same without synchronising the device (a resident block keeps running):

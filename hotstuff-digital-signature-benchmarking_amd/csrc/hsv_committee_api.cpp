@@ -124,6 +124,7 @@ class KeyIndex {
 struct CommitteeDev {
   int device = 0;
   uint32_t n = 0;
+  const uint8_t *h_pks = nullptr;  // host copy of the n key encodings, by member index
   const uint8_t *d_pks = nullptr;
   const uint8_t *d_kflags = nullptr;
   const uint32_t *const *d_tabptr = nullptr;
@@ -257,6 +258,7 @@ int resident_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t 
   const size_t mm = std::min<size_t>(m, kResidentVotes);  // m > kResidentVotes is the kernel's to refuse
   for (size_t i = 0; i < mm; ++i) {
     b.key_idx[i] = key_idx[i];
+    if (key_idx[i] < cd.n) std::memcpy(b.pk[i], cd.h_pks + (size_t)key_idx[i] * 32, 32);  // else flag 0
     std::memcpy(b.sig[i], sig + i * sig_stride, 64);
     if (msg_stride) std::memcpy(b.msg[i], msg + i * msg_stride, 32);
   }
@@ -337,6 +339,8 @@ int resident_post_bad(uint32_t m) {
   CommitteeDev cd;
   cd.device = c.device;
   cd.n = 1;
+  static const uint8_t zero_key[32] = {0};
+  cd.h_pks = zero_key;
   cd.d_pks = reinterpret_cast<const uint8_t *>(c.d_btable);  // valid device memory, never read: m is refused
   cd.d_kflags = cd.d_pks;
   cd.d_tabptr = reinterpret_cast<const uint32_t *const *>(c.d_btable);
@@ -488,6 +492,7 @@ using namespace hsvh;
 // ---- explicit committee ------------------------------------------------------------
 struct hsv_committee {
   CommitteeDev dev;
+  std::vector<uint8_t> h_pks;
   uint8_t *d_pks = nullptr;
   uint8_t *d_kflags = nullptr;
   uint32_t *d_tables = nullptr;
@@ -510,6 +515,8 @@ int hsv_committee_create(const uint8_t *pks, size_t n, hsv_committee **out) {
   std::unique_ptr<hsv_committee> cm(new hsv_committee());
   cm->dev.device = dev;
   cm->dev.n = (uint32_t)n;
+  cm->h_pks.assign(pks, pks + 32 * n);
+  cm->dev.h_pks = cm->h_pks.data();
   for (size_t i = 0; i < n; ++i) cm->index.emplace(key_of(pks + 32 * i), (uint32_t)i);
   if (n) {
     const uint64_t words = hsv_comb_table_bytes() / 4;
@@ -652,6 +659,9 @@ struct AutoStore {  // append-only device storage, freed with the last view usin
   uint32_t *d_tmp = nullptr;
   hipStream_t stream = nullptr;  // builds only
   std::vector<uint32_t *> blocks;
+  // host copy of the encodings (kAutoMaxKeys * 32 B, allocated once: a view's
+  // pointer into it stays valid as later builds append)
+  std::unique_ptr<uint8_t[]> h_pks{new uint8_t[(size_t)kAutoMaxKeys * 32]};
   ~AutoStore() {
     resident_quiesce();
     DeviceGuard guard(device);
@@ -746,6 +756,7 @@ int build_view(const std::shared_ptr<const AutoView> &base, int device, const st
     const uint32_t slot = n0 + i;
     ptrs[i] = store->blocks[slot / kBlockKeys] + (uint64_t)(slot % kBlockKeys) * words;
   }
+  std::memcpy(store->h_pks.get() + (size_t)n0 * 32, encs.data(), encs.size());  // slots no published view reads yet
   e = hipMemcpyAsync(store->d_pks + (size_t)n0 * 32, encs.data(), encs.size(), hipMemcpyHostToDevice, store->stream);
   if (e == hipSuccess)
     e = hipMemcpyAsync(store->d_tabptr + n0, ptrs.data(), m * sizeof(uint32_t *), hipMemcpyHostToDevice, store->stream);
@@ -758,6 +769,7 @@ int build_view(const std::shared_ptr<const AutoView> &base, int device, const st
   v->store = store;
   v->dev.device = store->device;
   v->dev.n = n0 + m;
+  v->dev.h_pks = store->h_pks.get();
   v->dev.d_pks = store->d_pks;
   v->dev.d_kflags = store->d_kflags;
   v->dev.d_tabptr = store->d_tabptr;

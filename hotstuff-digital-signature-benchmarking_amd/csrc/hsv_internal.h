@@ -78,10 +78,10 @@ double hsv_launch_mad_peak(int device_cus);
 // csrc/hsv_committee.hip), in coherent pinned host memory.  The host fills
 // `body` and the answer words, then bumps `seq` with a release store; the
 // kernel sees the new seq, performs a system-scope acquire, reads the whole
-// body in ONE vector load (64 lanes x 8 bytes), validates it, and answers
+// body in ONE vector load (64 lanes x 16 bytes), validates it, and answers
 // with `done` = seq after a release.  kResidentVotes votes at most.
 constexpr int kResidentVotes = 4;
-struct QcResidentBody {                  // 512 bytes, word offsets fixed (the kernel reads it raw)
+struct QcResidentBody {                  // 1 KiB, word offsets fixed (the kernel reads it raw)
   uint32_t m, nkeys, inject, msg_per_vote;  // votes (1..kResidentVotes), members, fault injection, 0/1
   const uint8_t *pks;                    // the committee view's device arrays
   const uint8_t *key_flags;
@@ -90,9 +90,10 @@ struct QcResidentBody {                  // 512 bytes, word offsets fixed (the k
   uint32_t key_idx[kResidentVotes];      // word 12
   uint32_t sig[kResidentVotes][16];      // word 16: R || s per vote
   uint32_t msg[kResidentVotes][8];       // word 80: one digest per vote, or the shared digest in msg[0]
-  uint32_t spare[16];
+  uint32_t pk[kResidentVotes][8];        // word 112: each vote's key encoding (the member's, byte for byte)
+  uint32_t spare[112];
 };
-static_assert(sizeof(QcResidentBody) == 512, "one 64-lane x 8-byte load");
+static_assert(sizeof(QcResidentBody) == 1024, "one 64-lane x 16-byte load");
 struct QcResidentReq {
   uint32_t seq, stop, alive, done;       // doorbell, stop word, set while the kernel runs, completion
   uint32_t pad0[12];

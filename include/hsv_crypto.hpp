@@ -31,6 +31,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -77,8 +78,9 @@ inline void set_infrastructure_fallback(InfrastructureFallback f) { infrastructu
 
 // Latency routing of the caller.
 // One signature on the GPU costs a launch plus one dependent root chain
-// (~0.08 ms for a cached committee key), one host core ~0.04 ms; a QC of
-// three votes is level; from a handful of votes on the GPU wins.  A
+// (0.0395 ms for a cached committee key, 0.0357 ms through the resident
+// service), one host core 0.037 ms (dalek port); a 3-vote QC is 0.04 ms on the
+// GPU against 0.077 ms on the host.  A
 // deployment installs a host verifier with the same semantics (dalek in the
 // Rust shim) and a size limit: verify calls and verify_batch calls of at most
 // max_batch votes go to it, everything larger to libhsv.  Unlike the
@@ -101,6 +103,18 @@ inline std::atomic<uint64_t> &host_route_uses() {
 }
 // Install once at startup, before verify calls run on other threads.
 inline void set_host_route(HostRoute r) { host_route() = std::move(r); }
+
+// The single-verify routing default (the Rust
+// shim's hsv_single_on_host): a lone signature stays on the host unless
+// libhsv's resident latency service is on (HSV_QC_RESIDENT=1: one cached-key
+// verify_strict 0.0357 ms against 0.0371 ms for the dalek port on one host
+// core, profiles/r05d_resident_ab.txt; launched 0.0395 ms).  HSV_ROUTE_SINGLE
+// = "gpu" / "host" overrides it.
+inline bool single_verify_on_host_default() {
+  if (const char *v = std::getenv("HSV_ROUTE_SINGLE")) return std::strcmp(v, "gpu") != 0;
+  const char *r = std::getenv("HSV_QC_RESIDENT");
+  return !(r && r[0] == '1');
+}
 
 // ed25519::Error: opaque.
 struct CryptoError {

@@ -201,11 +201,12 @@ static void install_oracle_fallback() {
   set_infrastructure_fallback(std::move(f));
 }
 
-// --route: single verifies and QCs of at most 2 votes on the host verifier
-// (the C oracle stands in for dalek), larger QCs on libhsv
+// --route: QCs of at most 2 votes on the host verifier (the C oracle stands
+// in for dalek), larger QCs on libhsv; single verifies on the host unless the
+// resident latency service is on (crypto::single_verify_on_host_default)
 static void install_host_route() {
   HostRoute r;
-  r.single = true;
+  r.single = single_verify_on_host_default();
   r.max_batch = 2;
   r.verify_strict = [](const uint8_t *digest, const uint8_t *pk, const uint8_t *sig) {
     return (oracle_verify_flags(pk, sig, digest, 32) & HSV_STRICT_OK) != 0;

@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""Where the drop-in QC call's tail reps lose their time (round-4 VERDICT
+item 4).  With the wave-clock build (tools/build_ab_libs.sh qcclk
+"-DHSV_QC_WAVE_CLOCKS"), block 0 of every marker-synced committee launch
+leaves its entry and end stamps (100 MHz constant clock) and its shader clock
+next to the call's self-check words in pinned memory; the host reads them after
+each call (hsv_qc_call_stamps, a 32-byte copy -- no device-wide sync), so the
+calls run back to back exactly as in bench.py.  Per rep: wall time, block 0's
+span, the shader clock over the span, and the host time outside the span
+(launch, dispatch, marker sync), plus the gap since the previous call's end on
+the GPU clock.  The reps above the wall-time p99 are compared with the median
+rep: a lower shader clock says clock ramp-down, a longer span at the same
+clock says the waves waited, and a normal span with a long wall time says the
+launch or dispatch queued.
+
+HSV_LIB=libhsv_qcclk.so python tools/qc_tail_clocks.py [--reps 1000]
+"""
+import argparse
+import ctypes
+import gc
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "hotstuff-digital-signature-benchmarking_amd"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=1000)
+    a = ap.parse_args()
+    from hsverify import _lib, synth, wire
+    lib = _lib.load()
+    st = lib.hsv_qc_call_stamps
+    st.restype = ctypes.c_int
+    st.argtypes = [ctypes.c_void_p]
+    lib.hsv_set_auto_committee(1)
+    stamp = np.zeros(4, np.uint64)
+    out = {}
+    cases = []
+    for committee in (4, 100, 1000):
+        w = synth.qc_votes(committee, seed=committee)
+        packed = np.concatenate([w.pk, w.sig], axis=1).tobytes()
+        d = bytes(w.msg)
+        cases.append((f"qc_n{committee}_votes{w.n}", lambda d=d, p=packed, n=w.n: lib.hsv_verify_batch_packed(d, p, n),
+                      lambda d=d, p=packed, n=w.n: lib.hsv_verify_batch_packed(d, p, n)))
+    import bench
+    t = bench.member_corrupted(synth.tc_votes, 1000, seed=1000, frac=0.05)
+    q = synth.qc_votes(1000, seed=1000)
+    pq = np.concatenate([q.pk, q.sig], 1).tobytes()
+    hqc = bench.tc_hqc(1000, 1000)
+    buf = wire.encode_tc(1000, [(bytes(p), bytes(s_), int(h)) for p, s_, h in zip(t.pk, t.sig, hqc)])
+    nv = ctypes.c_size_t(0)
+    cases.append(("tc_n1000_corrupt5pct_bincode", lambda: lib.hsv_tc_verify_bincode(buf, len(buf), ctypes.byref(nv), None),
+                  lambda: lib.hsv_verify_batch_packed(bytes(q.msg), pq, q.n)))
+    for name, call, learn in cases:
+        for _ in range(3):
+            learn()
+        lib.hsv_auto_committee_wait(60000)
+        wall, span, mhz, gap = [], [], [], []
+        prev_end = None
+        gc.collect()
+        gc.disable()
+        for i in range(a.reps + 20):
+            t0 = time.perf_counter()
+            rc = call()
+            dt = time.perf_counter() - t0
+            assert rc in (0, 1), rc
+            assert st(stamp.ctypes.data) == 0
+            e0, e1, s0, s1 = (int(x) for x in stamp)
+            if i >= 20:
+                wall.append(dt * 1e3)
+                span.append((e1 - e0) * 1e-5)
+                mhz.append((s1 - s0) / max(1, e1 - e0) * 100.0)
+                gap.append((e0 - prev_end) * 1e-5 if prev_end else np.nan)
+            prev_end = e1
+        gc.enable()
+        wall, span, mhz, gap = (np.array(x) for x in (wall, span, mhz, gap))
+        outside = wall - span
+        cut = np.percentile(wall, 99)
+        tail = wall > cut
+        med = lambda x: round(float(np.nanmedian(x)), 4)
+        out[name] = {
+            "reps": len(wall), "wall_p50_ms": med(wall), "wall_p99_ms": round(float(cut), 4),
+            "p99_over_p50": round(float(cut / np.median(wall)), 3),
+            "median_rep": {"block0_span_ms": med(span), "outside_span_ms": med(outside), "shader_mhz": med(mhz),
+                           "gpu_gap_since_last_ms": med(gap)},
+            "tail_reps": {"n": int(tail.sum()), "wall_ms": med(wall[tail]), "block0_span_ms": med(span[tail]),
+                          "outside_span_ms": med(outside[tail]), "shader_mhz": med(mhz[tail]),
+                          "gpu_gap_since_last_ms": med(gap[tail])},
+            "corr_wall_span": round(float(np.corrcoef(wall, span)[0, 1]), 3),
+            "corr_wall_outside": round(float(np.corrcoef(wall, outside)[0, 1]), 3),
+        }
+        print(json.dumps({name: out[name]}), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
