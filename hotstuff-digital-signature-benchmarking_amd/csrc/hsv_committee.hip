@@ -392,6 +392,9 @@ __device__ __forceinline__ void comb_quad_block(const uint32_t *__restrict__ key
   uint32_t pkw[8], sigw[16], msgw[8];
   load_vote_words(vote_pk(vl, kk), vote_sig(vl), vote_msg(vl), pkw, sigw, msgw);
   const uint32_t s_ok = sc_is_canonical(sigw + 8);
+  // the key's flags now: read after the final barrier, this load's latency sat
+  // on the call's critical path
+  const uint32_t kf = key_flags[kk];
 #ifdef HSV_TIMING_STUB_QUADPATH  // tools/qc_phase_probe.py only: wrong flags, the R waves' time alone
   ge_ext q = ge_identity();
   const uint32_t *ta = key_tables[kk];
@@ -468,7 +471,6 @@ __device__ __forceinline__ void comb_quad_block(const uint32_t *__restrict__ key
   uint32_t same;
   if constexpr (kRowChecks) same = ge_eq_affine_row(q, rx, ry, z_nonzero);
   else same = ge_eq_affine(q, rx, ry);
-  const uint32_t kf = key_flags[kk];
   const uint32_t a_ok = (kf & kKeyAOk) ? 1u : 0u;
   const uint32_t small_a = a_ok & ((kf & kKeySmallA) ? 1u : 0u);
   const uint32_t parse_ok = s_ok & a_ok & r_ok;
@@ -524,49 +526,60 @@ hsv_comb_verify_quad_fused_kernel(const uint32_t *__restrict__ key_idx, const ui
 // hsv_internal.h), instead of a launch per request: a block of this shape
 // answers a doorbell in 2.2 us against 5.8 us for a launch with marker sync
 // (profiles/r05a_aql_latency.txt, tools/resident_latency.hip).  Per request:
-//   * wave 0 polls the doorbell (relaxed system-scope loads, s_sleep between
-//     polls); on a new seq every lane performs a system-scope acquire, then
-//     the wave reads the whole request body in ONE vector load (64 lanes x 16
-//     bytes) into LDS.  Round 4's form read eight header words one by one
-//     with dependent LDS stores between them -- eight PCIe round trips, the
-//     ~10 us the service lost against a launch -- and its only acquire was
-//     an agent-scope fence after those reads;
+//   * wave 0 polls the request itself: lanes 0..47 each read their 16-byte
+//     chunk {seq, 3 payload words} with one uncached vector load (sc0 sc1, so
+//     no cache can answer with an older copy), s_sleep between polls.  Once
+//     every chunk carries the same new seq the whole request has arrived --
+//     the host writes each chunk's payload before its seq, and x86 keeps
+//     stores in order -- so the doorbell and the body take ONE PCIe round
+//     trip.  (Round 4's form read eight header words one by one with
+//     dependent LDS stores between them, ~10 us; the round-5 form before this
+//     one took a doorbell read, a system-scope acquire and a body read.)
 //   * the block validates the header before it dereferences anything: 1 <= m
 //     <= kResidentVotes, non-null committee arrays, 1 <= nkeys <= 2^20.  An
-//     invalid request is answered with fault[2] = 1 and no verification
-//     (HSV_ERR_DEVICE_FAULT on the host), never with a memory access;
-//   * the votes' key indices, key encodings, signatures and digests are then
-//     read from LDS by comb_quad_block (no PCIe or HBM read before the R
-//     waves' root chain and the hash wave's SHA-512 start), and thread 0
-//     answers done = seq after a release.
+//     invalid request is answered with kResidentBadRequest and no
+//     verification (HSV_ERR_DEVICE_FAULT on the host), never with a memory
+//     access;
+//   * comb_quad_block reads the votes' key indices, key encodings, signatures
+//     and digests from the LDS copy and writes its flags and self-check word
+//     into LDS; thread 0 answers with two 8-byte system-scope stores {seq,
+//     flags} and {seq, fault bits} -- each one transaction, so no release
+//     fence (and no L2 write-back) is needed before them.
 // It leaves on the stop word or after idle_ticks (100 MHz) without a request,
 // and clears `alive` as it goes, so no grid outlives its process; the host
 // relaunches it on the next request.
-template <class T>
-__device__ __forceinline__ T req_load(T *p) {  // a vector load, never the scalar cache
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+__device__ __forceinline__ uint4 load16_uncached(const void *p) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 r;
+  asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(r) : "v"(p) : "memory");
+  return make_uint4(r.x, r.y, r.z, r.w);
 }
 
 constexpr uint32_t kResidentMaxKeys = 1u << 20;  // hsv_committee_create's bound and above the auto cache's
 
 __global__ void __launch_bounds__(kFusedThreads) hsv_comb_resident_kernel(QcResidentReq *req, uint64_t idle_ticks) {
-  static_assert(sizeof(QcResidentBody) == 64 * 16, "16 bytes per lane");
-  __shared__ uint4 body[64];
-  __shared__ uint32_t cmd_seq, cmd_stop;
+  __shared__ uint32_t payload[kResidentChunks * 3 + 4];  // QcResidentBody, word for word
+  __shared__ uint32_t cmd_seq, cmd_stop, res_fault;
+  __shared__ uint8_t res_flags[kResidentVotes];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const bool chunk_lane = lane < (uint32_t)kResidentChunks;
   uint32_t last = 0;
   if (wave == 0u) {
-    last = req_load(&req->seq);
+    last = __builtin_amdgcn_readfirstlane(load16_uncached(&req->chunk[0]).x);
     if (lane == 0u) __hip_atomic_store(&req->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   for (;;) {
     if (wave == 0u) {
       const uint64_t t0 = wall_clock64();
       uint32_t sq = last, stop = 0;
-      for (;;) {  // every lane polls the same word: one request per poll
-        sq = req_load(&req->seq);
-        stop = req_load(&req->stop);
-        if (sq != last || stop) break;
+      uint4 c = make_uint4(0, 0, 0, 0);
+      for (;;) {
+        if (chunk_lane) c = load16_uncached(&req->chunk[lane]);
+        stop = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&req->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        sq = __builtin_amdgcn_readfirstlane(c.x);
+        // the request is complete when every chunk carries chunk 0's seq and it is new
+        const bool same = !chunk_lane || c.x == sq;
+        if (stop || (sq != last && __all(same))) break;
         if (wall_clock64() - t0 > idle_ticks) {
           stop = 1u;
           break;
@@ -574,36 +587,40 @@ __global__ void __launch_bounds__(kFusedThreads) hsv_comb_resident_kernel(QcResi
         __builtin_amdgcn_s_sleep(1);
       }
       last = sq;
-      if (!stop) {
-        // the body the host wrote before its release store of seq: after the
-        // system-scope acquire no cache holds an older copy, so a plain
-        // 16-byte vector load per lane reads it (one instruction, one trip)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        body[lane] = reinterpret_cast<const uint4 *>(&req->body)[lane];
+      if (!stop && chunk_lane) {
+        payload[3u * lane] = c.y;
+        payload[3u * lane + 1u] = c.z;
+        payload[3u * lane + 2u] = c.w;
       }
       if (lane == 0u) {
         cmd_seq = sq;
         cmd_stop = stop;
+        res_fault = 0u;
       }
+      if (lane < (uint32_t)kResidentVotes) res_flags[lane] = 0u;  // an unwritten flag reads as a rejection
     }
     __syncthreads();
     if (cmd_stop) break;
     const uint32_t sq = cmd_seq;
-    const QcResidentBody &b = *reinterpret_cast<const QcResidentBody *>(body);
+    const QcResidentBody &b = *reinterpret_cast<const QcResidentBody *>(payload);
     const uint32_t m = b.m, nkeys = b.nkeys;
     const bool valid = m >= 1u && m <= (uint32_t)kResidentVotes && m <= (uint32_t)kFusedVotes && nkeys >= 1u &&
                        nkeys <= kResidentMaxKeys && b.pks && b.key_flags && b.key_tables && b.btable;
     if (valid) {  // block-uniform: every wave takes the same branch
       comb_quad_block(b.key_idx, reinterpret_cast<const uint8_t *>(b.sig), 64,
                       reinterpret_cast<const uint8_t *>(b.msg), b.msg_per_vote ? 32 : 0, m, b.pks, b.key_flags,
-                      nkeys, b.key_tables, b.btable, req->flags, b.inject, req->fault, nullptr, 0u,
+                      nkeys, b.key_tables, b.btable, res_flags, b.inject, &res_fault, nullptr, 0u,
                       reinterpret_cast<const uint8_t *>(b.pk));
     }
-    __syncthreads();  // every wave past its reads of this request (LDS included) and its flag stores
+    __syncthreads();  // every wave past its reads of this request and its LDS flag stores
     if (threadIdx.x == 0) {
-      if (!valid) __hip_atomic_store(&req->fault[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __atomic_thread_fence(__ATOMIC_RELEASE);
-      __hip_atomic_store(&req->done, sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      uint32_t fl = 0;
+      for (int i = 0; i < kResidentVotes; ++i) fl |= (uint32_t)res_flags[i] << (8 * i);
+      const uint32_t fb = (res_fault ? kResidentFaultCurve : 0u) | (valid ? 0u : kResidentBadRequest);
+      __hip_atomic_store(&req->answer[0], (uint64_t)sq | ((uint64_t)fl << 32), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&req->answer[1], (uint64_t)sq | ((uint64_t)fb << 32), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
   if (threadIdx.x == 0) __hip_atomic_store(&req->alive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

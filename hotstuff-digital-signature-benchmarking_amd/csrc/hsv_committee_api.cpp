@@ -246,7 +246,7 @@ int resident_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t 
   std::lock_guard<std::mutex> lk(r.mu);
   if (resident_ensure_locked(r, cd.device) != HSV_OK) return kResidentUnavailable;
   QcResidentReq &q = *r.h;
-  QcResidentBody &b = q.body;
+  QcResidentBody b{};  // the payload, chunked into the request area at each post
   b.m = (uint32_t)m;
   b.nkeys = cd.n;
   b.inject = (uint32_t)hsvi_inject_mode();
@@ -263,24 +263,41 @@ int resident_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t 
     if (msg_stride) std::memcpy(b.msg[i], msg + i * msg_stride, 32);
   }
   if (!msg_stride) std::memcpy(b.msg[0], msg, 32);
-  std::memset(q.flags, 0, sizeof(q.flags));  // an unwritten flag reads as a rejection
-  std::memset(q.fault, 0, sizeof(q.fault));
+  uint32_t words[kResidentChunks * 3];
+  std::memcpy(words, &b, sizeof(b));
   call_mark(HSV_MARK_STAGED);
+  // Each chunk's payload words, then its seq (a release store: the compiler
+  // keeps the order, and x86 makes stores visible in program order), so a
+  // chunk read with the new seq holds the new payload.
+  auto post = [&](uint32_t sq) {
+    for (int c = 0; c < kResidentChunks; ++c) {
+      QcResidentChunk &ch = q.chunk[c];
+      ch.w[0] = words[3 * c];
+      ch.w[1] = words[3 * c + 1];
+      ch.w[2] = words[3 * c + 2];
+      __atomic_store_n(&ch.seq, sq, __ATOMIC_RELEASE);
+    }
+  };
   // One retry: the kernel may leave on its idle timer just as a request is
   // posted (it read the doorbell before the store); then it is relaunched
   // and the same request posted again under a new number.
+  uint64_t a0 = 0, a1 = 0;
   for (int attempt = 0;; ++attempt) {
     const uint32_t sq = ++r.seq == 0 ? ++r.seq : r.seq;  // never 0
-    __atomic_store_n(&q.seq, sq, __ATOMIC_RELEASE);      // everything above is visible first
+    post(sq);
     ++r.posted;
     call_mark(HSV_MARK_LAUNCH);
     const auto t0 = std::chrono::steady_clock::now();
-    bool answered = true;
-    while (__atomic_load_n(&q.done, __ATOMIC_ACQUIRE) != sq)
-      if (std::chrono::steady_clock::now() - t0 > kResidentWait) {
-        answered = false;
+    bool answered = false;
+    for (;;) {  // both 8-byte answer words carry this request's seq
+      a0 = __atomic_load_n(&q.answer[0], __ATOMIC_ACQUIRE);
+      a1 = __atomic_load_n(&q.answer[1], __ATOMIC_ACQUIRE);
+      if ((uint32_t)a0 == sq && (uint32_t)a1 == sq) {
+        answered = true;
         break;
       }
+      if (std::chrono::steady_clock::now() - t0 > kResidentWait) break;
+    }
     if (answered) break;
     if (attempt == 0 && __atomic_load_n(&q.alive, __ATOMIC_ACQUIRE) == 0u &&
         resident_ensure_locked(r, cd.device) == HSV_OK)
@@ -293,13 +310,13 @@ int resident_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t 
   }
   ++r.answered;
   call_mark(HSV_MARK_SYNC);
-  uint32_t fw[3];
-  std::memcpy(fw, q.fault, sizeof(fw));
-  if (fw[2])
+  const uint32_t fb = (uint32_t)(a1 >> 32), fl = (uint32_t)(a0 >> 32);
+  if (fb & kResidentBadRequest)
     return fail(HSV_ERR_DEVICE_FAULT, "committee verify (resident): the kernel refused the request header");
+  const uint32_t fw[2] = {fb & kResidentFaultCurve, fb & kResidentFaultCanary};
   const int rc = check_faults(reinterpret_cast<const uint8_t *>(fw), "committee verify (resident)");
   if (rc != HSV_OK) return rc;
-  std::memcpy(flags_out, q.flags, m);
+  for (size_t i = 0; i < m; ++i) flags_out[i] = (uint8_t)(fl >> (8 * i));
   call_mark(HSV_MARK_DONE);
   return HSV_OK;
 }

@@ -75,13 +75,18 @@ double hsv_launch_mad_peak(int device_cus);
 
 // ---- committee key cache (hsv_committee.hip) -----------------------------
 // Request block of the resident committee service (hsv_comb_resident_kernel,
-// csrc/hsv_committee.hip), in coherent pinned host memory.  The host fills
-// `body` and the answer words, then bumps `seq` with a release store; the
-// kernel sees the new seq, performs a system-scope acquire, reads the whole
-// body in ONE vector load (64 lanes x 16 bytes), validates it, and answers
-// with `done` = seq after a release.  kResidentVotes votes at most.
+// csrc/hsv_committee.hip), in coherent pinned host memory.  The request's
+// payload (QcResidentBody, 144 words) travels in 48 chunks of 16 bytes, each
+// {seq, three payload words}: the host writes a chunk's payload words, then
+// its seq with a release store (x86 keeps stores in order), so a 16-byte
+// read that finds the new seq in a chunk finds that chunk's new payload.  The
+// kernel polls all 48 chunks with ONE vector load (one 16-byte read per lane)
+// and takes the request once every chunk carries the same new seq -- the
+// doorbell and the body in one PCIe round trip, no acquire fence.  It answers
+// with two 8-byte stores {seq, flags} and {seq, fault bits}, each a single
+// transaction, so the host needs no fence on its side either.
 constexpr int kResidentVotes = 4;
-struct QcResidentBody {                  // 1 KiB, word offsets fixed (the kernel reads it raw)
+struct QcResidentBody {                  // 144 words, offsets fixed (the kernel reads them raw)
   uint32_t m, nkeys, inject, msg_per_vote;  // votes (1..kResidentVotes), members, fault injection, 0/1
   const uint8_t *pks;                    // the committee view's device arrays
   const uint8_t *key_flags;
@@ -91,15 +96,20 @@ struct QcResidentBody {                  // 1 KiB, word offsets fixed (the kerne
   uint32_t sig[kResidentVotes][16];      // word 16: R || s per vote
   uint32_t msg[kResidentVotes][8];       // word 80: one digest per vote, or the shared digest in msg[0]
   uint32_t pk[kResidentVotes][8];        // word 112: each vote's key encoding (the member's, byte for byte)
-  uint32_t spare[112];
 };
-static_assert(sizeof(QcResidentBody) == 1024, "one 64-lane x 16-byte load");
+constexpr int kResidentChunks = 48;      // 3 payload words each
+static_assert(sizeof(QcResidentBody) == kResidentChunks * 3 * 4, "48 chunks of three words");
+struct alignas(16) QcResidentChunk {
+  uint32_t seq, w[3];
+};
+// answer bits besides the flags: bit 0 / 1 the self-check words of the
+// launched form (curve check, canary), bit 2 the request header was refused
+constexpr uint32_t kResidentFaultCurve = 1u, kResidentFaultCanary = 2u, kResidentBadRequest = 4u;
 struct QcResidentReq {
-  uint32_t seq, stop, alive, done;       // doorbell, stop word, set while the kernel runs, completion
-  uint32_t pad0[12];
-  QcResidentBody body;
-  uint32_t fault[8];                     // [0..1] self-check words (launched form's layout), [2] invalid request
-  uint8_t flags[16];
+  uint32_t stop, alive, pad0[14];        // host: stop word; kernel: set while it runs
+  QcResidentChunk chunk[64];             // [0, kResidentChunks): the request
+  uint64_t answer[2];                    // kernel: seq | flags << 32, seq | fault bits << 32
+  uint32_t pad1[12];
 };
 
 #ifdef __cplusplus
