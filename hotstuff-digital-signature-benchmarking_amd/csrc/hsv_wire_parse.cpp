@@ -235,8 +235,15 @@ bool parse_tc(const uint8_t *buf, size_t len, TcParsed &out, std::string &err) {
   out.sigs.resize(out.n * 64);
   out.digests.resize(out.n * 32);
   // the per-vote digest depends only on (round, high_qc_round), and a TC's
-  // high_qc_rounds take few distinct values: hash each once
-  std::unordered_map<uint64_t, std::array<uint8_t, 32>> memo;
+  // high_qc_rounds take few distinct values (the last rounds before a
+  // timeout): hash each once.  A small array searched from the last hit, not
+  // a hash map -- no allocation per call, and a C3 TC's 667 lookups cost a
+  // few compares each (the map made the parse ~28 us of a 0.092 ms bincode
+  // TC on the GPU box, profiles/r05e_bench_detail.json).
+  constexpr size_t kMemo = 32;
+  uint64_t memo_key[kMemo];
+  uint8_t memo_dig[kMemo][32];
+  size_t memo_n = 0, memo_last = 0;
   for (size_t i = 0; i < out.n; ++i) {
     const uint8_t *sig = nullptr;
     uint64_t hqc = 0;
@@ -249,17 +256,27 @@ bool parse_tc(const uint8_t *buf, size_t len, TcParsed &out, std::string &err) {
       return false;
     }
     std::memcpy(out.sigs.data() + i * 64, sig, 64);
-    auto it = memo.find(hqc);
-    if (it == memo.end()) {
-      uint8_t pre[16], h[64];
-      put_le64(pre, out.round);
-      put_le64(pre + 8, hqc);
-      hsv::sha512_bytes(pre, sizeof(pre), h);
-      std::array<uint8_t, 32> d;
-      std::memcpy(d.data(), h, 32);
-      it = memo.emplace(hqc, d).first;
+    uint8_t *dig = out.digests.data() + i * 32;
+    size_t k = memo_last;
+    if (memo_n == 0 || memo_key[k] != hqc) {
+      for (k = 0; k < memo_n && memo_key[k] != hqc; ++k) {
+      }
     }
-    std::memcpy(out.digests.data() + i * 32, it->second.data(), 32);
+    if (k < memo_n) {
+      memo_last = k;
+      std::memcpy(dig, memo_dig[k], 32);
+      continue;
+    }
+    uint8_t pre[16], h[64];
+    put_le64(pre, out.round);
+    put_le64(pre + 8, hqc);
+    hsv::sha512_bytes(pre, sizeof(pre), h);
+    std::memcpy(dig, h, 32);
+    if (memo_n < kMemo) {  // beyond kMemo distinct values every new one is hashed
+      memo_key[memo_n] = hqc;
+      std::memcpy(memo_dig[memo_n], h, 32);
+      memo_last = memo_n++;
+    }
   }
   if (r.left != 0) {
     err = "trailing bytes after the TC";
