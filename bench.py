@@ -814,6 +814,9 @@ def parse_args(argv=None):
                     help="repetitions per latency figure (BASELINE.md: >= 1,000 for C2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-qc", action="store_true")
+    ap.add_argument("--qc", action="store_true",
+                    help="run the latency legs at N > 1 too (by default they run at N = 1 only: the QC p50 is a "
+                         "one-GPU metric, and the other ranks would wait minutes at the final barrier)")
     ap.add_argument("--global-n", type=int, default=None,
                     help="C5 strong scaling: total triples split over the ranks (e.g. 16777216 = 2^24); "
                          "default: weak scaling with --n per GPU")
@@ -901,6 +904,8 @@ def main():
         a.n = a.global_n // world
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not a.qc:
+        a.no_qc = True
 
     import torch.distributed as dist
     if a.dry_run:

@@ -815,6 +815,149 @@ hsv_verify_row_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const 
   }
 }
 
+// Quad form of the latency kernel (default at <= kQuadMax items, round 5):
+// one item per block of three waves.  Wave 0 holds R, wave 1 holds A, each as
+// one point per WAVE whose four rows compute the four independent products of
+// every formula round at once (hsv_rowpoint.hpp q_*), so a doubling costs two
+// row products instead of eight.  Each of the two waves decompresses its point
+// (the two-row chain, run by both row pairs), builds [0..8](-P) in LDS, runs
+// its one-scalar Straus (c1 for R, |c0| for A) and half of the wide B comb;
+// wave 2 runs the scalar prepass meanwhile.  The A wave hands its sum over in
+// LDS and the R wave adds it and checks.  Fallback items (no short lattice
+// pair) run the full-length one-lane path on lane 0 of the R wave.  Same
+// flags, self-checks and canaries as the row form.
+constexpr uint32_t kQuadMax = 256;
+#ifdef HSV_QUAD_CLOCKS
+// Measurement builds only (tools/build_ab_libs.sh quadclk "-DHSV_QUAD_CLOCKS"):
+// lane 0 of each wave of block 0 stamps the 100 MHz clock at fixed points
+// (0 entry, 1 decompressed / prepass done, 2 table built, 3 past barrier 1,
+// 4 Straus done, 5 comb half done, 6 past barrier 2, 7 exit).
+__device__ uint64_t g_quad_clk[3][8];
+#define HSV_QUAD_CLK(w, slot)                                                  \
+  do {                                                                         \
+    if (blockIdx.x == 0u && (threadIdx.x & 63u) == 0u) g_quad_clk[w][slot] = wall_clock64(); \
+  } while (0)
+#else
+#define HSV_QUAD_CLK(w, slot) \
+  do {                        \
+  } while (0)
+#endif
+template <int WA, int CB>
+__global__ void __launch_bounds__(3 * 64)
+hsv_verify_quad_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const uint8_t *__restrict__ sig,
+                       uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
+                       uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
+                       uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b, int lat_bits,
+                       uint32_t *__restrict__ canary, uint32_t nonce, uint32_t inject, uint32_t *__restrict__ fault) {
+  using G = HalfCombWindows<WA>;
+  constexpr int TS = 1 << (WA - 1);
+  constexpr int kEnt = TS + 1;
+  __shared__ uint32_t srec[kPrepWords];
+  __shared__ uint32_t stab[2][kEnt * 64];
+  __shared__ uint32_t sq_a[4 * 16];   // the A wave's sum, cached form (component r on row r)
+  __shared__ uint32_t s_a[2];         // the A wave's ok, small
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint32_t item = blockIdx.x;
+  const uint32_t li = item < n ? item : n - 1u;
+  HSV_QUAD_CLK(wave, 0);
+  if (wave == 2) {
+    if (lane == 0u) {
+      uint32_t pkw[8], sigw[16], msgw[8];
+      load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, li, pkw, sigw, msgw);
+      (void)prep_scalars<WA>(pkw, sigw, msgw, srec, 1, lat_bits);
+    }
+    HSV_QUAD_CLK(2, 1);
+    __syncthreads();
+    HSV_QUAD_CLK(2, 3);
+    __syncthreads();
+    HSV_QUAD_CLK(2, 6);
+    return;
+  }
+  const uint32_t role = wave;  // 0: R, 1: A
+  const uint32_t slot = blockIdx.x * 2u + role;
+  if (lane == 0u) canary[slot] = inject == kInjectCanary ? ~nonce : nonce;
+  uint32_t ok, small, nc = 0;
+  uint32_t *tab = stab[role];
+  {
+    const RowLane2 L2;
+    uint32_t enc[8];
+    const uint4 *ep = reinterpret_cast<const uint4 *>(role ? pk + (uint64_t)li * pk_stride : sig + (uint64_t)li * sig_stride);
+    const uint4 e0 = ep[0], e1 = ep[1];
+    enc[0] = e0.x; enc[1] = e0.y; enc[2] = e0.z; enc[3] = e0.w;
+    enc[4] = e1.x; enc[5] = e1.y; enc[6] = e1.z; enc[7] = e1.w;
+    fe x, y;
+    ok = ge_decompress_row(enc, x, y, small, nc, L2);  // both row pairs, the same chain
+    small &= ok;
+    HSV_QUAD_CLK(role, 1);
+    const QuadLane L;
+    quad_table_build<TS>(tab, x, y, L, inject, role == 0u);
+    HSV_QUAD_CLK(role, 2);
+  }
+  __syncthreads();
+  HSV_QUAD_CLK(role, 3);
+  const QuadLane L;
+  const uint32_t meta = srec[kPrepWords - 1];
+  uint32_t f = 0, bad = 0;
+  qp_ext q{};
+  if (!(meta & kPrepFallback)) {
+    uint32_t d[5];
+    HSV_UNROLL
+    for (int i = 0; i < 5; ++i) d[i] = srec[i + 5 * (int)role];
+    q = quad_straus<WA, G::NW>(d, tab, (role && (meta & kPrepC0Neg)) ? 1u : 0u, L);
+    HSV_QUAD_CLK(role, 4);
+    uint32_t b[8];
+    HSV_UNROLL
+    for (int i = 0; i < 8; ++i) b[i] = srec[10 + i];
+    q = quad_comb_half<CB>(q, b, comb_b, role, L);
+    HSV_QUAD_CLK(role, 5);
+    if (role == 1u) {
+      sq_a[L.r * 16u + L.k] = q_cached_component(q, fl_from_fe(fe_d2(), L), L);
+      if (lane == 0u) {
+        s_a[0] = ok;
+        s_a[1] = small;
+      }
+    }
+  }
+  __syncthreads();
+  HSV_QUAD_CLK(role, 6);
+  if (role == 1u) {
+    report_faults(fault, nc | (canary[slot] != nonce ? 2u : 0u));
+    return;
+  }
+  if (meta & kPrepFallback) {
+    if (lane == 0u) {
+      GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)slot * vt_lane_uint4<WA>(), inject};
+      uint32_t pkw[8], sigw[16], msgw[8];
+      load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, li, pkw, sigw, msgw);
+      f = verify_one_full_comb<WA, false, CB>(pkw, sigw, msgw, comb_b, vt);
+      bad = (f & kFault) ? 1u : 0u;
+    }
+  } else {
+    // Q = the R wave's sum + the A wave's (its cached form from LDS)
+    const uint32_t c = sq_a[(L.r ^ (L.r < 2u ? 1u : 0u)) * 16u + L.k];  // row 0: YmX, row 1: YpX
+    const uint32_t op = L.r == 2u ? sq_a[3u * 16u + L.k] : L.r == 3u ? sq_a[2u * 16u + L.k] : c;
+    q = q_add_op(q, op, L);
+    const uint32_t a_ok = s_a[0], small_a = s_a[1];
+    const RowLane &R = L;
+    ge_ext qe;
+    qe.X = fl_to_fe(q.X, R, nc);
+    qe.Y = fl_to_fe(q.Y, R, nc);
+    qe.Z = fl_to_fe(q.Z, R, nc);
+    qe.T = qe.Z;
+    uint32_t z_nonzero;
+    const uint32_t sane = ge_is_sane_row(qe, z_nonzero);
+    const uint32_t same = fe_is_zero(qe.X) & fe_eq(qe.Y, qe.Z) & z_nonzero;  // ge_is_neutral
+    f = flags_byte(meta & kPrepSOk, a_ok, ok, small_a, small, same);
+    bad = (a_ok & ok & (sane ^ 1u)) ? 1u : 0u;
+  }
+  report_faults(fault, bad | nc | (canary[slot] != nonce ? 2u : 0u));
+  if (item < n && lane == 0u) {
+    if (flags_out) flags_out[item] = (uint8_t)f;
+    if (strict_bits && (f & kStrictOk)) atomicOr(&strict_bits[item >> 5], 1u << (item & 31u));
+  }
+  HSV_QUAD_CLK(0, 7);
+}
+
 #if HSV_ALL_VARIANTS
 // Point pass with a pair-lane tail (variant 22): as hsv_verify_hp_kernel, but
 // the last n_tail items (a multiple-of-64 boundary, about one round of the
@@ -1285,6 +1428,38 @@ hipError_t launch_row(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig,
   return e != hipSuccess ? e : ef;
 }
 
+// Quad form (variant 21 at <= kQuadMax items): one item per block of three
+// waves.  The workspace holds one full-length table and one canary per point
+// wave (the fallback path's tables; the quad tables live in LDS).
+template <int WA, int CB>
+hipError_t launch_quad(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
+                       const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
+                       uint32_t *strict_bits, const uint32_t *comb_b, uint32_t *fault, hipStream_t stream,
+                       void *ws_in = nullptr, size_t ws_cap = 0, size_t *ws_need = nullptr) {
+  const uint32_t grid = n;
+  const size_t slots = (size_t)grid * 2u;
+  const size_t ws_bytes = slots * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
+  const size_t need = ws_bytes + slots * sizeof(uint32_t);
+  if (ws_need) {
+    *ws_need = need;
+    return hipSuccess;
+  }
+  void *ws = ws_in && ws_cap >= need ? ws_in : nullptr;
+  const bool own = ws == nullptr;
+  hipError_t e = own ? hsv_ws_malloc(&ws, need, stream) : hipSuccess;
+  if (e != hipSuccess) return e;
+  if (strict_bits) e = hipMemsetAsync(strict_bits, 0, (size_t)((n + 31u) / 32u) * 4u, stream);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL((hsv::hsv_verify_quad_kernel<WA, CB>), dim3(grid), dim3(3 * 64), 0, stream, pk, pk_stride,
+                       sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, static_cast<uint4 *>(ws), comb_b,
+                       g_lat_bits.load(), reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(ws) + ws_bytes),
+                       next_nonce(), t_inject, fault);
+    e = hipGetLastError();
+  }
+  const hipError_t ef = own ? hipFreeAsync(ws, stream) : hipSuccess;
+  return e != hipSuccess ? e : ef;
+}
+
 }  // namespace
 
 extern "C" hipError_t hsv_launch_verify_ws(int variant, const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig,
@@ -1296,6 +1471,9 @@ extern "C" hipError_t hsv_launch_verify_ws(int variant, const uint8_t *pk, uint6
     return hsv_launch_verify(variant, pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits,
                              comb_b, fault, stream);
   if (!comb_b || !fault) return hipErrorInvalidValue;
+  if (variant == 21 && n <= hsv::kQuadMax)
+    return launch_quad<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b,
+                              fault, stream, ws, ws_cap);
   if (variant == 21 && n <= row_max())
     return launch_row<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b,
                              fault, stream, ws, ws_cap);
@@ -1308,7 +1486,10 @@ extern "C" hipError_t hsv_launch_verify_ws(int variant, const uint8_t *pk, uint6
 
 extern "C" size_t hsv_launch_ws_bytes(int variant, uint32_t n) {
   size_t need = 0;
-  if (variant == 21 && n <= row_max())
+  if (variant == 21 && n <= hsv::kQuadMax)
+    (void)launch_quad<4, 16>(nullptr, 0, nullptr, 0, nullptr, 0, n, nullptr, nullptr, nullptr, nullptr, nullptr,
+                             nullptr, 0, &need);
+  else if (variant == 21 && n <= row_max())
     (void)launch_row<4, 16>(nullptr, 0, nullptr, 0, nullptr, 0, n, nullptr, nullptr, nullptr, nullptr, nullptr,
                             nullptr, 0, &need);
   else if (variant == 21 && n <= kPairMax)
@@ -1333,6 +1514,9 @@ extern "C" hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t
       return launch_hp<4, 3, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b,
                                  fault, stream);
     case 21:
+      if (n <= hsv::kQuadMax)
+        return launch_quad<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b,
+                                  fault, stream);
       if (n <= row_max())
         return launch_row<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b,
                                  fault, stream);
@@ -1498,5 +1682,14 @@ extern "C" __attribute__((visibility("default"))) int hsv_phase_clocks_read(uint
     if (hipMemset(p, 0, (size_t)hsv::kPhaseCap * 8 * sizeof(uint64_t)) != hipSuccess) return -1;
   }
   return 0;
+}
+#endif
+
+#ifdef HSV_QUAD_CLOCKS
+// Measurement builds only: block 0's stamps of the last quad-form launch (3
+// waves x 8 u64, 100 MHz); 0 or -1 on a HIP error.
+extern "C" __attribute__((visibility("default"))) int hsv_quad_clocks(uint64_t *out) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(hsv::g_quad_clk), sizeof(hsv::g_quad_clk)) == hipSuccess ? 0 : -1;
 }
 #endif

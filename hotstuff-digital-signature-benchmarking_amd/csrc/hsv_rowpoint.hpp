@@ -203,5 +203,184 @@ __device__ __forceinline__ rp_ext row_comb_half(rp_ext q, const uint32_t s[8], c
   return q;
 }
 
+// ---- one point per wave, the formulas' four products on the four rows ----
+// The HWCD formulas above are two rounds of four independent products each:
+// a doubling squares X, Y, Z and X + Y, then forms E F, G H, F G, E H; an
+// addition multiplies (Y - X, Y + X, T, Z) by the other point's four
+// components, then forms the same four products.  Here every row of a wave
+// holds the whole point (row-form limbs, lane k of each row holding limb k of
+// X, Y, Z and T) and row r computes product r of each round with fl_mul on
+// RowLane -- four products in the time of one -- then three permlane swaps
+// give every row all four results.  Against RowLane2, which splits each
+// product of the same sequence over two rows, a doubling issues ~135
+// instructions instead of ~330.  The values are those of rp_dbl /
+// rp_add_cached / rp_add_niels operation for operation (the Niels addition's D
+// = 2 Z is computed as Z * 2 on row 3), so tools/lanesplit_model.py's bounds
+// carry over.
+struct QuadLane : RowLane {
+  uint32_t r;  // row of the wave: which product of a round this lane's row computes
+  __device__ __forceinline__ QuadLane() : RowLane() { r = (__lane_id() >> 4) & 3u; }
+};
+
+struct qp_ext {
+  uint32_t X, Y, Z, T;
+};
+
+// a0 on row 0, a1 on row 1, a2 on row 2, a3 on row 3
+__device__ __forceinline__ uint32_t qsel(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
+  uint32_t x;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(x) : "v"(a0), "v"(a1), "s"(0x00000000ffff0000ull));
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(x) : "v"(x), "v"(a2), "s"(0x0000ffff00000000ull));
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(x) : "v"(x), "v"(a3), "s"(0xffff000000000000ull));
+  return x;
+}
+
+// rows 0..3's values of v, on every row: v_permlane16_swap leaves the even
+// row's value of each row pair in result 0 and the odd row's in result 1, on
+// both rows of the pair; v_permlane32_swap does the same for the two halves
+__device__ __forceinline__ void qgather(uint32_t v, uint32_t &v0, uint32_t &v1, uint32_t &v2, uint32_t &v3) {
+  const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  const auto q0 = __builtin_amdgcn_permlane32_swap(p[0], p[0], false, false);
+  const auto q1 = __builtin_amdgcn_permlane32_swap(p[1], p[1], false, false);
+  v0 = q0[0];
+  v1 = q1[0];
+  v2 = q0[1];
+  v3 = q1[1];
+}
+
+// round 2 of every formula: X3 = E F, Y3 = G H, Z3 = F G, T3 = E H
+__device__ __forceinline__ qp_ext q_finish(uint32_t E, uint32_t F, uint32_t G, uint32_t H, const QuadLane &L) {
+  const uint32_t t = fl_mul(qsel(E, G, F, E), qsel(F, H, G, H), L);
+  qp_ext r;
+  qgather(t, r.X, r.Y, r.Z, r.T);
+  return r;
+}
+
+// 2P (rp_dbl, T always formed)
+__device__ __forceinline__ qp_ext q_dbl(const qp_ext &p, const QuadLane &L) {
+  const uint32_t s = fl_sq(qsel(p.X, p.Y, p.Z, p.X + p.Y), L);
+  uint32_t A, B, C, S;
+  qgather(s, A, B, C, S);
+  const uint32_t H = A + B;
+  return q_finish(fl_sub(H, S, L), fl_carry(C + C + fl_sub(A, B, L), L), fl_sub(A, B, L), H, L);
+}
+
+// P + Q given Q's operand for this row: row 0 (y - x)', row 1 (y + x)', row 2
+// the T factor (2dT, or 2dxy for a Niels entry), row 3 the Z factor (2Z, or 2
+// for a Niels entry) -- rp_add_cached / rp_add_niels
+__device__ __forceinline__ qp_ext q_add_op(const qp_ext &p, uint32_t op, const QuadLane &L) {
+  const uint32_t s = fl_mul(qsel(fl_sub(p.Y, p.X, L), p.Y + p.X, p.T, p.Z), op, L);
+  uint32_t A, B, C, D;
+  qgather(s, A, B, C, D);
+  return q_finish(fl_sub(B, A, L), fl_sub(D, C, L), D + C, B + A, L);
+}
+
+// this row's component of P's cached form (rp_to_cached): row 0 Y + X,
+// row 1 Y - X, row 2 2Z, row 3 2dT
+__device__ __forceinline__ uint32_t q_cached_component(const qp_ext &p, uint32_t d2, const QuadLane &L) {
+  const uint32_t t2d = fl_mul(p.T, d2, L);
+  return qsel(p.Y + p.X, fl_sub(p.Y, p.X, L), p.Z + p.Z, t2d);
+}
+
+// this row's operand for adding a cached entry (components c = 0 YpX, 1 YmX,
+// 2 Z2, 3 T2d of cmp_of(c)), negated when neg (swap YpX / YmX, -2dT)
+__device__ __forceinline__ uint32_t q_cached_col(uint32_t r, uint32_t neg) {
+  // row 0 wants YmX (YpX when negated), row 1 YpX (YmX), row 2 T2d, row 3 Z2
+  return r < 2u ? (r ^ (neg ? 0u : 1u)) : (r == 2u ? 3u : 2u);
+}
+
+// The wave's variable-base table in LDS, entries m = 0..TS of [m](-P) in
+// cached form at tab[(m * 4 + c) * 16 + k] (row_table_build's layout): built
+// as [m](-P) = [m-1](-P) + (-P), -P as an affine Niels operand.
+template <int TS>
+__device__ __forceinline__ void quad_table_build(uint32_t *tab, const fe &x, const fe &y, const QuadLane &L,
+                                                 uint32_t inject, bool flip_this_table) {
+  const uint32_t nx = fl_from_fe(fe_carry(fe_neg(x)), L);  // -x
+  const uint32_t yl = fl_from_fe(y, L);
+  const uint32_t d2 = fl_from_fe(fe_d2(), L);
+  const uint32_t t1 = fl_mul(nx, yl, L);
+  const uint32_t ypx = yl + nx, ymx = fl_sub(yl, nx, L), xy2d = fl_mul(t1, d2, L);
+  auto put = [&](int m, uint32_t v) {  // this row's component c = r of entry m
+    if (m > 0 && inject == kInjectZeroTables) v = 0u;
+    if (m > 0 && inject == kInjectFlipTables && flip_this_table && L.k == 0u && L.r == 0u) v ^= 1u;
+    tab[(m * 4 + (int)L.r) * 16 + L.k] = v;
+  };
+  put(0, qsel(fl_small(1, L), fl_small(1, L), fl_small(2, L), 0u));
+  put(1, qsel(ypx, ymx, fl_small(2, L), xy2d));
+  const uint32_t op = qsel(ymx, ypx, xy2d, fl_small(2, L));  // -P as a Niels operand
+  qp_ext p{nx, yl, fl_small(1, L), t1};
+  HSV_NOUNROLL
+  for (int m = 2; m <= TS; ++m) {
+    p = q_add_op(p, op, L);
+    put(m, q_cached_component(p, d2, L));
+  }
+}
+
+// One-scalar Straus over the wave's table (row_straus).  T is valid on return.
+template <int WA, int NW>
+__device__ __forceinline__ qp_ext quad_straus(uint32_t d[5], const uint32_t *tab, uint32_t flip, const QuadLane &L) {
+  constexpr int TS = 1 << (WA - 1);
+  qp_ext q{0u, fl_small(1, L), fl_small(1, L), 0u};
+  int top = NW - 1;
+  HSV_NOUNROLL
+  while (top > 0) {
+    if (__ballot(((d[4] >> (32 - WA)) ^ (uint32_t)TS) != 0u)) break;
+    limbs_shl<5>(d, WA);
+    --top;
+  }
+  HSV_NOUNROLL
+  for (int i = top; i >= 0; --i) {
+    uint32_t neg;
+    const uint32_t m = digit_mag<TS>(d[4] >> (32 - WA), neg);
+    limbs_shl<5>(d, WA);
+    neg ^= flip;
+    uint32_t op = tab[(m * 4u + q_cached_col(L.r, neg)) * 16u + L.k];
+    if (neg && L.r == 2u) op = fl_sub(0u, op, L);
+    if (i != top) {
+      HSV_NOUNROLL
+      for (int j = 0; j < WA; ++j) q = q_dbl(q, L);
+    }
+    q = q_add_op(q, op, L);
+  }
+  return q;
+}
+
+// q + the comb digits of half h of s (row_comb_half), each row reading only
+// the coordinate its product needs; the half's entries are loaded up front so
+// their latency overlaps the additions
+template <int CB>
+__device__ __forceinline__ qp_ext quad_comb_half(qp_ext q, const uint32_t s[8], const uint32_t *tb, uint32_t h,
+                                                 const QuadLane &L) {
+  constexpr int NP = 256 / CB, HALF = NP / 2;
+  constexpr int ENT = 1 << (CB - 1);
+  uint32_t sr[9];
+  recode_add<9, CB, NP>(s, 8, sr);
+  HSV_UNROLL
+  for (int i = 0; i < 4; ++i) sr[i] = h ? sr[i + 4] : sr[i];
+  const uint32_t wsel = L.k >> 1, hs = (L.k & 1u) * 16u;
+  uint32_t op[HALF];
+  HSV_UNROLL
+  for (int j = 0; j < HALF; ++j) {
+    const uint32_t cb = sr[0] & ((1u << CB) - 1u);
+    HSV_UNROLL
+    for (int i = 0; i < 3; ++i) sr[i] = (sr[i] >> CB) | (sr[i + 1] << (32 - CB));
+    sr[3] >>= CB;
+    const int32_t dg = (int32_t)cb - (1 << (CB - 1));
+    const uint32_t neg = dg < 0, mag = (uint32_t)(neg ? -dg : dg);
+    const uint32_t idx = mag == 0u ? 0u : mag - 1u;
+    const uint32_t *e = tb + ((uint64_t)(j + (int)h * HALF) * ENT + idx) * kCombEntryWords;
+    // row 0: y - x (y + x when negated), row 1: y + x (y - x), row 2: 2dxy (negated), row 3: 2
+    const uint32_t coord = L.r == 2u ? 16u : (L.r ^ (neg ? 1u : 0u)) == 0u ? 8u : 0u;
+    uint32_t v = L.r == 3u ? 0u : (e[coord + wsel] >> hs) & 0xffffu;
+    if (mag == 0u) v = L.r == 2u ? 0u : fl_small(1, L);
+    if (L.r == 3u) v = fl_small(2, L);
+    if (neg && L.r == 2u && mag != 0u) v = fl_sub(0u, v, L);
+    op[j] = v;
+  }
+  HSV_UNROLL
+  for (int j = 0; j < HALF; ++j) q = q_add_op(q, op[j], L);
+  return q;
+}
+
 }  // namespace hsv
 #endif

@@ -46,8 +46,10 @@ def test_golden_every_variant(api, golden):
 def test_golden_row_form_chunks(api, golden):
     """Batches at or below the row form's cut-over (row_max(), 3072 items)
     run hsv_verify_row_kernel: the golden records in chunks of 1000 (one row
-    per element) and of 700 (at or below 768 items: two rows per element), and
-    in ragged small batches (1, 5, 7, 13 items: partial blocks), every flag bit
+    per element) and of 700 (at or below 768 items: two rows per element);
+    at or below kQuadMax (256) the quad form, hsv_verify_quad_kernel (one
+    point per wave, the formulas' four products on the four rows): chunks of
+    256 and 200, and ragged small batches (1, 5, 7, 13 items); every flag bit
     against the fixtures.  The committee cache is off so the generic kernels
     run."""
     _, verifier, _ = api
@@ -56,7 +58,7 @@ def test_golden_row_form_chunks(api, golden):
     lib.hsv_set_auto_committee(0)
     try:
         n = len(golden["flags"])
-        for chunk in (1000, 700):
+        for chunk in (1000, 700, 256, 200):
             for lo in range(0, n, chunk):
                 hi = min(n, lo + chunk)
                 got = verifier.verify_flags(golden["pk"][lo:hi], golden["sig"][lo:hi], golden["msg"][lo:hi])
