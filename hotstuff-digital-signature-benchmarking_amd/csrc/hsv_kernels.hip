@@ -825,8 +825,17 @@ hsv_verify_row_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const 
 // wave 2 runs the scalar prepass meanwhile.  The A wave hands its sum over in
 // LDS and the R wave adds it and checks.  Fallback items (no short lattice
 // pair) run the full-length one-lane path on lane 0 of the R wave.  Same
-// flags, self-checks and canaries as the row form.
-constexpr uint32_t kQuadMax = 256;
+// flags, self-checks and canaries as the row form.  Kernel 95.6 us at one
+// item: decompression 30.7, table 4.0 (the prepass ends at 35.4), Straus 52,
+// comb half 4, checks 3 (profiles/r05j_quad_clocks.txt).  The cut-over: one
+// block per CU runs 0.117 ms at 256 items; from 257 on some SIMDs hold two of
+// these lone-issue waves and the call takes 0.169-0.173 ms
+// (profiles/r05k_cutover.txt), so larger batches take the joint form below
+// (0.130-0.134 ms up to 768 items, profiles/r05l_cutover.txt).
+#ifndef HSV_QUAD_MAX  // measurement builds may move the cut-over (tools/row_cutover_probe.py)
+#define HSV_QUAD_MAX 256
+#endif
+constexpr uint32_t kQuadMax = HSV_QUAD_MAX;
 #ifdef HSV_QUAD_CLOCKS
 // Measurement builds only (tools/build_ab_libs.sh quadclk "-DHSV_QUAD_CLOCKS"):
 // lane 0 of each wave of block 0 stamps the 100 MHz clock at fixed points
@@ -956,6 +965,122 @@ hsv_verify_quad_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const
     if (strict_bits && (f & kStrictOk)) atomicOr(&strict_bits[item >> 5], 1u << (item & 31u));
   }
   HSV_QUAD_CLK(0, 7);
+}
+
+// Joint quad form (variant 21 above kQuadMax, at <= kJointMax items): one
+// item per WAVE, kJointItems point waves and one prepass wave per block, so
+// 768 items still hold one block per CU and one wave per SIMD.  The point
+// wave decompresses R on rows 0-1 and A on rows 2-3 at once (the two-row
+// chain, each pair its own element), builds both tables [0..8](-R),
+// [0..8](-A) in LDS with the quad formulas, then runs one two-scalar Straus
+// (shared doublings, quad_straus2) and the whole wide B comb.  Same flags,
+// fallback, self-checks and canaries as the quad form.
+constexpr uint32_t kJointItems = 3;
+#ifndef HSV_JOINT_MAX  // measurement builds may move the cut-over (tools/row_cutover_probe.py)
+#define HSV_JOINT_MAX 768
+#endif
+constexpr uint32_t kJointMax = HSV_JOINT_MAX;
+template <int WA, int CB>
+__global__ void __launch_bounds__((kJointItems + 1) * 64)
+hsv_verify_joint_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const uint8_t *__restrict__ sig,
+                        uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
+                        uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
+                        uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b, int lat_bits,
+                        uint32_t *__restrict__ canary, uint32_t nonce, uint32_t inject, uint32_t *__restrict__ fault) {
+  using G = HalfCombWindows<WA>;
+  constexpr int TS = 1 << (WA - 1);
+  constexpr int kEnt = TS + 1;
+  constexpr uint32_t K = kJointItems;
+  __shared__ uint32_t srec[kPrepWords * K];
+  __shared__ uint32_t stab[K][2][kEnt * 64];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint32_t base = blockIdx.x * K;
+  if (wave == K) {
+    if (lane < K) {
+      const uint32_t li = base + lane < n ? base + lane : n - 1u;
+      uint32_t pkw[8], sigw[16], msgw[8];
+      load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, li, pkw, sigw, msgw);
+      (void)prep_scalars<WA>(pkw, sigw, msgw, srec + lane, K, lat_bits);
+    }
+    __syncthreads();
+    return;
+  }
+  const uint32_t item = base + wave;
+  const uint32_t li = item < n ? item : n - 1u;
+  const uint32_t slot = blockIdx.x * K + wave;
+  if (lane == 0u) canary[slot] = inject == kInjectCanary ? ~nonce : nonce;
+  uint32_t ok, small, nc = 0;  // rows 0-1: R's, rows 2-3: A's
+  uint32_t *tab_r = stab[wave][0], *tab_a = stab[wave][1];
+  {
+    const RowLane2 L2;
+    const uint32_t role = lane >> 5;  // 0: R, 1: A
+    uint32_t enc[8];
+    const uint4 *ep = reinterpret_cast<const uint4 *>(role ? pk + (uint64_t)li * pk_stride : sig + (uint64_t)li * sig_stride);
+    const uint4 e0 = ep[0], e1 = ep[1];
+    enc[0] = e0.x; enc[1] = e0.y; enc[2] = e0.z; enc[3] = e0.w;
+    enc[4] = e1.x; enc[5] = e1.y; enc[6] = e1.z; enc[7] = e1.w;
+    fe x, y;
+    ok = ge_decompress_row(enc, x, y, small, nc, L2);  // each row pair its own element
+    small &= ok;
+    const QuadLane L;
+    HSV_NOUNROLL
+    for (uint32_t t = 0; t < 2u; ++t) {
+      // element t (rows 2t, 2t + 1) on every row: v_permlane32_swap puts the
+      // lower half's value in result 0 and the upper half's in result 1
+      fe xt, yt;
+      HSV_UNROLL
+      for (int l = 0; l < kFeLimbs; ++l) {
+        const auto px = __builtin_amdgcn_permlane32_swap(x.v[l], x.v[l], false, false);
+        const auto py = __builtin_amdgcn_permlane32_swap(y.v[l], y.v[l], false, false);
+        xt.v[l] = t ? px[1] : px[0];
+        yt.v[l] = t ? py[1] : py[0];
+      }
+      quad_table_build<TS>(t ? tab_a : tab_r, xt, yt, L, inject, t == 0u);
+    }
+  }
+  __syncthreads();
+  const QuadLane L;
+  const uint32_t meta = srec[(kPrepWords - 1) * K + wave];
+  const uint32_t r_ok = __builtin_amdgcn_readlane(ok, 0), small_r = __builtin_amdgcn_readlane(small, 0);
+  const uint32_t a_ok = __builtin_amdgcn_readlane(ok, 32), small_a = __builtin_amdgcn_readlane(small, 32);
+  uint32_t f = 0, bad = 0;
+  if (meta & kPrepFallback) {
+    if (lane == 0u) {
+      GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)slot * vt_lane_uint4<WA>(), inject};
+      uint32_t pkw[8], sigw[16], msgw[8];
+      load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, li, pkw, sigw, msgw);
+      f = verify_one_full_comb<WA, false, CB>(pkw, sigw, msgw, comb_b, vt);
+      bad = (f & kFault) ? 1u : 0u;
+    }
+  } else {
+    uint32_t d1[5], d0[5], b[8];
+    HSV_UNROLL
+    for (int i = 0; i < 5; ++i) {
+      d1[i] = srec[i * K + wave];
+      d0[i] = srec[(5 + i) * K + wave];
+    }
+    HSV_UNROLL
+    for (int i = 0; i < 8; ++i) b[i] = srec[(10 + i) * K + wave];
+    qp_ext q = quad_straus2<WA, G::NW>(d1, d0, tab_r, tab_a, (meta & kPrepC0Neg) ? 1u : 0u, L);
+    HSV_NOUNROLL
+    for (uint32_t h = 0; h < 2u; ++h) q = quad_comb_half<CB>(q, b, comb_b, h, L);
+    const RowLane &R = L;
+    ge_ext qe;
+    qe.X = fl_to_fe(q.X, R, nc);
+    qe.Y = fl_to_fe(q.Y, R, nc);
+    qe.Z = fl_to_fe(q.Z, R, nc);
+    qe.T = qe.Z;
+    uint32_t z_nonzero;
+    const uint32_t sane = ge_is_sane_row(qe, z_nonzero);
+    const uint32_t same = fe_is_zero(qe.X) & fe_eq(qe.Y, qe.Z) & z_nonzero;  // ge_is_neutral
+    f = flags_byte(meta & kPrepSOk, a_ok, r_ok, small_a, small_r, same);
+    bad = (a_ok & r_ok & (sane ^ 1u)) ? 1u : 0u;
+  }
+  report_faults(fault, bad | nc | (canary[slot] != nonce ? 2u : 0u));
+  if (item < n && lane == 0u) {
+    if (flags_out) flags_out[item] = (uint8_t)f;
+    if (strict_bits && (f & kStrictOk)) atomicOr(&strict_bits[item >> 5], 1u << (item & 31u));
+  }
 }
 
 #if HSV_ALL_VARIANTS
@@ -1384,25 +1509,21 @@ hipError_t launch_pair(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig
   return e != hipSuccess ? e : ef;
 }
 
-// Row form (variant 21 at <= row_max() items): kRowItemsOf<RR> items per
-// block of four waves.  The workspace holds one full-length table and one canary per
-// row (the fallback path's tables; the row tables live in LDS).
+// Row form (variant 21 above kJointMax, at <= row_max() items): kRowItemsOf<1>
+// items per block of four waves.  The workspace holds one full-length table
+// and one canary per row (the fallback path's tables; the row tables live in
+// LDS).  The two-rows-per-element form (RR = 2, round 3's default up to 768
+// items, 0.178-0.182 ms) gave way to the joint quad form there (0.130-0.134
+// ms, profiles/r05l_cutover.txt); the kernel template still takes RR, and
+// only RR = 1 is instantiated.
 constexpr uint32_t row_max() { return kRowMaxDefault; }
-
-// Two rows per element up to row2_max() items: 3 items per block, so 768
-// items fill the 256 CUs with one block each (0.169 / 0.205 ms at 64 items,
-// 0.175 / 0.210 at 768, 0.327 / 0.212 at 1024, two rows / one row,
-// profiles/r03zz4_row2_cutover.txt).
-constexpr uint32_t kRow2MaxDefault = 768;
-constexpr uint32_t row2_max() { return kRow2MaxDefault; }
 
 template <int WA, int CB>
 hipError_t launch_row(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
                       const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
                       uint32_t *strict_bits, const uint32_t *comb_b, uint32_t *fault, hipStream_t stream,
                       void *ws_in = nullptr, size_t ws_cap = 0, size_t *ws_need = nullptr) {
-  const bool two = n <= row2_max();
-  const uint32_t items = two ? hsv::kRowItemsOf<2> : hsv::kRowItemsOf<1>;
+  const uint32_t items = hsv::kRowItemsOf<1>;
   const uint32_t grid = (n + items - 1) / items;
   const size_t slots = (size_t)grid * hsv::kRowRows;
   const size_t ws_bytes = slots * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
@@ -1417,8 +1538,7 @@ hipError_t launch_row(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig,
   if (e != hipSuccess) return e;
   if (strict_bits) e = hipMemsetAsync(strict_bits, 0, (size_t)((n + 31u) / 32u) * 4u, stream);
   if (e == hipSuccess) {
-    auto kern = two ? hsv::hsv_verify_row_kernel<WA, CB, 2> : hsv::hsv_verify_row_kernel<WA, CB, 1>;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(4 * 64), 0, stream, pk, pk_stride, sig, sig_stride, msg, msg_stride,
+    hipLaunchKernelGGL((hsv::hsv_verify_row_kernel<WA, CB, 1>), dim3(grid), dim3(4 * 64), 0, stream, pk, pk_stride, sig, sig_stride, msg, msg_stride,
                        n, flags_out, strict_bits, static_cast<uint4 *>(ws), comb_b, g_lat_bits.load(),
                        reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(ws) + ws_bytes), next_nonce(),
                        t_inject, fault);
@@ -1460,6 +1580,39 @@ hipError_t launch_quad(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig
   return e != hipSuccess ? e : ef;
 }
 
+// Joint quad form (variant 21 above kQuadMax, at <= kJointMax items):
+// kJointItems items per block; one full-length table and one canary per
+// point wave in the workspace.
+template <int WA, int CB>
+hipError_t launch_joint(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
+                        const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
+                        uint32_t *strict_bits, const uint32_t *comb_b, uint32_t *fault, hipStream_t stream,
+                        void *ws_in = nullptr, size_t ws_cap = 0, size_t *ws_need = nullptr) {
+  const uint32_t grid = (n + hsv::kJointItems - 1) / hsv::kJointItems;
+  const size_t slots = (size_t)grid * hsv::kJointItems;
+  const size_t ws_bytes = slots * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
+  const size_t need = ws_bytes + slots * sizeof(uint32_t);
+  if (ws_need) {
+    *ws_need = need;
+    return hipSuccess;
+  }
+  void *ws = ws_in && ws_cap >= need ? ws_in : nullptr;
+  const bool own = ws == nullptr;
+  hipError_t e = own ? hsv_ws_malloc(&ws, need, stream) : hipSuccess;
+  if (e != hipSuccess) return e;
+  if (strict_bits) e = hipMemsetAsync(strict_bits, 0, (size_t)((n + 31u) / 32u) * 4u, stream);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL((hsv::hsv_verify_joint_kernel<WA, CB>), dim3(grid), dim3((hsv::kJointItems + 1) * 64), 0,
+                       stream, pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits,
+                       static_cast<uint4 *>(ws), comb_b, g_lat_bits.load(),
+                       reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(ws) + ws_bytes), next_nonce(), t_inject,
+                       fault);
+    e = hipGetLastError();
+  }
+  const hipError_t ef = own ? hipFreeAsync(ws, stream) : hipSuccess;
+  return e != hipSuccess ? e : ef;
+}
+
 }  // namespace
 
 extern "C" hipError_t hsv_launch_verify_ws(int variant, const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig,
@@ -1474,6 +1627,9 @@ extern "C" hipError_t hsv_launch_verify_ws(int variant, const uint8_t *pk, uint6
   if (variant == 21 && n <= hsv::kQuadMax)
     return launch_quad<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b,
                               fault, stream, ws, ws_cap);
+  if (variant == 21 && n <= hsv::kJointMax)
+    return launch_joint<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b,
+                               fault, stream, ws, ws_cap);
   if (variant == 21 && n <= row_max())
     return launch_row<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b,
                              fault, stream, ws, ws_cap);
@@ -1489,6 +1645,9 @@ extern "C" size_t hsv_launch_ws_bytes(int variant, uint32_t n) {
   if (variant == 21 && n <= hsv::kQuadMax)
     (void)launch_quad<4, 16>(nullptr, 0, nullptr, 0, nullptr, 0, n, nullptr, nullptr, nullptr, nullptr, nullptr,
                              nullptr, 0, &need);
+  else if (variant == 21 && n <= hsv::kJointMax)
+    (void)launch_joint<4, 16>(nullptr, 0, nullptr, 0, nullptr, 0, n, nullptr, nullptr, nullptr, nullptr, nullptr,
+                              nullptr, 0, &need);
   else if (variant == 21 && n <= row_max())
     (void)launch_row<4, 16>(nullptr, 0, nullptr, 0, nullptr, 0, n, nullptr, nullptr, nullptr, nullptr, nullptr,
                             nullptr, 0, &need);
@@ -1517,6 +1676,9 @@ extern "C" hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t
       if (n <= hsv::kQuadMax)
         return launch_quad<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b,
                                   fault, stream);
+      if (n <= hsv::kJointMax)
+        return launch_joint<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b,
+                                   fault, stream);
       if (n <= row_max())
         return launch_row<4, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b,
                                  fault, stream);

@@ -345,6 +345,44 @@ __device__ __forceinline__ qp_ext quad_straus(uint32_t d[5], const uint32_t *tab
   return q;
 }
 
+// The two-scalar Straus of one wave holding both tables (the joint form):
+// [c1](-R) + [c0](-A) with shared doublings, digits d1 over tab_r and d0 over
+// tab_a (the sign of c0 flips the A digits), as straus_vt over two tables.
+template <int WA, int NW>
+__device__ __forceinline__ qp_ext quad_straus2(uint32_t d1[5], uint32_t d0[5], const uint32_t *tab_r,
+                                               const uint32_t *tab_a, uint32_t flip_a, const QuadLane &L) {
+  constexpr int TS = 1 << (WA - 1);
+  qp_ext q{0u, fl_small(1, L), fl_small(1, L), 0u};
+  int top = NW - 1;
+  HSV_NOUNROLL
+  while (top > 0) {
+    if (__ballot((((d1[4] >> (32 - WA)) ^ (uint32_t)TS) | ((d0[4] >> (32 - WA)) ^ (uint32_t)TS)) != 0u)) break;
+    limbs_shl<5>(d1, WA);
+    limbs_shl<5>(d0, WA);
+    --top;
+  }
+  HSV_NOUNROLL
+  for (int i = top; i >= 0; --i) {
+    uint32_t n1, n0;
+    const uint32_t m1 = digit_mag<TS>(d1[4] >> (32 - WA), n1);
+    const uint32_t m0 = digit_mag<TS>(d0[4] >> (32 - WA), n0);
+    limbs_shl<5>(d1, WA);
+    limbs_shl<5>(d0, WA);
+    n0 ^= flip_a;
+    uint32_t op1 = tab_r[(m1 * 4u + q_cached_col(L.r, n1)) * 16u + L.k];
+    uint32_t op0 = tab_a[(m0 * 4u + q_cached_col(L.r, n0)) * 16u + L.k];
+    if (n1 && L.r == 2u) op1 = fl_sub(0u, op1, L);
+    if (n0 && L.r == 2u) op0 = fl_sub(0u, op0, L);
+    if (i != top) {
+      HSV_NOUNROLL
+      for (int j = 0; j < WA; ++j) q = q_dbl(q, L);
+    }
+    q = q_add_op(q, op1, L);
+    q = q_add_op(q, op0, L);
+  }
+  return q;
+}
+
 // q + the comb digits of half h of s (row_comb_half), each row reading only
 // the coordinate its product needs; the half's entries are loaded up front so
 // their latency overlaps the additions

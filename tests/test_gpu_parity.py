@@ -45,20 +45,21 @@ def test_golden_every_variant(api, golden):
 
 def test_golden_row_form_chunks(api, golden):
     """Batches at or below the row form's cut-over (row_max(), 3072 items)
-    run hsv_verify_row_kernel: the golden records in chunks of 1000 (one row
-    per element) and of 700 (at or below 768 items: two rows per element);
-    at or below kQuadMax (256) the quad form, hsv_verify_quad_kernel (one
-    point per wave, the formulas' four products on the four rows): chunks of
-    256 and 200, and ragged small batches (1, 5, 7, 13 items); every flag bit
-    against the fixtures.  The committee cache is off so the generic kernels
-    run."""
+    run the latency kernels: the golden records in chunks of 1000 (above
+    kJointMax, 768: hsv_verify_row_kernel, one row per element), of 700 and
+    512 (above kQuadMax, 256: hsv_verify_joint_kernel, one item per wave with
+    R and A decompressed on the two row pairs and one two-scalar Straus), of
+    256 and 200 (hsv_verify_quad_kernel, one point per wave, the formulas'
+    four products on the four rows), and ragged small batches (1, 5, 7, 13
+    items); every flag bit against the fixtures.  The committee cache is off
+    so the generic kernels run."""
     _, verifier, _ = api
     from hsverify import _lib
     lib = _lib.load()
     lib.hsv_set_auto_committee(0)
     try:
         n = len(golden["flags"])
-        for chunk in (1000, 700, 256, 200):
+        for chunk in (1000, 700, 512, 256, 200):
             for lo in range(0, n, chunk):
                 hi = min(n, lo + chunk)
                 got = verifier.verify_flags(golden["pk"][lo:hi], golden["sig"][lo:hi], golden["msg"][lo:hi])
@@ -317,7 +318,7 @@ def test_zero_copy_boundary_vs_c_oracle(api, oracle_lib, n):
     assert (got == exp).all()
 
 
-@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 256, 257, 1000])
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 256, 257, 258, 767, 768, 769, 1000])
 def test_ragged_sizes(api, golden, n):
     _, verifier, _ = api
     idx = np.arange(n) % len(golden["flags"])
