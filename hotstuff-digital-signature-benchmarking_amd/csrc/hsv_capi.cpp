@@ -816,13 +816,17 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
     const int nparts = (int)std::min<size_t>(64, (m * 128 + kPackPart - 1) / kPackPart);
     auto part = [&](int p) {
       const size_t lo = m * p / nparts, hi = m * (p + 1) / nparts;
-      if (pk_stride == 32) std::memcpy(h + pk_off + 32 * lo, pk + (base + lo) * 32, (hi - lo) * 32);
-      else for (size_t i = lo; i < hi; ++i) std::memcpy(h + pk_off + 32 * i, pk + (base + i) * pk_stride, 32);
-      if (sig_stride == 64) std::memcpy(h + sig_off + 64 * lo, sig + (base + lo) * 64, (hi - lo) * 64);
-      else for (size_t i = lo; i < hi; ++i) std::memcpy(h + sig_off + 64 * i, sig + (base + i) * sig_stride, 64);
-      if (msg_stride == 32) std::memcpy(h + msg_off + 32 * lo, msg + (base + lo) * 32, (hi - lo) * 32);
+      // streaming stores (stage_copy, hsv_host.h): the kernels or the DMA
+      // engine read these lines next, from DRAM rather than from this core's
+      // cache; each part fences its own stores
+      if (pk_stride == 32) stage_copy(h + pk_off + 32 * lo, pk + (base + lo) * 32, (hi - lo) * 32);
+      else for (size_t i = lo; i < hi; ++i) stage_copy(h + pk_off + 32 * i, pk + (base + i) * pk_stride, 32);
+      if (sig_stride == 64) stage_copy(h + sig_off + 64 * lo, sig + (base + lo) * 64, (hi - lo) * 64);
+      else for (size_t i = lo; i < hi; ++i) stage_copy(h + sig_off + 64 * i, sig + (base + i) * sig_stride, 64);
+      if (msg_stride == 32) stage_copy(h + msg_off + 32 * lo, msg + (base + lo) * 32, (hi - lo) * 32);
       else if (msg_stride != 0)
-        for (size_t i = lo; i < hi; ++i) std::memcpy(h + msg_off + 32 * i, msg + (base + i) * msg_stride, 32);
+        for (size_t i = lo; i < hi; ++i) stage_copy(h + msg_off + 32 * i, msg + (base + i) * msg_stride, 32);
+      stage_fence();
     };
     if (nparts < 2) part(0);
     else PackPool::get().run(nparts, part);

@@ -398,13 +398,14 @@ int committee_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t
     rc = slot_prepare(s, total, total);
     if (rc != HSV_OK) return rc;
     uint8_t *h = s.h_buf;
-    std::memcpy(h + idx_off, key_idx + base, k * 4);
+    stage_copy(h + idx_off, key_idx + base, k * 4);
     if (sig_stride == 64) {
-      std::memcpy(h + sig_off, sig + base * 64, k * 64);
+      stage_copy(h + sig_off, sig + base * 64, k * 64);
     } else {  // signatures inside packed votes: gathered straight into the staging
-      for (size_t i = 0; i < k; ++i) std::memcpy(h + sig_off + i * 64, sig + (base + i) * sig_stride, 64);
+      for (size_t i = 0; i < k; ++i) stage_copy(h + sig_off + i * 64, sig + (base + i) * sig_stride, 64);
     }
-    std::memcpy(h + msg_off, msg + base * msg_stride, msg_bytes);
+    stage_copy(h + msg_off, msg + base * msg_stride, msg_bytes);
+    stage_fence();
     // The zero-copy latency form (<= kZeroCopyMax votes) reads the inputs from
     // the pinned staging through its device mapping (copying them to HBM first
     // made C1 0.0444 -> 0.0498 ms and C3 0.0592 -> 0.0689 ms,

@@ -15,6 +15,7 @@
 #include <atomic>
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -22,6 +23,10 @@
 
 #include "hsv.h"
 #include "hsv_internal.h"
+
+#if defined(__SSE2__)
+#include <emmintrin.h>
+#endif
 
 namespace hsvh {
 
@@ -50,6 +55,31 @@ constexpr size_t kChunk = size_t(1) << 22;        // items per verification laun
 constexpr size_t kShardMin = size_t(1) << 16;     // shard host batches across devices at or above this
 constexpr size_t kZeroCopyMax = size_t(1) << 12;  // small batches read straight from pinned memory
 inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Inputs a kernel reads straight from pinned memory (the zero-copy latency
+// form) are written with streaming stores, so they sit in DRAM and not in the
+// writing core's cache: the GPU's reads then need no snoop of a remote core's
+// cache, whose cost grows with the distance from that core to the PCIe root
+// (after a host load had moved the calling thread, the C3 QC read 0.0634
+// against 0.0543 ms, profiles/r05q_idle.txt).  dst 16-byte aligned; the tail
+// of n that is not a multiple of 16 is a plain copy.  stage_fence() orders the
+// streaming stores before the launch that reads them.
+inline void stage_copy(uint8_t *dst, const void *src, size_t n) {
+  const uint8_t *s = static_cast<const uint8_t *>(src);
+#if defined(__SSE2__)
+  size_t i = 0;
+  for (; i + 16 <= n; i += 16)
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i), _mm_loadu_si128(reinterpret_cast<const __m128i *>(s + i)));
+  if (i < n) std::memcpy(dst + i, s + i, n - i);
+#else
+  std::memcpy(dst, s, n);
+#endif
+}
+inline void stage_fence() {
+#if defined(__SSE2__)
+  _mm_sfence();
+#endif
+}
 
 // ---- device contexts ---------------------------------------------------------
 struct Slot {
