@@ -820,10 +820,11 @@ hsv_verify_row_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const 
 // one point per WAVE whose four rows compute the four independent products of
 // every formula round at once (hsv_rowpoint.hpp q_*), so a doubling costs two
 // row products instead of eight.  Each of the two waves decompresses its point
-// (the two-row chain, run by both row pairs), builds [0..8](-P) in LDS, runs
-// its one-scalar Straus (c1 for R, |c0| for A) and half of the wide B comb;
-// wave 2 runs the scalar prepass meanwhile.  The A wave hands its sum over in
-// LDS and the R wave adds it and checks.  Fallback items (no short lattice
+// (the two-row chain, run by both row pairs), builds [0..8](-P) in LDS and
+// runs its one-scalar Straus (c1 for R, |c0| for A); wave 2 runs the scalar
+// prepass meanwhile, then the whole wide B comb over b while the Straus loops
+// run.  The A wave and wave 2 hand their sums over in LDS and the R wave adds
+// them and checks.  Fallback items (no short lattice
 // pair) run the full-length one-lane path on lane 0 of the R wave.  Same
 // flags, self-checks and canaries as the row form.  Kernel 95.6 us at one
 // item: decompression 30.7, table 4.0 (the prepass ends at 35.4), Straus 52,
@@ -836,15 +837,21 @@ hsv_verify_row_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const 
 #define HSV_QUAD_MAX 256
 #endif
 constexpr uint32_t kQuadMax = HSV_QUAD_MAX;
+// windows of each half-size scalar run by the helper waves (the low 80 bits):
+// the point waves keep their 128 doublings but add only the high windows
+constexpr int kQuadLo = 20;
 #ifdef HSV_QUAD_CLOCKS
 // Measurement builds only (tools/build_ab_libs.sh quadclk "-DHSV_QUAD_CLOCKS"):
 // lane 0 of each wave of block 0 stamps the 100 MHz clock at fixed points
 // (0 entry, 1 decompressed / prepass done, 2 table built, 3 past barrier 1,
-// 4 Straus done, 5 comb half done, 6 past barrier 2, 7 exit).
-__device__ uint64_t g_quad_clk[3][8];
+// 4 Straus done, 5 wave 2's B comb done, 6 past barrier 2, 7 exit).
+__device__ uint64_t g_quad_clk[4][9];  // slot 8: the wave's HW_ID (SIMD_ID in bits 5:4)
 #define HSV_QUAD_CLK(w, slot)                                                  \
   do {                                                                         \
-    if (blockIdx.x == 0u && (threadIdx.x & 63u) == 0u) g_quad_clk[w][slot] = wall_clock64(); \
+    if (blockIdx.x == 0u && (threadIdx.x & 63u) == 0u) {                       \
+      g_quad_clk[w][slot] = wall_clock64();                                    \
+      if (slot == 0) g_quad_clk[w][8] = __builtin_amdgcn_s_getreg((31 << 11) | 4); \
+    }                                                                          \
   } while (0)
 #else
 #define HSV_QUAD_CLK(w, slot) \
@@ -852,7 +859,7 @@ __device__ uint64_t g_quad_clk[3][8];
   } while (0)
 #endif
 template <int WA, int CB>
-__global__ void __launch_bounds__(3 * 64)
+__global__ void __launch_bounds__(4 * 64)
 hsv_verify_quad_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const uint8_t *__restrict__ sig,
                        uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
                        uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
@@ -863,23 +870,47 @@ hsv_verify_quad_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const
   constexpr int kEnt = TS + 1;
   __shared__ uint32_t srec[kPrepWords];
   __shared__ uint32_t stab[2][kEnt * 64];
-  __shared__ uint32_t sq_a[4 * 16];   // the A wave's sum, cached form (component r on row r)
-  __shared__ uint32_t s_a[2];         // the A wave's ok, small
+  __shared__ uint32_t sq_a[4 * 16];     // the A wave's sum, cached form (component r on row r)
+  __shared__ uint32_t sq_h[2][4 * 16];  // the helpers' sums: [c1_lo](-R) + [b]B, [c0_lo](-A)
+  __shared__ uint32_t s_a[2];           // the A wave's ok, small
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint32_t item = blockIdx.x;
   const uint32_t li = item < n ? item : n - 1u;
   HSV_QUAD_CLK(wave, 0);
-  if (wave == 2) {
-    if (lane == 0u) {
+  if (wave >= 2) {
+    // helpers: wave 2 runs the scalar prepass on lane 0; after the tables
+    // are built, each helper adds the low kQuadLo windows of one scalar over
+    // its table (wave 2: c1 over -R, then the whole wide B comb over b; wave
+    // 3: |c0| over -A) while the point waves run the high windows
+    if (wave == 2u && lane == 0u) {
       uint32_t pkw[8], sigw[16], msgw[8];
       load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, li, pkw, sigw, msgw);
       (void)prep_scalars<WA>(pkw, sigw, msgw, srec, 1, lat_bits);
     }
-    HSV_QUAD_CLK(2, 1);
+    HSV_QUAD_CLK(wave, 1);
     __syncthreads();
-    HSV_QUAD_CLK(2, 3);
+    HSV_QUAD_CLK(wave, 3);
+    const uint32_t meta = srec[kPrepWords - 1];
+    if (!(meta & kPrepFallback)) {
+      const QuadLane L;
+      const uint32_t h = wave - 2u;  // 0: R, 1: A
+      uint32_t d[5];
+      HSV_UNROLL
+      for (int i = 0; i < 5; ++i) d[i] = srec[i + 5 * (int)h];
+      qp_ext q = quad_straus_low<WA, G::NW, kQuadLo>(d, stab[h], (h && (meta & kPrepC0Neg)) ? 1u : 0u, L);
+      HSV_QUAD_CLK(wave, 4);
+      if (h == 0u) {
+        uint32_t b[8];
+        HSV_UNROLL
+        for (int i = 0; i < 8; ++i) b[i] = srec[10 + i];
+        HSV_NOUNROLL
+        for (uint32_t half = 0; half < 2u; ++half) q = quad_comb_half<CB>(q, b, comb_b, half, L);
+      }
+      sq_h[h][L.r * 16u + L.k] = q_cached_component(q, fl_from_fe(fe_d2(), L), L);
+    }
+    HSV_QUAD_CLK(wave, 5);
     __syncthreads();
-    HSV_QUAD_CLK(2, 6);
+    HSV_QUAD_CLK(wave, 6);
     return;
   }
   const uint32_t role = wave;  // 0: R, 1: A
@@ -912,13 +943,8 @@ hsv_verify_quad_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const
     uint32_t d[5];
     HSV_UNROLL
     for (int i = 0; i < 5; ++i) d[i] = srec[i + 5 * (int)role];
-    q = quad_straus<WA, G::NW>(d, tab, (role && (meta & kPrepC0Neg)) ? 1u : 0u, L);
+    q = quad_straus<WA, G::NW, kQuadLo>(d, tab, (role && (meta & kPrepC0Neg)) ? 1u : 0u, L);
     HSV_QUAD_CLK(role, 4);
-    uint32_t b[8];
-    HSV_UNROLL
-    for (int i = 0; i < 8; ++i) b[i] = srec[10 + i];
-    q = quad_comb_half<CB>(q, b, comb_b, role, L);
-    HSV_QUAD_CLK(role, 5);
     if (role == 1u) {
       sq_a[L.r * 16u + L.k] = q_cached_component(q, fl_from_fe(fe_d2(), L), L);
       if (lane == 0u) {
@@ -942,10 +968,10 @@ hsv_verify_quad_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const
       bad = (f & kFault) ? 1u : 0u;
     }
   } else {
-    // Q = the R wave's sum + the A wave's (its cached form from LDS)
-    const uint32_t c = sq_a[(L.r ^ (L.r < 2u ? 1u : 0u)) * 16u + L.k];  // row 0: YmX, row 1: YpX
-    const uint32_t op = L.r == 2u ? sq_a[3u * 16u + L.k] : L.r == 3u ? sq_a[2u * 16u + L.k] : c;
-    q = q_add_op(q, op, L);
+    // Q = the R wave's sum + the A wave's + the helpers' (cached forms from LDS)
+    q = q_add_op(q, q_op_of_cached(sq_a, L), L);
+    q = q_add_op(q, q_op_of_cached(sq_h[0], L), L);
+    q = q_add_op(q, q_op_of_cached(sq_h[1], L), L);
     const uint32_t a_ok = s_a[0], small_a = s_a[1];
     const RowLane &R = L;
     ge_ext qe;
@@ -973,8 +999,9 @@ hsv_verify_quad_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const
 // wave decompresses R on rows 0-1 and A on rows 2-3 at once (the two-row
 // chain, each pair its own element), builds both tables [0..8](-R),
 // [0..8](-A) in LDS with the quad formulas, then runs one two-scalar Straus
-// (shared doublings, quad_straus2) and the whole wide B comb.  Same flags,
-// fallback, self-checks and canaries as the quad form.
+// (shared doublings, quad_straus2); the prepass wave runs each item's wide B
+// comb meanwhile and hands it over in LDS.  Same flags, fallback, self-checks
+// and canaries as the quad form.
 constexpr uint32_t kJointItems = 3;
 #ifndef HSV_JOINT_MAX  // measurement builds may move the cut-over (tools/row_cutover_probe.py)
 #define HSV_JOINT_MAX 768
@@ -993,14 +1020,31 @@ hsv_verify_joint_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, cons
   constexpr uint32_t K = kJointItems;
   __shared__ uint32_t srec[kPrepWords * K];
   __shared__ uint32_t stab[K][2][kEnt * 64];
+  __shared__ uint32_t sq_b[K][4 * 16];  // [b]B of each item, cached form (component r on row r)
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint32_t base = blockIdx.x * K;
   if (wave == K) {
+    // the items' scalar prepasses on lanes 0..K-1, then each item's whole
+    // wide B comb (16 additions) while the point waves run their Straus loops
     if (lane < K) {
       const uint32_t li = base + lane < n ? base + lane : n - 1u;
       uint32_t pkw[8], sigw[16], msgw[8];
       load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, li, pkw, sigw, msgw);
       (void)prep_scalars<WA>(pkw, sigw, msgw, srec + lane, K, lat_bits);
+    }
+    __syncthreads();
+    const QuadLane L;
+    const uint32_t d2 = fl_from_fe(fe_d2(), L);
+    HSV_NOUNROLL
+    for (uint32_t t = 0; t < K; ++t) {
+      if (srec[(kPrepWords - 1) * K + t] & kPrepFallback) continue;
+      uint32_t b[8];
+      HSV_UNROLL
+      for (int i = 0; i < 8; ++i) b[i] = srec[(10 + i) * K + t];
+      qp_ext qb{0u, fl_small(1, L), fl_small(1, L), 0u};
+      HSV_NOUNROLL
+      for (uint32_t h = 0; h < 2u; ++h) qb = quad_comb_half<CB>(qb, b, comb_b, h, L);
+      sq_b[t][L.r * 16u + L.k] = q_cached_component(qb, d2, L);
     }
     __syncthreads();
     return;
@@ -1044,6 +1088,17 @@ hsv_verify_joint_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, cons
   const uint32_t r_ok = __builtin_amdgcn_readlane(ok, 0), small_r = __builtin_amdgcn_readlane(small, 0);
   const uint32_t a_ok = __builtin_amdgcn_readlane(ok, 32), small_a = __builtin_amdgcn_readlane(small, 32);
   uint32_t f = 0, bad = 0;
+  qp_ext q{};
+  if (!(meta & kPrepFallback)) {
+    uint32_t d1[5], d0[5];
+    HSV_UNROLL
+    for (int i = 0; i < 5; ++i) {
+      d1[i] = srec[i * K + wave];
+      d0[i] = srec[(5 + i) * K + wave];
+    }
+    q = quad_straus2<WA, G::NW>(d1, d0, tab_r, tab_a, (meta & kPrepC0Neg) ? 1u : 0u, L);
+  }
+  __syncthreads();  // the prepass wave's [b]B
   if (meta & kPrepFallback) {
     if (lane == 0u) {
       GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)slot * vt_lane_uint4<WA>(), inject};
@@ -1053,17 +1108,7 @@ hsv_verify_joint_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, cons
       bad = (f & kFault) ? 1u : 0u;
     }
   } else {
-    uint32_t d1[5], d0[5], b[8];
-    HSV_UNROLL
-    for (int i = 0; i < 5; ++i) {
-      d1[i] = srec[i * K + wave];
-      d0[i] = srec[(5 + i) * K + wave];
-    }
-    HSV_UNROLL
-    for (int i = 0; i < 8; ++i) b[i] = srec[(10 + i) * K + wave];
-    qp_ext q = quad_straus2<WA, G::NW>(d1, d0, tab_r, tab_a, (meta & kPrepC0Neg) ? 1u : 0u, L);
-    HSV_NOUNROLL
-    for (uint32_t h = 0; h < 2u; ++h) q = quad_comb_half<CB>(q, b, comb_b, h, L);
+    q = q_add_op(q, q_op_of_cached(sq_b[wave], L), L);
     const RowLane &R = L;
     ge_ext qe;
     qe.X = fl_to_fe(q.X, R, nc);
@@ -1570,7 +1615,7 @@ hipError_t launch_quad(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig
   if (e != hipSuccess) return e;
   if (strict_bits) e = hipMemsetAsync(strict_bits, 0, (size_t)((n + 31u) / 32u) * 4u, stream);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL((hsv::hsv_verify_quad_kernel<WA, CB>), dim3(grid), dim3(3 * 64), 0, stream, pk, pk_stride,
+    hipLaunchKernelGGL((hsv::hsv_verify_quad_kernel<WA, CB>), dim3(grid), dim3(4 * 64), 0, stream, pk, pk_stride,
                        sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, static_cast<uint4 *>(ws), comb_b,
                        g_lat_bits.load(), reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(ws) + ws_bytes),
                        next_nonce(), t_inject, fault);

@@ -282,6 +282,13 @@ __device__ __forceinline__ uint32_t q_cached_component(const qp_ext &p, uint32_t
   return qsel(p.Y + p.X, fl_sub(p.Y, p.X, L), p.Z + p.Z, t2d);
 }
 
+// this row's operand for adding a point handed over in cached form (c[r * 16
+// + k] = component r, q_cached_component's layout): row 0 YmX, row 1 YpX, row
+// 2 T2d, row 3 Z2
+__device__ __forceinline__ uint32_t q_op_of_cached(const uint32_t *c, const QuadLane &L) {
+  return c[(L.r ^ 1u) * 16u + L.k];  // components 0 <-> 1, 2 <-> 3
+}
+
 // this row's operand for adding a cached entry (components c = 0 YpX, 1 YmX,
 // 2 Z2, 3 T2d of cmp_of(c)), negated when neg (swap YpX / YmX, -2dT)
 __device__ __forceinline__ uint32_t q_cached_col(uint32_t r, uint32_t neg) {
@@ -317,7 +324,10 @@ __device__ __forceinline__ void quad_table_build(uint32_t *tab, const fe &x, con
 }
 
 // One-scalar Straus over the wave's table (row_straus).  T is valid on return.
-template <int WA, int NW>
+// LO > 0: windows LO-1..0 are only doubled through, their digits left to a
+// helper wave (quad_straus_low): the sum is [c - c_lo](-P), c_lo the signed
+// value of the low LO windows, so a helper's [c_lo](-P) completes it.
+template <int WA, int NW, int LO = 0>
 __device__ __forceinline__ qp_ext quad_straus(uint32_t d[5], const uint32_t *tab, uint32_t flip, const QuadLane &L) {
   constexpr int TS = 1 << (WA - 1);
   qp_ext q{0u, fl_small(1, L), fl_small(1, L), 0u};
@@ -334,15 +344,29 @@ __device__ __forceinline__ qp_ext quad_straus(uint32_t d[5], const uint32_t *tab
     const uint32_t m = digit_mag<TS>(d[4] >> (32 - WA), neg);
     limbs_shl<5>(d, WA);
     neg ^= flip;
-    uint32_t op = tab[(m * 4u + q_cached_col(L.r, neg)) * 16u + L.k];
-    if (neg && L.r == 2u) op = fl_sub(0u, op, L);
+    uint32_t op = 0u;
+    if (i >= LO) {
+      op = tab[(m * 4u + q_cached_col(L.r, neg)) * 16u + L.k];
+      if (neg && L.r == 2u) op = fl_sub(0u, op, L);
+    }
     if (i != top) {
       HSV_NOUNROLL
       for (int j = 0; j < WA; ++j) q = q_dbl(q, L);
     }
-    q = q_add_op(q, op, L);
+    if (i >= LO) q = q_add_op(q, op, L);
   }
   return q;
+}
+
+// The helper's part of a split Straus: [c_lo](-P) over the low LO windows of
+// the same digits (the main wave runs quad_straus<WA, NW, LO>).
+template <int WA, int NW, int LO>
+__device__ __forceinline__ qp_ext quad_straus_low(uint32_t d[5], const uint32_t *tab, uint32_t flip,
+                                                  const QuadLane &L) {
+  static_assert(LO > 0 && LO < NW, "split window");
+  HSV_UNROLL
+  for (int i = 0; i < NW - LO; ++i) limbs_shl<5>(d, WA);
+  return quad_straus<WA, LO, 0>(d, tab, flip, L);
 }
 
 // The two-scalar Straus of one wave holding both tables (the joint form):
