@@ -816,23 +816,23 @@ hsv_verify_row_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const 
 }
 
 // Quad form of the latency kernel (default at <= kQuadMax items, round 5):
-// one item per block of three waves.  Wave 0 holds R, wave 1 holds A, each as
-// one point per WAVE whose four rows compute the four independent products of
-// every formula round at once (hsv_rowpoint.hpp q_*), so a doubling costs two
-// row products instead of eight.  Each of the two waves decompresses its point
-// (the two-row chain, run by both row pairs), builds [0..8](-P) in LDS and
-// runs its one-scalar Straus (c1 for R, |c0| for A); wave 2 runs the scalar
-// prepass meanwhile, then the whole wide B comb over b while the Straus loops
-// run.  The A wave and wave 2 hand their sums over in LDS and the R wave adds
-// them and checks.  Fallback items (no short lattice
-// pair) run the full-length one-lane path on lane 0 of the R wave.  Same
-// flags, self-checks and canaries as the row form.  Kernel 95.6 us at one
-// item: decompression 30.7, table 4.0 (the prepass ends at 35.4), Straus 52,
-// comb half 4, checks 3 (profiles/r05j_quad_clocks.txt).  The cut-over: one
-// block per CU runs 0.117 ms at 256 items; from 257 on some SIMDs hold two of
-// these lone-issue waves and the call takes 0.169-0.173 ms
-// (profiles/r05k_cutover.txt), so larger batches take the joint form below
-// (0.130-0.134 ms up to 768 items, profiles/r05l_cutover.txt).
+// one item per block of four waves, one per SIMD.  Waves 0 and 1 hold R and
+// A, each as one point per WAVE whose four rows compute the four independent
+// products of every formula round at once (hsv_rowpoint.hpp q_*), so a
+// doubling costs two row products instead of eight.  Each decompresses its
+// point (the two-row chain, run by both row pairs) and builds [0..8](-P) in
+// LDS while wave 2 runs the scalar prepass; then each runs its one-scalar
+// Straus (c1 for R, |c0| for A) adding only the windows above the low
+// kQuadLo.  The helper waves add those low windows over the same tables
+// (wave 2 for c1, then the whole wide B comb; wave 3 for |c0|), and the R
+// wave adds the three handed-over sums and checks.  Fallback items (no short
+// lattice pair) run the full-length one-lane path on lane 0 of the R wave.
+// Same flags, self-checks and canaries as the row form.  Kernel 84.4 us at one
+// item (95.6 us without the helpers, profiles/r05y_kernel_trace/); phases in
+// profiles/r05y_quadclk.txt.  The cut-over: one block per CU at <= 256 items;
+// from 257 on some SIMDs would hold two of these lone-issue waves (0.169-0.173
+// ms, profiles/r05k_cutover.txt), so larger batches take the joint form below
+// (0.129-0.132 ms up to 768 items, profiles/r05x_cutover.txt).
 #ifndef HSV_QUAD_MAX  // measurement builds may move the cut-over (tools/row_cutover_probe.py)
 #define HSV_QUAD_MAX 256
 #endif
