@@ -116,6 +116,10 @@ def test_lattice_fallback_records_every_variant(api, fallback_records, bits):
                 idx = np.arange(256) % len(fb["flags"])
                 got = verifier.verify_flags(fb["pk"][idx], fb["sig"][idx], fb["msg"][idx])
                 assert (got == fb["flags"][idx]).all(), v
+                # the joint quad form's range (257 .. 768 items)
+                idx = np.arange(600) % len(fb["flags"])
+                got = verifier.verify_flags(fb["pk"][idx], fb["sig"][idx], fb["msg"][idx])
+                assert (got == fb["flags"][idx]).all(), v
                 # the pair form's range (3073 .. 2^13 items)
                 idx = np.arange(4096) % len(fb["flags"])
                 got = verifier.verify_flags(fb["pk"][idx], fb["sig"][idx], fb["msg"][idx])
@@ -132,12 +136,12 @@ def test_lattice_fallback_records_every_variant(api, fallback_records, bits):
 
 def test_lattice_fallback_records_product_library(api, fallback_records, hsv):
     """The same records on the product library itself (default bound, default
-    variant), in the row, pair and point-pass ranges."""
+    variant), in the quad, joint, row, pair and point-pass ranges."""
     _, verifier, _ = api
     fb = fallback_records
     hsv.hsv_set_auto_committee(0)
     try:
-        for m in (len(fb["flags"]), 4096, (1 << 13) + 64):
+        for m in (len(fb["flags"]), 256, 600, 1000, 4096, (1 << 13) + 64):
             idx = np.arange(m) % len(fb["flags"])
             got = verifier.verify_flags(fb["pk"][idx], fb["sig"][idx], fb["msg"][idx])
             assert (got == fb["flags"][idx]).all(), m
