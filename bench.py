@@ -629,7 +629,8 @@ def mempool_bench(dev, n=1 << 20, tx_size=512, cpu_sample=1 << 17, nstreams=2, s
     buf = np.ascontiguousarray(w.txs[:m])
     out = np.zeros(m, np.uint8)
     t0 = time.perf_counter()
-    lib.oracle_verify_tx_many(buf.ctypes.data, None, tx_size, m, out.ctypes.data, threads)
+    with all_host_cpus():
+        lib.oracle_verify_tx_many(buf.ctypes.data, None, tx_size, m, out.ctypes.data, threads)
     dt = time.perf_counter() - t0
     res["cpu_baseline"] = {"value": m / dt, "unit": "tx/s", "cores": threads, "kind": "port",
                            "sample": f"first {m} transactions", "sample_parity_vs_gpu": bool((out == f[:m]).all())}
@@ -714,7 +715,7 @@ def compact(out):
     c["ms_per_step"] = _r(out["ms_per_step"], 5)
     cfg = out["config"]
     c["config"] = {k: cfg[k] for k in ("workload", "batch_per_gpu", "global_batch", "parallelism", "kernel_variant",
-                                       "streams")}
+                                       "streams", "host_affinity") if k in cfg}
     rf = out["roofline"]
     c["roofline"] = {"bound": rf["bound"], "achieved": _r(rf["achieved"]), "peak": _r(rf["peak"]), "unit": rf["unit"],
                      "frac": _r(rf["frac"]), "traffic": _r(rf["traffic"]),
@@ -920,6 +921,7 @@ def main():
         dist.init_process_group("gloo")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    affinity = pin_to_gpu_node(local_rank)
     _lib.load()
     if a.variant is not None:
         # a measurement run of another variant: every call goes to the test
@@ -1044,6 +1046,7 @@ def main():
             "batch_per_gpu": a.n,
             "global_batch": a.n * world,
             "parallelism": f"dp{world} (contiguous shards, no collective on the data path)",
+            "host_affinity": affinity,
             "kernel_variant": verifier.get_variant(),
             "streams": nst,
         },
@@ -1080,7 +1083,8 @@ def main():
         if early_host_api is not None:
             out["host_api_early"] = early_host_api
     if world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(w, f, a.cpu_sample)
+        with all_host_cpus():
+            out["cpu_baseline"] = cpu_baseline(w, f, a.cpu_sample)
     if not a.no_qc:
         out["qc_latency"] = qc_latency(a.qc_reps, auto=True)
         out["qc_latency_generic"] = qc_latency(a.qc_reps, auto=False)
@@ -1096,7 +1100,8 @@ def main():
         # per 2^20, profiles/r04z_mempool_streams2.txt)
         out["mempool_tx"] = mempool_bench(dev, nstreams=2, streams=streams[:2] if nst >= 2 else None)
         if world == 1 and not a.no_cpu_baseline:
-            out["qc_cpu_baseline"] = qc_cpu()
+            with all_host_cpus():
+                out["qc_cpu_baseline"] = qc_cpu()
     if a.detail:
         try:
             os.makedirs(os.path.dirname(os.path.abspath(a.detail)), exist_ok=True)
@@ -1109,6 +1114,63 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _cpulist(text):
+    cpus = set()
+    for part in text.strip().split(","):
+        if "-" in part:
+            lo, hi = part.split("-")
+            cpus.update(range(int(lo), int(hi) + 1))
+        elif part:
+            cpus.add(int(part))
+    return cpus
+
+
+_ALL_HOST_CPUS = None  # the process's CPU set before pin_to_gpu_node
+
+
+class all_host_cpus:
+    """The CPU baselines run on every CPU the process had before the GPU
+    pinning (its worker threads, created inside the call, inherit the set)."""
+
+    def __enter__(self):
+        self.cur = os.sched_getaffinity(0)
+        if _ALL_HOST_CPUS:
+            os.sched_setaffinity(0, _ALL_HOST_CPUS)
+        return self
+
+    def __exit__(self, *exc):
+        os.sched_setaffinity(0, self.cur)
+        return False
+
+
+def pin_to_gpu_node(device):
+    """Bind this rank's threads to the CPUs of its GPU's NUMA node, the usual
+    placement of one process per GPU.  The latency legs depend on it: a C3 QC
+    called from the other socket of the box took 0.064 against 0.055 ms, C1
+    +1 us, whichever node the library had allocated on
+    (tools/qc_numa_probe.py, profiles/r05ac_numa.txt).  Threads the process
+    starts later (the library's pack pool, the CPU baseline's workers) inherit
+    the set.  Returns what was done, or None when the topology is not visible."""
+    import torch
+    try:
+        p = torch.cuda.get_device_properties(device)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as fh:
+            node = int(fh.read())
+        if node < 0:
+            return None
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as fh:
+            cpus = _cpulist(fh.read()) & os.sched_getaffinity(0)
+        if len(cpus) < host_cores()[0]:
+            return None
+        global _ALL_HOST_CPUS
+        _ALL_HOST_CPUS = os.sched_getaffinity(0)
+        os.sched_setaffinity(0, cpus)
+        return {"numa_node": node, "cpus": len(cpus), "gpu_pci": bdf}
+    except (OSError, ValueError, AttributeError, RuntimeError):
+        return None
 
 
 def _free_port():

@@ -33,7 +33,11 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=1000)
+    ap.add_argument("--cpus", default=None, help="pin the process to these CPUs first (e.g. 64-71)")
     a = ap.parse_args()
+    if a.cpus:
+        lo, _, hi = a.cpus.partition("-")
+        os.sched_setaffinity(0, set(range(int(lo), int(hi or lo) + 1)))
     from hsverify import _lib, synth, wire
     lib = _lib.load()
     st = lib.hsv_qc_call_stamps
