@@ -80,7 +80,7 @@ hsv_comb_verify_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__re
 }
 
 // Latency form of hsv_comb_verify_kernel for small batches (a QC is 67 or
-// 667 votes): L lanes per vote (HSV_COMB_LANES, default 16).  Lane g of a
+// 667 votes): L = 16 lanes per vote, one DPP row.  Lane g of a
 // vote's group adds the comb entries of positions [g P, (g+1) P), P = 32 / L,
 // for both k (the key's table) and s (the B table): 2P mixed additions on the
 // critical lane instead of 64; the group's partial sums meet through log2(L)
@@ -93,23 +93,18 @@ hsv_comb_verify_kernel(const uint32_t *__restrict__ key_idx, const uint8_t *__re
 // the longer piece at 4 lanes per vote, and a block of 4 lanes per vote needs
 // 5 waves, which then share SIMDs: C1 / C3 p50 0.099 / 0.105 ms at 4 lanes,
 // 0.057 / 0.062 at 8 (3 waves), 0.055 / 0.062 at 16 (2 waves), against
-// 0.082 / 0.088 ms for round 2's form (profiles/r03z_qc_ab.txt).
-#ifndef HSV_COMB_LANES
-#define HSV_COMB_LANES 16
-#endif
-constexpr int kCombLanes = HSV_COMB_LANES;
-static_assert(kCombLanes == 4 || kCombLanes == 8 || kCombLanes == 16 || kCombLanes == 32, "lanes per vote");
+// 0.082 / 0.088 ms for round 2's form (profiles/r03z_qc_ab.txt).  (The
+// lane-count switch and the other closed latency-form experiments of rounds
+// 3-4 -- one-lane R, one row per R, the hash on the comb wave or on every
+// lane, one-lane final checks, compact root-chain and SHA-512 bodies -- were
+// removed in round 5; they are in git history at 5c186e7.)
+constexpr int kCombLanes = 16;
 constexpr int kCombPosPerLane = kCombPos / kCombLanes;
 
-// Checks of a vote's final sum spread over its 16-lane row (L = 16): after
-// the swap rounds every lane of the vote's row holds Q, and the row is a DPP
-// row, so the self-check and the equation run as rounds of one field
-// operation per lane (ge_is_sane_row, ge_eq_affine_row in hsv_fe16x16.hpp).
-#ifdef HSV_COMB_SEQ_CHECKS  // measurement builds only: the one-lane checks of round 2
-constexpr bool kRowChecks = false;
-#else
-constexpr bool kRowChecks = kCombLanes >= 16;
-#endif
+// Checks of a vote's final sum spread over its 16-lane row: after the swap
+// rounds every lane of the vote's row holds Q, and the row is a DPP row, so
+// the self-check and the equation run as rounds of one field operation per
+// lane (ge_is_sane_row, ge_eq_affine_row in hsv_fe16x16.hpp).
 
 __device__ __forceinline__ ge_ext ge_swap_xor(const ge_ext &p, int m) {
   ge_ext r;
@@ -132,44 +127,23 @@ __device__ __forceinline__ ge_ext ge_swap_xor(const ge_ext &p, int m) {
 // waves hold one vote per 16-lane row with the products spread over the row
 // (ge_decompress_row, hsv_fe16x16.hpp: 32 us for the root chain on a lone
 // wave against 57 us on one lane, profiles/r03z_ubench_lanesplit.txt), four
-// votes per wave.  HSV_COMB_R_ONELANE (measurement builds only) keeps round
-// 2's single R wave with one vote per lane.  Each vote takes two rows
-// (RowLane2: a product's 16 steps split 8 + 8 between the rows, 25.4 against
-// 32.2 us for the root chain, profiles/r03zz_ubench_lanesplit2.txt), two
-// votes per wave; HSV_COMB_R_ROWS=1 (measurement builds) keeps one row.
-#ifndef HSV_COMB_R_ROWS
-#define HSV_COMB_R_ROWS 2
-#endif
-constexpr int kRRows = HSV_COMB_R_ROWS;
-static_assert(kRRows == 1 || kRRows == 2, "HSV_COMB_R_ROWS is 1 or 2");
-using RLane = std::conditional_t<kRRows == 2, RowLane2, RowLane>;
+// votes per wave.  Each vote takes two rows (RowLane2: a product's 16 steps
+// split 8 + 8 between the rows, 25.4 against 32.2 us for the root chain,
+// profiles/r03zz_ubench_lanesplit2.txt), two votes per wave.
+constexpr int kRRows = 2;
+using RLane = RowLane2;
 constexpr int kRVotesPerWave = 4 / kRRows;
 constexpr int kFusedVotes = 64 / kCombLanes;
-#ifdef HSV_COMB_R_ONELANE
-constexpr int kFusedRWaves = 1;
-#else
 constexpr int kFusedRWaves = (kFusedVotes + kRVotesPerWave - 1) / kRVotesPerWave;
-#endif
 // A hash wave (the last of the block) computes k = H(R || A || M) mod l and
 // its comb digits for the block's votes while the comb wave adds the s half
 // (the B table needs no hash), and hands the digits over in LDS: the comb
 // wave's path becomes max(hash, s additions) + k additions + swap rounds
-// instead of their sum.  HSV_COMB_HASH_WAVE=0 (measurement builds) keeps the
-// hash on the comb wave.
-#ifndef HSV_COMB_HASH_WAVE
-#define HSV_COMB_HASH_WAVE 1
-#endif
-constexpr bool kHashWave = HSV_COMB_HASH_WAVE != 0;
-// HSV_COMB_SHA_COMPACT=1 (measurement builds only): the hash wave runs
-// SHA-512 with one 16-round body (sha512_compress_compact), half the code
-// fetched cold at each launch.  Measured no faster: the hash took 10.2 against
-// 9.7 us at C1 and 13.5 against 13.2 us at C3 (profiles/r04t_qcclk_*.txt).
-#ifndef HSV_COMB_SHA_COMPACT
-#define HSV_COMB_SHA_COMPACT 0
-#endif
-constexpr bool kShaCompact = HSV_COMB_SHA_COMPACT != 0;
+// instead of their sum.  A one-body SHA-512 (half the code fetched cold at
+// each launch) measured no faster: 10.2 against 9.7 us at C1, 13.5 against
+// 13.2 us at C3 (profiles/r04t_qcclk_*.txt).
 constexpr uint32_t kHashWaveIdx = 1 + kFusedRWaves;
-constexpr int kFusedThreads = 64 * (1 + kFusedRWaves + (kHashWave ? 1 : 0));
+constexpr int kFusedThreads = 64 * (2 + kFusedRWaves);
 
 #ifdef HSV_QC_WAVE_CLOCKS
 // Measurement builds only (tools/qc_wave_clocks.py): lane 0 of every wave
@@ -272,12 +246,10 @@ __device__ __forceinline__ void comb_quad_block(const uint32_t *__restrict__ key
   // vote v of the block reads vote min(base + v, m - 1): the last block's
   // spare slots repeat the batch's last vote and write no flag
   auto vote_of = [&](uint32_t v) { return base + v < m ? base + v : m - 1u; };
-  if constexpr (kHashWave) {
-    // LDS keeps the last block's flag: cleared before any wave can look
-    if (threadIdx.x == 0) k_ready = 0u;
-    __syncthreads();
-    HSV_QC_CLK(1);
-  }
+  // LDS keeps the last block's flag: cleared before any wave can look
+  if (threadIdx.x == 0) k_ready = 0u;
+  __syncthreads();
+  HSV_QC_CLK(1);
   // (the resident service passes key_idx / sig / msg pointing into its LDS copy of the request)
   auto vote_sig = [&](uint32_t v) { return reinterpret_cast<const uint4 *>(sig + (uint64_t)vote_of(v) * sig_stride); };
   auto vote_msg = [&](uint32_t v) { return reinterpret_cast<const uint4 *>(msg + (uint64_t)vote_of(v) * msg_stride); };
@@ -288,42 +260,30 @@ __device__ __forceinline__ void comb_quad_block(const uint32_t *__restrict__ key
   auto vote_pk = [&](uint32_t v, uint32_t kk) {
     return reinterpret_cast<const uint4 *>(vote_pks ? vote_pks + 32ull * vote_of(v) : pks + (uint64_t)kk * 32);
   };
-  if constexpr (kHashWave) {
-    if (wave == kHashWaveIdx) {
-      // one lane per vote hashes (lanes 0..kFusedVotes-1); the rest of the
-      // wave stays masked off (HSV_COMB_HASH_ALL_LANES: every lane, as the
-      // comb wave's lanes did)
-#ifdef HSV_COMB_HASH_ALL_LANES
-      const bool hashes = true;
-      const uint32_t vl = lane / kCombLanes, g = lane % kCombLanes;
-#else
-      const bool hashes = lane < (uint32_t)kFusedVotes;
-      const uint32_t vl = lane, g = 0u;
-#endif
-      if (hashes) {
-        const uint32_t kidx = vote_kidx(vl);
-        const uint32_t kk = kidx < nkeys ? kidx : 0u;
-        uint32_t pkw[8], sigw[16], msgw[8], h[16], kr[9];
-        load_vote_words(vote_pk(vl, kk), vote_sig(vl), vote_msg(vl), pkw, sigw, msgw);
-        HSV_QC_CLK_LOADED(3);
-        sha512_96<kShaCompact>(sigw, pkw, msgw, h);
-        const sc k = sc_reduce512(h);
-        recode_add<9, 8, kCombPos>(k.v, 8, kr);
-        if (g == 0u) {
-          HSV_UNROLL
-          for (int w = 0; w < 9; ++w) k_rec[vl][w] = kr[w];
-        }
-      }
-      HSV_QC_CLK(2);
-      __hip_atomic_store(&k_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      HSV_QC_CLK(4);
-      __syncthreads();
-      HSV_QC_CLK(5);
-      return;
+  if (wave == kHashWaveIdx) {
+    // one lane per vote hashes (lanes 0..kFusedVotes-1); the rest of the
+    // wave stays masked off
+    const uint32_t vl = lane;
+    if (vl < (uint32_t)kFusedVotes) {
+      const uint32_t kidx = vote_kidx(vl);
+      const uint32_t kk = kidx < nkeys ? kidx : 0u;
+      uint32_t pkw[8], sigw[16], msgw[8], h[16], kr[9];
+      load_vote_words(vote_pk(vl, kk), vote_sig(vl), vote_msg(vl), pkw, sigw, msgw);
+      HSV_QC_CLK_LOADED(3);
+      sha512_96(sigw, pkw, msgw, h);
+      const sc k = sc_reduce512(h);
+      recode_add<9, 8, kCombPos>(k.v, 8, kr);
+      HSV_UNROLL
+      for (int w = 0; w < 9; ++w) k_rec[vl][w] = kr[w];
     }
+    HSV_QC_CLK(2);
+    __hip_atomic_store(&k_ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    HSV_QC_CLK(4);
+    __syncthreads();
+    HSV_QC_CLK(5);
+    return;
   }
   if (wave >= 1) {
-#ifndef HSV_COMB_R_ONELANE
     const RLane L;
     const uint32_t row = lane >> 4;
     const uint32_t vr = (wave - 1u) * kRVotesPerWave + row / kRRows;  // this row's vote in the block
@@ -361,22 +321,6 @@ __device__ __forceinline__ void comb_quad_block(const uint32_t *__restrict__ key
         r_fl[vr] = r_ok | (small_r << 1) | (nc << 2);  // bit 2: self-check (fl_to_fe)
       }
     }
-#else
-    if (lane < (uint32_t)kFusedVotes) {
-      const uint4 *sp = vote_sig(lane);
-      const uint4 s0 = sp[0], s1 = sp[1];
-      const uint32_t rw[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-      fe rx, ry;
-      const uint32_t r_ok = ge_decompress(rw, rx, ry);
-      const uint32_t small_r = r_ok & y_is_small_order(ry);
-      HSV_UNROLL
-      for (int l = 0; l < kFeLimbs; ++l) {
-        r_x[lane][l] = rx.v[l];
-        r_y[lane][l] = ry.v[l];
-      }
-      r_fl[lane] = r_ok | (small_r << 1);
-    }
-#endif
     HSV_QC_CLK(2);
     HSV_QC_CLK(4);
     __syncthreads();
@@ -405,59 +349,40 @@ __device__ __forceinline__ void comb_quad_block(const uint32_t *__restrict__ key
   uint32_t sr[9];
   recode_add<9, 8, kCombPos>(sigw + 8, 8, sr);
   uint64_t sd = lane_digits(sr, g), kd;
-  if constexpr (kHashWave) {
-    // the s half first, while the hash wave works on k
-    HSV_NOUNROLL
-    for (int jj = 0; jj < kCombPosPerLane; ++jj) {
-      const uint32_t j = g * kCombPosPerLane + (uint32_t)jj;
-      const CombPosTab tpb{btable + (uint64_t)j * kCombEnt * kCombEntryWords};
-      q = ge_add_niels<true>(q, select_niels<8>(tpb, (uint32_t)sd & 0xffu));
-      sd >>= 8;
-    }
-    HSV_QC_CLK(2);
-    while (__hip_atomic_load(&k_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
-      __builtin_amdgcn_s_sleep(1);
-    HSV_QC_CLK(3);
+  // the s half first, while the hash wave works on k
+  HSV_NOUNROLL
+  for (int jj = 0; jj < kCombPosPerLane; ++jj) {
+    const uint32_t j = g * kCombPosPerLane + (uint32_t)jj;
+    const CombPosTab tpb{btable + (uint64_t)j * kCombEnt * kCombEntryWords};
+    q = ge_add_niels<true>(q, select_niels<8>(tpb, (uint32_t)sd & 0xffu));
+    sd >>= 8;
+  }
+  HSV_QC_CLK(2);
+  while (__hip_atomic_load(&k_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+    __builtin_amdgcn_s_sleep(1);
+  HSV_QC_CLK(3);
+  {
     uint32_t kr[9];
     HSV_UNROLL
     for (int w = 0; w < 9; ++w) kr[w] = k_rec[vl][w];
     kd = lane_digits(kr, g);
-    HSV_NOUNROLL
-    for (int jj = 0; jj < kCombPosPerLane; ++jj) {
-      const uint32_t j = g * kCombPosPerLane + (uint32_t)jj;
-      const CombPosTab tpa{ta + (uint64_t)j * kCombEnt * kCombEntryWords};
-      ge_niels na = select_niels<8>(tpa, (uint32_t)kd & 0xffu);
-      kd >>= 8;
-      if (inject != kInjectNone && jj == 0) na = niels_injected(na, inject);
-      q = ge_add_niels<true>(q, na);
-    }
-  } else {
-    uint32_t h[16], kr[9];
-    sha512_96(sigw, pkw, msgw, h);
-    const sc k = sc_reduce512(h);
-    recode_add<9, 8, kCombPos>(k.v, 8, kr);
-    kd = lane_digits(kr, g);
-    HSV_NOUNROLL
-    for (int jj = 0; jj < kCombPosPerLane; ++jj) {
-      const uint32_t j = g * kCombPosPerLane + (uint32_t)jj;
-      const uint32_t ca = (uint32_t)kd & 0xffu, cb = (uint32_t)sd & 0xffu;
-      kd >>= 8;
-      sd >>= 8;
-      const CombPosTab tpa{ta + (uint64_t)j * kCombEnt * kCombEntryWords};
-      const CombPosTab tpb{btable + (uint64_t)j * kCombEnt * kCombEntryWords};
-      ge_niels na = select_niels<8>(tpa, ca);
-      if (inject != kInjectNone && jj == 0) na = niels_injected(na, inject);
-      q = ge_add_niels<true>(q, na);
-      q = ge_add_niels<true>(q, select_niels<8>(tpb, cb));
-    }
+  }
+  HSV_NOUNROLL
+  for (int jj = 0; jj < kCombPosPerLane; ++jj) {
+    const uint32_t j = g * kCombPosPerLane + (uint32_t)jj;
+    const CombPosTab tpa{ta + (uint64_t)j * kCombEnt * kCombEntryWords};
+    ge_niels na = select_niels<8>(tpa, (uint32_t)kd & 0xffu);
+    kd >>= 8;
+    if (inject != kInjectNone && jj == 0) na = niels_injected(na, inject);
+    q = ge_add_niels<true>(q, na);
   }
   HSV_UNROLL
   for (int mask = 1; mask < kCombLanes; mask <<= 1)
     q = ge_add_cached_rt(q, ge_to_cached(ge_swap_xor(q, mask)), mask < kCombLanes / 2);
 #endif
   // the self-check of Q needs nothing from the R waves: before the barrier
-  uint32_t z_nonzero = 0, sane = 0;
-  if constexpr (kRowChecks) sane = ge_is_sane_row(q, z_nonzero);
+  uint32_t z_nonzero = 0;
+  const uint32_t sane = ge_is_sane_row(q, z_nonzero);
   HSV_QC_CLK(4);
   __syncthreads();
   fe rx, ry;
@@ -468,9 +393,7 @@ __device__ __forceinline__ void comb_quad_block(const uint32_t *__restrict__ key
   }
   const uint32_t rf = r_fl[vl];
   const uint32_t r_ok = rf & 1u, small_r = (rf >> 1) & 1u;
-  uint32_t same;
-  if constexpr (kRowChecks) same = ge_eq_affine_row(q, rx, ry, z_nonzero);
-  else same = ge_eq_affine(q, rx, ry);
+  const uint32_t same = ge_eq_affine_row(q, rx, ry, z_nonzero);
   const uint32_t a_ok = (kf & kKeyAOk) ? 1u : 0u;
   const uint32_t small_a = a_ok & ((kf & kKeySmallA) ? 1u : 0u);
   const uint32_t parse_ok = s_ok & a_ok & r_ok;
@@ -479,9 +402,7 @@ __device__ __forceinline__ void comb_quad_block(const uint32_t *__restrict__ key
   const uint32_t f = (strict_ok ? kStrictOk : 0u) | (eq_ok ? kEqOk : 0u) | (parse_ok ? kParseOk : 0u) |
                      (small_a ? kSmallA : 0u) | (small_r ? kSmallR : 0u) | (s_ok ? kSOk : 0u) |
                      (a_ok ? kAOk : 0u) | (r_ok ? kROk : 0u);
-  uint32_t fb;
-  if constexpr (kRowChecks) fb = a_ok & r_ok & (sane ^ 1u);
-  else fb = fault_bit(a_ok, r_ok, q) ? 1u : 0u;
+  const uint32_t fb = a_ok & r_ok & (sane ^ 1u);
   if (fb | ((rf >> 2) & 1u)) fault[0] = 1u;  // device self-check (hsv_kernels.hip report_faults)
   if (valid && g == 0u) flags_out[i0] = kvalid ? (uint8_t)f : (uint8_t)0;
   HSV_QC_CLK(5);

@@ -163,61 +163,14 @@ __device__ __forceinline__ uint32_t fl_sqn(uint32_t f, int n, const Lane &L) {
   return f;
 }
 
-// HSV_ROW_CHAIN_COMPACT=1 (measurement builds only): the same chain as a
-// program over three registers (z, t0, t1), step i setting dst_i =
-// src_i^(2^n_i) * mul_i, so the whole chain is one squaring body and one
-// product body in two rolled loops instead of 21 inlined products.  A lone
-// wave's first pass over straight-line code fetches every instruction cold,
-// and at C3 (167 CUs fetching the same lines) the unrolled chain's R waves run
-// ~4-5 us longer than at C1 (profiles/r04k_qcclk_twice.txt).  The compact
-// chain removes most of that (R at C3: 30.6 against 34.1 us,
-// profiles/r04t_qcclk_*.txt), yet the drop-in QC call measured 2.2-2.5 us
-// slower with it at every size (r04t_qc_ab_compact.txt), outside the waves'
-// stamped lifetimes; so it stays off.
-#ifndef HSV_ROW_CHAIN_COMPACT
-#define HSV_ROW_CHAIN_COMPACT 0
-#endif
-// Step i: n_i squarings of register src_i, then a product with register
-// mul_i (3 = none), into register dst_i (0 = z, 1 = t0, 2 = t1).  The program
-// lives in 64-bit immediates, read with uniform shifts: a table in memory
-// would cost a scalar-cache miss per step at every launch (the cache starts
-// cold at each dispatch), which made a first version 2.2 us slower per call.
-constexpr uint64_t fl_chain_pack(const uint32_t (&v)[12], int lo, int hi, int bits) {
-  uint64_t r = 0;
-  for (int i = hi - 1; i >= lo; --i) r = (r << bits) | v[i];
-  return r;
-}
-template <class Lane>
-__device__ __forceinline__ uint32_t fl_pow22523_compact(uint32_t z, const Lane &L) {
-  //                                t0=z^2 z^9 z^11 2^5-1 2^10-1 2^20-1 2^40-1 2^50-1 2^100-1 2^200-1 2^250-1 2^252-3
-  constexpr uint32_t kN[12]    = {1,     2,  0,   1,    5,     10,    20,    10,    50,     100,    50,     2};
-  constexpr uint32_t kCtl[12]  = {       // src | mul << 2 | dst << 4
-      0 | 3 << 2 | 1 << 4, 1 | 0 << 2 | 2 << 4, 1 | 2 << 2 | 1 << 4, 1 | 2 << 2 | 1 << 4,
-      1 | 1 << 2 | 1 << 4, 1 | 1 << 2 | 2 << 4, 2 | 2 << 2 | 2 << 4, 2 | 1 << 2 | 1 << 4,
-      1 | 1 << 2 | 2 << 4, 2 | 2 << 2 | 2 << 4, 2 | 1 << 2 | 1 << 4, 1 | 0 << 2 | 1 << 4};
-  constexpr uint64_t kN0 = fl_chain_pack(kN, 0, 8, 8), kN1 = fl_chain_pack(kN, 8, 12, 8);
-  constexpr uint64_t kC0 = fl_chain_pack(kCtl, 0, 10, 6), kC1 = fl_chain_pack(kCtl, 10, 12, 6);
-  uint32_t t0 = 0u, t1 = 0u;
-  HSV_NOUNROLL
-  for (uint32_t i = 0; i < 12u; ++i) {
-    const uint32_t n = (uint32_t)((i < 8u ? kN0 >> (8u * i) : kN1 >> (8u * (i - 8u))) & 0xffu);
-    const uint32_t ctl = (uint32_t)((i < 10u ? kC0 >> (6u * i) : kC1 >> (6u * (i - 10u))) & 0x3fu);
-    const uint32_t src = ctl & 3u, mul = (ctl >> 2) & 3u, dst = ctl >> 4;
-    uint32_t x = src == 0u ? z : src == 1u ? t0 : t1;
-    const uint32_t y = mul == 0u ? z : mul == 1u ? t0 : t1;  // read before dst is written
-    HSV_NOUNROLL
-    for (uint32_t k = 0; k < n; ++k) x = fl_sq(x, L);
-    if (mul != 3u) x = fl_mul(x, y, L);
-    if (dst == 1u) t0 = x;
-    else t1 = x;
-  }
-  return t0;
-}
+// (Round 4's compact form of this chain -- one squaring body and one product
+// body looped over a 12-step program -- shortened the R waves at C3 but made
+// the drop-in call 2.2-2.5 us slower, profiles/r04t_qc_ab_compact.txt; it was
+// removed in round 5 and is in git history at 5c186e7.)
 
 // z^((p-5)/8) = z^(2^252 - 3), the chain of fe_pow22523 (hsv_field.hpp)
 template <class Lane>
 __device__ __forceinline__ uint32_t fl_pow22523(uint32_t z, const Lane &L) {
-  if constexpr (HSV_ROW_CHAIN_COMPACT != 0) return fl_pow22523_compact(z, L);
   uint32_t t0 = fl_sq(z, L);                 // 2
   uint32_t t1 = fl_sq(fl_sq(t0, L), L);      // 8
   t1 = fl_mul(z, t1, L);                     // 9

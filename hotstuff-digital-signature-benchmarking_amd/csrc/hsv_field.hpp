@@ -37,11 +37,7 @@
 #define HSV_NOUNROLL _Pragma("nounroll")
 // Keep the scheduler from interleaving independent field multiplies: one
 // multiply alone has ample ILP, several interleaved multiply the live registers.
-#ifndef HSV_NO_SCHED_FENCE
 #define HSV_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
-#else
-#define HSV_SCHED_FENCE()
-#endif
 #else
 #define HSV_UNROLL _Pragma("GCC unroll 16")
 #define HSV_NOUNROLL

@@ -159,12 +159,6 @@ struct GlobalVarTab {
     for (int q = 0; q < 8; ++q) {
 #ifdef HSV_TIMING_STUB_TABLE_STORES  // timing probe only: entries computed, never stored
       asm volatile("" ::"v"(w[4 * q]), "v"(w[4 * q + 1]), "v"(w[4 * q + 2]), "v"(w[4 * q + 3]));
-#elif defined(HSV_VT_NT_STORES)  // A/B probe: streaming (nontemporal) table stores
-      {
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 v = {w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(e + q));
-      }
 #else
       e[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 #endif
@@ -427,13 +421,6 @@ hsv_verify_hp_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const u
   const uint32_t nfb = __builtin_amdgcn_readfirstlane(ctr->fb_count);
   const uint32_t fb_end = (nfb + 63u) & ~63u;
   const uint32_t words = (n + 31u) / 32u;
-#ifdef HSV_STAGGER_US  // timing probe only: wave slot s of a SIMD starts s * HSV_STAGGER_US us late
-  {
-    const uint32_t slot = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 4) % 3u;  // HW_ID.WAVE_ID
-    const uint64_t until = wall_clock64() + (uint64_t)slot * HSV_STAGGER_US * 100u;
-    while (wall_clock64() < until) __builtin_amdgcn_s_sleep(64);
-  }
-#endif
 #ifdef HSV_PHASE_CLOCKS
   uint32_t nbw = 0;  // batches this wave has taken
 #endif

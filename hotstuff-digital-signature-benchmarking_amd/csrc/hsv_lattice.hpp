@@ -564,9 +564,7 @@ HSV_INL LatOut lattice_reduce(const sc &k, int max_bits = kLatMaxBits) {
     ta[i] = 0;
     tb[i] = i == 0 ? 1u : 0u;
   }
-#if defined(HSV_LATTICE_EUCLID)
-  lat_euclid_to_128(a, b, ta, tb);
-#elif defined(HSV_LATTICE_LEHMER1)  // round-1 Lehmer form (A/B and the host cross-check)
+#if defined(HSV_LATTICE_LEHMER1)  // round-1 Lehmer form (the host cross-check)
   lat_lehmer_to_128(a, b, ta, tb);
 #else
   lat_lehmer_lean_to_128(a, b, ta, tb);

@@ -99,10 +99,7 @@ __global__ void __launch_bounds__(kTxBlock) hsv_tx_record_kernel(const uint8_t *
                                                                   uint32_t *__restrict__ fb_count,
                                                                   uint32_t *__restrict__ fb_list, int lat_bits) {
   __shared__ uint4 stage_all[kTxWaves][64 * kTxQ];
-#ifndef HSV_TX_PREP_PRIO
-#define HSV_TX_PREP_PRIO 3  // measurement builds: 0 leaves the record waves at normal priority
-#endif
-  if constexpr (PREP && HSV_TX_PREP_PRIO > 0) __builtin_amdgcn_s_setprio(HSV_TX_PREP_PRIO);  // as hsv_prep_kernel: ahead of a running point pass
+  if constexpr (PREP) __builtin_amdgcn_s_setprio(3);  // as hsv_prep_kernel: ahead of a running point pass
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   if (blockIdx.x * kTxBlock + wv * 64u >= n) return;  // whole wave past the end
   uint4 *stage = stage_all[wv];
