@@ -986,10 +986,15 @@ hsv_verify_quad_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const
 // wave decompresses R on rows 0-1 and A on rows 2-3 at once (the two-row
 // chain, each pair its own element), builds both tables [0..8](-R),
 // [0..8](-A) in LDS with the quad formulas, then runs one two-scalar Straus
-// (shared doublings, quad_straus2); the prepass wave runs each item's wide B
-// comb meanwhile and hands it over in LDS.  Same flags, fallback, self-checks
+// (shared doublings, quad_straus2) over all but the low kJointLo windows; the
+// prepass wave adds each item's low windows and its wide B comb meanwhile and
+// hands the sum over in LDS.  Same flags, fallback, self-checks
 // and canaries as the quad form.
 constexpr uint32_t kJointItems = 3;
+// windows of both scalars the prepass wave adds for each item after its
+// prepasses (the low 28 bits): it finishes its three items' shares about when
+// the point waves finish the rest
+constexpr int kJointLo = 7;
 #ifndef HSV_JOINT_MAX  // measurement builds may move the cut-over (tools/row_cutover_probe.py)
 #define HSV_JOINT_MAX 768
 #endif
@@ -1007,7 +1012,7 @@ hsv_verify_joint_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, cons
   constexpr uint32_t K = kJointItems;
   __shared__ uint32_t srec[kPrepWords * K];
   __shared__ uint32_t stab[K][2][kEnt * 64];
-  __shared__ uint32_t sq_b[K][4 * 16];  // [b]B of each item, cached form (component r on row r)
+  __shared__ uint32_t sq_b[K][4 * 16];  // each item's low windows + [b]B, cached form (component r on row r)
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint32_t base = blockIdx.x * K;
   if (wave == K) {
@@ -1024,11 +1029,20 @@ hsv_verify_joint_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, cons
     const uint32_t d2 = fl_from_fe(fe_d2(), L);
     HSV_NOUNROLL
     for (uint32_t t = 0; t < K; ++t) {
-      if (srec[(kPrepWords - 1) * K + t] & kPrepFallback) continue;
-      uint32_t b[8];
+      const uint32_t meta_t = srec[(kPrepWords - 1) * K + t];
+      if (meta_t & kPrepFallback) continue;
+      // the low kJointLo windows of the item's two scalars over its tables,
+      // then its whole wide B comb onto that sum
+      uint32_t d1[5], d0[5], b[8];
+      HSV_UNROLL
+      for (int i = 0; i < 5; ++i) {
+        d1[i] = srec[i * K + t];
+        d0[i] = srec[(5 + i) * K + t];
+      }
       HSV_UNROLL
       for (int i = 0; i < 8; ++i) b[i] = srec[(10 + i) * K + t];
-      qp_ext qb{0u, fl_small(1, L), fl_small(1, L), 0u};
+      qp_ext qb = quad_straus2_low<WA, G::NW, kJointLo>(d1, d0, stab[t][0], stab[t][1],
+                                                         (meta_t & kPrepC0Neg) ? 1u : 0u, L);
       HSV_NOUNROLL
       for (uint32_t h = 0; h < 2u; ++h) qb = quad_comb_half<CB>(qb, b, comb_b, h, L);
       sq_b[t][L.r * 16u + L.k] = q_cached_component(qb, d2, L);
@@ -1083,7 +1097,7 @@ hsv_verify_joint_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, cons
       d1[i] = srec[i * K + wave];
       d0[i] = srec[(5 + i) * K + wave];
     }
-    q = quad_straus2<WA, G::NW>(d1, d0, tab_r, tab_a, (meta & kPrepC0Neg) ? 1u : 0u, L);
+    q = quad_straus2<WA, G::NW, kJointLo>(d1, d0, tab_r, tab_a, (meta & kPrepC0Neg) ? 1u : 0u, L);
   }
   __syncthreads();  // the prepass wave's [b]B
   if (meta & kPrepFallback) {

@@ -372,7 +372,9 @@ __device__ __forceinline__ qp_ext quad_straus_low(uint32_t d[5], const uint32_t 
 // The two-scalar Straus of one wave holding both tables (the joint form):
 // [c1](-R) + [c0](-A) with shared doublings, digits d1 over tab_r and d0 over
 // tab_a (the sign of c0 flips the A digits), as straus_vt over two tables.
-template <int WA, int NW>
+// LO > 0: the low LO windows are only doubled through (quad_straus, and
+// quad_straus2_low for the helper's part).
+template <int WA, int NW, int LO = 0>
 __device__ __forceinline__ qp_ext quad_straus2(uint32_t d1[5], uint32_t d0[5], const uint32_t *tab_r,
                                                const uint32_t *tab_a, uint32_t flip_a, const QuadLane &L) {
   constexpr int TS = 1 << (WA - 1);
@@ -393,18 +395,37 @@ __device__ __forceinline__ qp_ext quad_straus2(uint32_t d1[5], uint32_t d0[5], c
     limbs_shl<5>(d1, WA);
     limbs_shl<5>(d0, WA);
     n0 ^= flip_a;
-    uint32_t op1 = tab_r[(m1 * 4u + q_cached_col(L.r, n1)) * 16u + L.k];
-    uint32_t op0 = tab_a[(m0 * 4u + q_cached_col(L.r, n0)) * 16u + L.k];
-    if (n1 && L.r == 2u) op1 = fl_sub(0u, op1, L);
-    if (n0 && L.r == 2u) op0 = fl_sub(0u, op0, L);
+    uint32_t op1 = 0u, op0 = 0u;
+    if (i >= LO) {
+      op1 = tab_r[(m1 * 4u + q_cached_col(L.r, n1)) * 16u + L.k];
+      op0 = tab_a[(m0 * 4u + q_cached_col(L.r, n0)) * 16u + L.k];
+      if (n1 && L.r == 2u) op1 = fl_sub(0u, op1, L);
+      if (n0 && L.r == 2u) op0 = fl_sub(0u, op0, L);
+    }
     if (i != top) {
       HSV_NOUNROLL
       for (int j = 0; j < WA; ++j) q = q_dbl(q, L);
     }
-    q = q_add_op(q, op1, L);
-    q = q_add_op(q, op0, L);
+    if (i >= LO) {
+      q = q_add_op(q, op1, L);
+      q = q_add_op(q, op0, L);
+    }
   }
   return q;
+}
+
+// The helper's part of a split two-scalar Straus: the low LO windows of both
+// digit strings (the main wave runs quad_straus2<WA, NW, LO>).
+template <int WA, int NW, int LO>
+__device__ __forceinline__ qp_ext quad_straus2_low(uint32_t d1[5], uint32_t d0[5], const uint32_t *tab_r,
+                                                   const uint32_t *tab_a, uint32_t flip_a, const QuadLane &L) {
+  static_assert(LO > 0 && LO < NW, "split window");
+  HSV_UNROLL
+  for (int i = 0; i < NW - LO; ++i) {
+    limbs_shl<5>(d1, WA);
+    limbs_shl<5>(d0, WA);
+  }
+  return quad_straus2<WA, LO, 0>(d1, d0, tab_r, tab_a, flip_a, L);
 }
 
 // q + the comb digits of half h of s (row_comb_half), each row reading only
