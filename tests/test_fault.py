@@ -51,7 +51,9 @@ def generic(tlib):
 def test_generic_paths_report_faults(env, tlib, generic, mode):
     _lib, _testing, crypto, synth, verifier = env
     lib = tlib
-    w = synth.qc_votes(100, seed=5)                                # 67 votes, row-form latency kernel
+    w = synth.qc_votes(100, seed=5)                                # 67 votes, quad-form latency kernel
+    joint = synth.independent_triples(600, seed=19, corrupt_frac=0.0)  # joint quad form (257..768)
+    row = synth.independent_triples(1000, seed=20, corrupt_frac=0.0)   # row form (769..3072)
     mid = synth.independent_triples(4096, seed=8, corrupt_frac=0.0)  # pair latency kernel (3073..8192)
     big = synth.independent_triples((1 << 13) + 64, seed=6, corrupt_frac=0.0)  # point-pass kernels
     packed = np.concatenate([w.pk, w.sig], axis=1).copy()
@@ -59,8 +61,11 @@ def test_generic_paths_report_faults(env, tlib, generic, mode):
     want_mid = verifier.verify_flags(mid.pk, mid.sig, mid.msg)
     want_big = verifier.verify_flags(big.pk, big.sig, big.msg)
     assert (want_small & 1).all() and (want_mid & 1).all() and (want_big & 1).all()
+    assert (verifier.verify_flags(joint.pk, joint.sig, joint.msg) & 1).all()
+    assert (verifier.verify_flags(row.pk, row.sig, row.msg) & 1).all()
     with _testing.injected_fault(mode):
-        for pk, sig, msg in ((w.pk, w.sig, w.msg), (mid.pk, mid.sig, mid.msg), (big.pk, big.sig, big.msg)):
+        for pk, sig, msg in ((w.pk, w.sig, w.msg), (joint.pk, joint.sig, joint.msg), (row.pk, row.sig, row.msg),
+                             (mid.pk, mid.sig, mid.msg), (big.pk, big.sig, big.msg)):
             with pytest.raises(_lib.HsvLibraryError, match="HSV_ERR_DEVICE_FAULT"):
                 verifier.verify_flags(pk, sig, msg)
         assert lib.hsv_verify_batch_packed(w.msg.tobytes(), packed.tobytes(), w.n) == FAULT
