@@ -310,6 +310,29 @@ def test_random_batch_vs_c_oracle(api, oracle_lib):
     assert (got == exp).all()
 
 
+def test_random_batches_latency_forms_vs_c_oracle(api, oracle_lib):
+    """The same random corrupted triples (every SURVEY 8(d) corruption kind,
+    20 %) through each latency kernel's range, cache off: quad form (1, 37,
+    256 items), joint form (257, 500, 768) and the row form (769, 2000), every
+    flag bit against the C oracle."""
+    _, verifier, synth = api
+    from hsverify import _lib
+    lib = _lib.load()
+    lib.hsv_set_auto_committee(0)
+    try:
+        w = synth.independent_triples(2000, seed=4242, corrupt_frac=0.2)
+        exp = oracle_flags(oracle_lib, w.pk, w.sig, w.msg)
+        lo = 0
+        for m in (1, 37, 256, 257, 500, 768, 769, 2000):
+            idx = (np.arange(m) + lo) % w.pk.shape[0]
+            lo += 611
+            got = verifier.verify_flags(w.pk[idx], w.sig[idx], w.msg[idx])
+            bad = np.nonzero(got != exp[idx])[0]
+            assert bad.size == 0, (m, [(int(idx[i]), int(got[i]), int(exp[idx][i])) for i in bad[:8]])
+    finally:
+        lib.hsv_set_auto_committee(1)
+
+
 # ---- ragged sizes, shared digests, layouts ------------------------------------
 @pytest.mark.parametrize("n", [1, 4095, 4096, 4097])
 def test_zero_copy_boundary_vs_c_oracle(api, oracle_lib, n):
