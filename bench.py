@@ -224,6 +224,24 @@ def _timed(fn, reps, warm=10):
     return ts
 
 
+def _timed_gap(fn, reps, gap_us, warm=5):
+    """p50 / p99 of fn with gap_us of host busy-wait before every call: a
+    consensus node verifies a QC every few milliseconds, not back to back, and
+    an idle GPU takes ~5 us longer for the next launch (profiles/r05an_gap.txt)."""
+    for _ in range(warm):
+        fn()
+    ts = []
+    for _ in range(reps):
+        t_end = time.perf_counter() + gap_us * 1e-6
+        while time.perf_counter() < t_end:
+            pass
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return {"p50_ms": float(np.median(ts) * 1e3), "p99_ms": float(np.percentile(ts, 99) * 1e3), "reps": reps,
+            "gap_us": gap_us}
+
+
 MARKS = ("lookup", "slot", "staged", "launch", "sync", "done")  # hsv.h HSV_MARK_*
 
 
@@ -318,6 +336,7 @@ def qc_latency(reps, auto=True):
             fn()
         lib.hsv_auto_committee_wait(60000)
 
+    gaps = {}
     for committee in (4, 100, 1000):
         w = synth.qc_votes(committee, seed=committee)
         packed = np.concatenate([w.pk, w.sig], axis=1).tobytes()
@@ -326,6 +345,10 @@ def qc_latency(reps, auto=True):
         settle(call)
         assert call() == 1
         res[f"n{committee}_votes{w.n}"] = _timed_lib(call, reps)
+        if auto and committee != 100:  # the same calls 1 ms apart, as consensus issues them
+            gaps[f"n{committee}_votes{w.n}"] = _timed_gap(call, min(reps, 200), 1000)
+    if gaps:
+        res["idle_gap_1ms"] = gaps
     # C3 with 5 % corrupted votes (member keys): Err, every flag computed
     w = member_corrupted(synth.qc_votes, 1000, seed=1000)
     packed = np.concatenate([w.pk, w.sig], axis=1).tobytes()
@@ -461,6 +484,8 @@ def resident_child(reps, tc_reps):
     call = lambda: lib.hsv_verify_batch_packed(d0, packed, w.n)
     assert call() == 1
     res["n4_votes3"] = _timed_lib(call, reps)
+    call = lambda: lib.hsv_verify_strict(d0, pk0, sig0)
+    res["single_verify_strict_gap_1ms"] = _timed_gap(call, min(reps, 200), 1000)
     res["tc_dropin_sequential"] = tc_dropin_sequential(tc_reps)
     orc = _oracle()
     ts = _timed(lambda: orc.oracle_verify_flags(pk0, sig0, d0, 32), 200, warm=5)
@@ -779,6 +804,11 @@ def compact(out):
             lat["tc_c3_dropin_sequential"] = {"gpu": _pp(seq), "gpu_call_p50": _r(seq["call_p50_ms"]),
                                               "cpu_p50": cpu("tc_n1000_votes667_clean_p50_ms"),
                                               "what": "667 sequential verify_strict calls, as TC::verify"}
+        gq = (out.get("qc_latency") or {}).get("idle_gap_1ms")
+        if gq:
+            lat["idle_gap_1ms"] = {"c1": _r(gq["n4_votes3"]["p50_ms"]), "c3": _r(gq["n1000_votes667"]["p50_ms"]),
+                                   "resident_single": _r(rs.get("single_verify_strict_gap_1ms", {}).get("p50_ms")),
+                                   "what": "p50 with 1 ms of host idle before each call (consensus pacing)"}
         cc = out.get("committee_cache", {})
         if cc:
             lat["explicit_committee"] = {"c2": _pp(cc.get("qc_n100_votes67")), "c3": _pp(cc.get("qc_n1000_votes667"))}

@@ -19,7 +19,7 @@ import json, sys
 sys.path.insert(0, {root!r}); sys.path.insert(0, {root!r} + "/hotstuff-digital-signature-benchmarking_amd")
 import bench
 r = bench.qc_latency({reps}, auto={auto})
-print(json.dumps({{k: v["p50_ms"] for k, v in r.items() if isinstance(v, dict)}}))
+print(json.dumps({{k: v["p50_ms"] for k, v in r.items() if isinstance(v, dict) and "p50_ms" in v}}))
 """
 
 

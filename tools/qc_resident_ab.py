@@ -19,7 +19,7 @@ import time
 import numpy as np
 from hsverify import synth
 r = bench.qc_latency({reps}, auto=True)
-out = {{k: v["p50_ms"] for k, v in r.items() if isinstance(v, dict)}}
+out = {{k: v["p50_ms"] for k, v in r.items() if isinstance(v, dict) and "p50_ms" in v}}
 lib = bench._oracle()   # the dalek port's single verify_strict, same process and box
 w = synth.qc_votes(4, seed=4)
 ts = bench._timed(lambda: lib.oracle_verify_flags(bytes(w.pk[0]), bytes(w.sig[0]), bytes(w.msg), 32), 200, warm=5)
