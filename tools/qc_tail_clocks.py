@@ -34,6 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=1000)
     ap.add_argument("--cpus", default=None, help="pin the process to these CPUs first (e.g. 64-71)")
+    ap.add_argument("--gap-us", type=float, default=0.0, help="host busy-wait before each call")
     a = ap.parse_args()
     if a.cpus:
         lo, _, hi = a.cpus.partition("-")
@@ -71,6 +72,9 @@ def main():
         gc.collect()
         gc.disable()
         for i in range(a.reps + 20):
+            t_end = time.perf_counter() + a.gap_us * 1e-6
+            while time.perf_counter() < t_end:
+                pass
             t0 = time.perf_counter()
             rc = call()
             dt = time.perf_counter() - t0
