@@ -2,6 +2,10 @@
  * ed25519_oracle.c -- C restatement of the reference's Ed25519 verification
  * rules (ed25519-dalek 1.0.1 on curve25519-dalek 3.x, u64 backend).
  *
+ * Parity status: UNPINNED (the reference holds no known-answer vectors for
+ * this path and ed25519-dalek cannot be built here); cross-checked against
+ * RFC 8032 section 7.1, libsodium and OpenSSL.
+ *
  * TEST INFRASTRUCTURE ONLY.  Used by tests/ as a fast checker (cross-checked
  * against oracle/ed25519_ref.py and the golden vectors) and by bench.py's
  * cpu_baseline leg as the "port" CPU baseline.  The product library never

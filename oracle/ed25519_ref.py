@@ -1,5 +1,9 @@
 """Pure-Python restatement of the reference's Ed25519 acceptance rules.
 
+Parity status: UNPINNED.  The reference holds no known-answer vectors for this
+path and ed25519-dalek cannot be built here; the restatement is cross-checked
+against RFC 8032 section 7.1, libsodium and OpenSSL instead.
+
 TEST INFRASTRUCTURE ONLY.  Nothing in the product path (the HIP library under
 ``hotstuff-digital-signature-benchmarking_amd/``) imports, links or executes
 this module.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
