@@ -13,7 +13,7 @@ Workload (config C4 / C5 shards): each rank holds n = 2^20 independent
 (public key, 32-byte digest, signature) triples in HBM, 5 % corrupted across
 the SURVEY 8(d) corruption kinds.  A step is one verification launch over the
 rank's whole batch (per-item flag bytes + packed STRICT_OK bits); consecutive
-steps alternate over --streams (default 2) HIP streams with their own outputs,
+steps alternate over --streams (default 3) HIP streams with their own outputs,
 so one batch's launch starts in the previous one's grid end.  Shards are
 contiguous and independent: no collective touches the data path; the gloo
 group only carries the timing barrier, the max-over-ranks reduction and the
@@ -34,7 +34,8 @@ Reported beside it:
                    of 64, verify_strict for failing chunks).
   qc_latency*      p50/p99 of the host-buffer QC call (C1/C2/C3), of one
                    verify_strict, of the C3 QC from bincode, and of C3 with 5 %
-                   corrupted votes.
+                   corrupted votes; C1 and C3 again paced 1 ms apart
+                   (idle_gap_1ms, as consensus issues them).
   tc_latency       C3 TC (667 timeouts, per-vote digests) through the batched
                    strict API and from bincode, 0 % and 5 % corrupted.
   tc_dropin_sequential  C3 TC the way the unchanged caller verifies it: 667
@@ -45,6 +46,11 @@ Reported beside it:
   qc_cpu_baseline  one host core: the C port of dalek verify_batch (Straus /
                    Pippenger MSM) for C1-C3 QCs and the sequential TC::verify loop.
   mempool_tx       2^20 client transactions of 512 B in HBM.
+
+Each rank binds its threads to its GPU's NUMA node before any measurement
+(pin_to_gpu_node; the CPU baselines run on all the host's CPUs): calls from
+the other socket of a two-socket host measured up to 9 us slower
+(profiles/r05ac_numa.txt).
 
 stdout carries ONE compact JSON line (< 4 KB: the C4 line, roofline,
 cpu_baseline, and a `latency` object with every GPU latency next to the CPU
