@@ -14,10 +14,9 @@ extern "C" {
 // QC latency kernel of one thread, run while another thread made the
 // process's first committee-cache allocations, accepted a forged vote in 8 of
 // 16 runs of tests/native/crypto_tests.cpp; with this pool, 0 of 16
-// (tools/forgery_debug.sh).  HSV_WS_POOL=default
-// selects the default pool again in the measurement build (ALL_VARIANTS=1,
-// libhsv_all.so) only; the product library always uses its own pool and reads
-// no such variable.
+// (tools/forgery_debug.sh).  The
+// default-pool switch of the measurement build (HSV_WS_POOL=default) left
+// the source with that build in round 5; the library always uses its own pool.
 hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream);
 void hsv_ws_trim(void);  // hsv_shutdown: release the pools' free blocks
 

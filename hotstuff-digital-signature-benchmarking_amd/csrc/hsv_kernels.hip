@@ -25,107 +25,6 @@ namespace hsv {
 
 constexpr int kBlock = 256;
 
-#if HSV_ALL_VARIANTS
-__device__ const uint32_t g_btable[256 * 24] = {
-#include "hsv_btable.inc"
-};
-// [m * 2^133]B and [m * 2^134]B: the second fixed base of the half-size
-// scalar path (b = b_lo + 2^SPLIT b_hi, hsv_verify_core.hpp)
-__device__ const uint32_t g_btable133[256 * 24] = {
-#include "hsv_btable133.inc"
-};
-__device__ const uint32_t g_btable134[256 * 24] = {
-#include "hsv_btable134.inc"
-};
-
-struct LdsBTab {
-  const uint4 *base;
-  __device__ __forceinline__ ge_niels load(uint32_t idx) const {
-    const uint4 *e = base + idx * 6u;
-    uint32_t w[24];
-    HSV_UNROLL
-    for (int q = 0; q < 6; ++q) {
-      const uint4 v = e[q];
-      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
-    }
-    ge_niels n;
-    n.ypx = fe_from_words_masked(w);
-    n.ymx = fe_from_words_masked(w + 8);
-    n.xy2d = fe_from_words_masked(w + 16);
-    return n;
-  }
-};
-
-// One verification per lane.  WA/WB: window widths (hsv_verify_core.hpp);
-// WAVES: waves per SIMD requested from the register allocator (256 regs at 2,
-// 512 at 1).  The B table needs 2^(WB-1) entries x 96 B of LDS.
-// HALF: half-size scalars (verify_one_half: ~135 doublings instead of ~253,
-// a second LDS table for B' = [2^SPLIT]B); a lane whose lattice reduction
-// does not give short scalars (~2^-14) takes the full-length path.
-template <int WA, int WB, int WAVES, bool HALF>
-__global__ void __launch_bounds__(kBlock, WAVES)
-hsv_verify_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
-                  const uint8_t *__restrict__ sig, uint64_t sig_stride,
-                  const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
-                  uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits) {
-  constexpr int kEntries = 1 << (WB - 1);
-  constexpr int kTables = HALF ? 2 : 1;
-  __shared__ uint4 lds_b[kTables * kEntries * 6];
-  {
-    const uint4 *src = reinterpret_cast<const uint4 *>(g_btable);
-    for (int i = threadIdx.x; i < kEntries * 6; i += kBlock) lds_b[i] = src[i];
-    if constexpr (HALF) {
-      const uint4 *src2 = reinterpret_cast<const uint4 *>(HalfWindows<WA, WB>::SPLIT == 133 ? g_btable133
-                                                                                           : g_btable134);
-      static_assert(HalfWindows<WA, WB>::SPLIT == 133 || HalfWindows<WA, WB>::SPLIT == 134, "B' table");
-      for (int i = threadIdx.x; i < kEntries * 6; i += kBlock) lds_b[kEntries * 6 + i] = src2[i];
-    }
-  }
-  __syncthreads();
-
-  const uint32_t idx = blockIdx.x * kBlock + threadIdx.x;
-  const bool valid = idx < n;
-  const uint64_t li = valid ? idx : (uint64_t)(n - 1);
-
-  uint32_t pkw[8], sigw[16], msgw[8];
-  {
-    const uint4 *p = reinterpret_cast<const uint4 *>(pk + li * pk_stride);
-    const uint4 *s = reinterpret_cast<const uint4 *>(sig + li * sig_stride);
-    const uint4 *m = reinterpret_cast<const uint4 *>(msg + li * msg_stride);
-    const uint4 p0 = p[0], p1 = p[1];
-    const uint4 s0 = s[0], s1 = s[1], s2 = s[2], s3 = s[3];
-    const uint4 m0 = m[0], m1 = m[1];
-    pkw[0] = p0.x; pkw[1] = p0.y; pkw[2] = p0.z; pkw[3] = p0.w;
-    pkw[4] = p1.x; pkw[5] = p1.y; pkw[6] = p1.z; pkw[7] = p1.w;
-    sigw[0] = s0.x; sigw[1] = s0.y; sigw[2] = s0.z; sigw[3] = s0.w;
-    sigw[4] = s1.x; sigw[5] = s1.y; sigw[6] = s1.z; sigw[7] = s1.w;
-    sigw[8] = s2.x; sigw[9] = s2.y; sigw[10] = s2.z; sigw[11] = s2.w;
-    sigw[12] = s3.x; sigw[13] = s3.y; sigw[14] = s3.z; sigw[15] = s3.w;
-    msgw[0] = m0.x; msgw[1] = m0.y; msgw[2] = m0.z; msgw[3] = m0.w;
-    msgw[4] = m1.x; msgw[5] = m1.y; msgw[6] = m1.z; msgw[7] = m1.w;
-  }
-
-  LdsBTab bt{lds_b};
-  uint32_t f;
-  if constexpr (HALF) {
-    LdsBTab bt2{lds_b + kEntries * 6};
-    bool fallback = false;
-    f = verify_one_half<WA, WB>(pkw, sigw, msgw, bt, bt2, fallback);
-    if (fallback) f = verify_one<WA, WB>(pkw, sigw, msgw, bt);
-  } else {
-    f = verify_one<WA, WB>(pkw, sigw, msgw, bt);
-  }
-
-  if (valid && flags_out) flags_out[idx] = (uint8_t)f;
-  if (strict_bits) {  // lanes 0 and 1 store the two halves of the wave's ballot
-    const uint64_t mask = __ballot(valid && (f & kStrictOk));
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w = (idx - lane) / 32u + lane;  // idx - lane: multiple of 64
-    if (lane < 2u && w < (n + 31u) / 32u) strict_bits[w] = lane ? (uint32_t)(mask >> 32) : (uint32_t)mask;
-  }
-}
-
-#endif  // HSV_ALL_VARIANTS
 
 // Per-lane variable-base tables in global memory (hsv_verify_core.hpp, VT):
 // lane region = 2 tables x (ENT - 1) entries x 128 B, entry = 8 x uint4.
@@ -177,70 +76,6 @@ struct GlobalVarTab {
 template <int WA>
 constexpr int vt_lane_uint4() { return 2 * (1 << (WA - 1)) * 8; }
 
-#if HSV_ALL_VARIANTS
-// Half-size scalars with memory-resident variable-base tables.  Persistent
-// grid: block b owns lane slots [b*kBlock, (b+1)*kBlock) of `vt_ws` and walks
-// the batch with stride gridDim.x * kBlock.
-template <int WA, int WB, int WAVES>
-__global__ void __launch_bounds__(kBlock, WAVES)
-hsv_verify_mt_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
-                     const uint8_t *__restrict__ sig, uint64_t sig_stride,
-                     const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
-                     uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
-                     uint4 *__restrict__ vt_ws) {
-  constexpr int kEntries = 1 << (WB - 1);
-  constexpr int kEnt = (1 << (WA - 1)) + 1;
-  using HW = HalfWindows<WA, WB>;
-  static_assert(HW::SPLIT == 133 || HW::SPLIT == 134, "B' table");
-  __shared__ uint4 lds_b[2 * kEntries * 6];
-  {
-    const uint4 *src = reinterpret_cast<const uint4 *>(g_btable);
-    const uint4 *src2 = reinterpret_cast<const uint4 *>(HW::SPLIT == 133 ? g_btable133 : g_btable134);
-    for (int i = threadIdx.x; i < kEntries * 6; i += kBlock) {
-      lds_b[i] = src[i];
-      lds_b[kEntries * 6 + i] = src2[i];
-    }
-  }
-  __syncthreads();
-  const GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)(blockIdx.x * kBlock + threadIdx.x) * vt_lane_uint4<WA>()};
-  const LdsBTab bt{lds_b}, bt2{lds_b + kEntries * 6};
-
-  for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-    const uint32_t idx = base + threadIdx.x;
-    const bool valid = idx < n;
-    const uint64_t li = valid ? idx : (uint64_t)(n - 1);
-    uint32_t pkw[8], sigw[16], msgw[8];
-    {
-      const uint4 *p = reinterpret_cast<const uint4 *>(pk + li * pk_stride);
-      const uint4 *s = reinterpret_cast<const uint4 *>(sig + li * sig_stride);
-      const uint4 *m = reinterpret_cast<const uint4 *>(msg + li * msg_stride);
-      const uint4 p0 = p[0], p1 = p[1];
-      const uint4 s0 = s[0], s1 = s[1], s2 = s[2], s3 = s[3];
-      const uint4 m0 = m[0], m1 = m[1];
-      pkw[0] = p0.x; pkw[1] = p0.y; pkw[2] = p0.z; pkw[3] = p0.w;
-      pkw[4] = p1.x; pkw[5] = p1.y; pkw[6] = p1.z; pkw[7] = p1.w;
-      sigw[0] = s0.x; sigw[1] = s0.y; sigw[2] = s0.z; sigw[3] = s0.w;
-      sigw[4] = s1.x; sigw[5] = s1.y; sigw[6] = s1.z; sigw[7] = s1.w;
-      sigw[8] = s2.x; sigw[9] = s2.y; sigw[10] = s2.z; sigw[11] = s2.w;
-      sigw[12] = s3.x; sigw[13] = s3.y; sigw[14] = s3.z; sigw[15] = s3.w;
-      msgw[0] = m0.x; msgw[1] = m0.y; msgw[2] = m0.z; msgw[3] = m0.w;
-      msgw[4] = m1.x; msgw[5] = m1.y; msgw[6] = m1.z; msgw[7] = m1.w;
-    }
-    bool fallback = false;
-    uint32_t f = verify_one_half_mt<WA, WB>(pkw, sigw, msgw, bt, bt2, vt, fallback);
-    if (fallback) f = verify_one_mt<WA, WB>(pkw, sigw, msgw, bt, vt);
-
-    if (valid && flags_out) flags_out[idx] = (uint8_t)f;
-    if (strict_bits) {
-      const uint64_t mask = __ballot(valid && (f & kStrictOk));
-      const uint32_t lane = threadIdx.x & 63u;
-      const uint32_t w = (idx - lane) / 32u + lane;
-      if (lane < 2u && w < (n + 31u) / 32u) strict_bits[w] = lane ? (uint32_t)(mask >> 32) : (uint32_t)mask;
-    }
-  }
-}
-
-#endif  // HSV_ALL_VARIANTS
 
 // one (pk, sig, msg) record into words
 __device__ __forceinline__ void load_triple(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig,
@@ -270,93 +105,6 @@ struct HcCounters {
   uint32_t pad;
 };
 
-#if HSV_ALL_VARIANTS
-// Half-size scalars + comb table for B (hsv_verify_hc.hpp).  No LDS; the
-// per-lane tables live in `vt_ws` (lane slot = blockIdx * kBlock + threadIdx),
-// the B comb table `comb_b` is read through L2 / MALL.  Work is handed out
-// per wave, 64 items at a time, from ctr->next: a wave that started late
-// simply takes fewer batches, so the grid finishes together.
-// A lane whose lattice reduction fails (~2^-13.5) needs the full-length path,
-// about twice the work of the whole batch.  DEFER = false runs it inline
-// (its wave's batch takes ~2x as long, which shows up as a tail at the end of
-// the grid); DEFER = true appends the item to fb_list and leaves it to
-// hsv_verify_fb_kernel, launched right after on the same stream, which deals
-// the deferred items out 64 per wave (its flag byte and strict bit are
-// written there; the strict bit with an atomic OR into the word this pass
-// stored with that bit clear).
-template <int WA, int WAVES, bool PREFETCH, int CB, bool DEFER>
-__global__ void __launch_bounds__(kBlock, WAVES)
-hsv_verify_hc_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
-                     const uint8_t *__restrict__ sig, uint64_t sig_stride,
-                     const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
-                     uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
-                     uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b,
-                     HcCounters *__restrict__ ctr, uint32_t *__restrict__ fb_list) {
-  constexpr int kEnt = (1 << (WA - 1)) + 1;
-  GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)(blockIdx.x * kBlock + threadIdx.x) * vt_lane_uint4<WA>()};
-  const uint32_t lane = threadIdx.x & 63u;
-  for (;;) {
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&ctr->next, 64u);
-    base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
-    if (base >= n) break;
-    const uint32_t idx = base + lane;
-    const bool valid = idx < n;
-    uint32_t pkw[8], sigw[16], msgw[8];
-    load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, valid ? idx : (uint64_t)(n - 1), pkw, sigw, msgw);
-    bool fallback = false;
-    uint32_t f = verify_one_half_comb<WA, PREFETCH, CB>(pkw, sigw, msgw, comb_b, vt, fallback);
-    bool deferred = false;
-    if constexpr (DEFER) {
-      deferred = fallback && valid;
-      if (deferred) fb_list[atomicAdd(&ctr->fb_count, 1u)] = idx;
-    } else {
-      if (fallback) f = verify_one_full_comb<WA, PREFETCH, CB>(pkw, sigw, msgw, comb_b, vt);
-    }
-
-    if (valid && !deferred && flags_out) flags_out[idx] = (uint8_t)f;
-    if (strict_bits) {
-      // lanes 0 and 1 store the two 32-bit halves of the wave's ballot
-      const uint64_t mask = __ballot(valid && !deferred && (f & kStrictOk));
-      const uint32_t w = base / 32u + lane;
-      if (lane < 2u && w < (n + 31u) / 32u) strict_bits[w] = lane ? (uint32_t)(mask >> 32) : (uint32_t)mask;
-    }
-  }
-}
-
-// The deferred full-length items of the preceding hsv_verify_hc_kernel<...,
-// DEFER = true> launch (same stream, same workspace).
-template <int WA, int WAVES, int CB>
-__global__ void __launch_bounds__(kBlock, WAVES)
-hsv_verify_fb_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride,
-                     const uint8_t *__restrict__ sig, uint64_t sig_stride,
-                     const uint8_t *__restrict__ msg, uint64_t msg_stride,
-                     uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
-                     uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b,
-                     HcCounters *__restrict__ ctr, const uint32_t *__restrict__ fb_list) {
-  constexpr int kEnt = (1 << (WA - 1)) + 1;
-  GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)(blockIdx.x * kBlock + threadIdx.x) * vt_lane_uint4<WA>()};
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t cnt = __builtin_amdgcn_readfirstlane(ctr->fb_count);
-  for (;;) {
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&ctr->fb_next, 64u);
-    base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
-    if (base >= cnt) break;
-    const uint32_t j = base + lane;
-    const bool valid = j < cnt;
-    const uint32_t idx = fb_list[valid ? j : base];
-    uint32_t pkw[8], sigw[16], msgw[8];
-    load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, idx, pkw, sigw, msgw);
-    const uint32_t f = verify_one_full_comb<WA, false, CB>(pkw, sigw, msgw, comb_b, vt);
-    if (valid) {
-      if (flags_out) flags_out[idx] = (uint8_t)f;
-      if (strict_bits && (f & kStrictOk)) atomicOr(&strict_bits[idx >> 5], 1u << (idx & 31u));
-    }
-  }
-}
-
-#endif  // HSV_ALL_VARIANTS
 
 #ifdef HSV_PHASE_CLOCKS  // tools/phase_clock_probe.py only: 8 words per 64-item batch of the point pass
 constexpr uint32_t kPhaseCap = 1u << 16;
@@ -1129,83 +877,6 @@ hsv_verify_joint_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, cons
   }
 }
 
-#if HSV_ALL_VARIANTS
-// Point pass with a pair-lane tail (variant 22): as hsv_verify_hp_kernel, but
-// the last n_tail items (a multiple-of-64 boundary, about one round of the
-// persistent grid) are dealt out as 32-item batches run two lanes per item
-// (verify_pair_prepped).  A pair batch finishes in ~72 % of a 64-item batch's
-// time, so the final partial round of the grid is shorter.  Virtual range:
-// [fallback items | n - n_tail items in 64-batches | n_tail items, 64 units per 32].
-template <int WA, int WAVES, int CB>
-__global__ void __launch_bounds__(kBlock, WAVES)
-hsv_verify_hpt_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const uint8_t *__restrict__ sig,
-                      uint64_t sig_stride, const uint8_t *__restrict__ msg, uint64_t msg_stride, uint32_t n,
-                      uint32_t n_tail, uint8_t *__restrict__ flags_out, uint32_t *__restrict__ strict_bits,
-                      uint4 *__restrict__ vt_ws, const uint32_t *__restrict__ comb_b,
-                      const uint32_t *__restrict__ rec, HcCounters *__restrict__ ctr,
-                      const uint32_t *__restrict__ fb_list) {
-  constexpr int kEnt = (1 << (WA - 1)) + 1;
-  GlobalVarTab<kEnt> vt{vt_ws + (uint64_t)(blockIdx.x * kBlock + threadIdx.x) * vt_lane_uint4<WA>()};
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t nfb = __builtin_amdgcn_readfirstlane(ctr->fb_count);
-  const uint32_t fb_end = (nfb + 63u) & ~63u;
-  const uint32_t n_reg = n - n_tail;  // multiple of 64 (launch_hpt)
-  const uint32_t tail_start = fb_end + n_reg;
-  const uint32_t v_end = tail_start + 2u * n_tail;
-  const uint32_t words = (n + 31u) / 32u;
-  for (;;) {
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&ctr->next, 64u);
-    base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
-    if (base >= v_end) break;
-    if (base < fb_end) {
-      const uint32_t j = base + lane;
-      const bool valid = j < nfb;
-      const uint32_t idx = fb_list[valid ? j : base];
-      uint32_t pkw[8], sigw[16], msgw[8];
-      load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, idx, pkw, sigw, msgw);
-      const uint32_t f = verify_one_full_comb<WA, false, CB>(pkw, sigw, msgw, comb_b, vt);
-      if (valid) {
-        if (flags_out) flags_out[idx] = (uint8_t)f;
-        if (strict_bits && (f & kStrictOk)) atomicOr(&strict_bits[idx >> 5], 1u << (idx & 31u));
-      }
-      continue;
-    }
-    const bool tail = base >= tail_start;
-    const uint32_t p = tail ? (lane & 1u) : 0u;
-    const uint32_t idx = tail ? n_reg + (base - tail_start) / 2u + lane / 2u : base - fb_end + lane;
-    const bool valid = idx < n;
-    const uint32_t li = valid ? idx : n - 1u;
-    uint32_t pkw[8], rw[8];
-    {
-      const uint4 *pp = reinterpret_cast<const uint4 *>(pk + (uint64_t)li * pk_stride);
-      const uint4 *rp = reinterpret_cast<const uint4 *>(sig + (uint64_t)li * sig_stride);
-      const uint4 p0 = pp[0], p1 = pp[1], r0 = rp[0], r1 = rp[1];
-      pkw[0] = p0.x; pkw[1] = p0.y; pkw[2] = p0.z; pkw[3] = p0.w;
-      pkw[4] = p1.x; pkw[5] = p1.y; pkw[6] = p1.z; pkw[7] = p1.w;
-      rw[0] = r0.x; rw[1] = r0.y; rw[2] = r0.z; rw[3] = r0.w;
-      rw[4] = r1.x; rw[5] = r1.y; rw[6] = r1.z; rw[7] = r1.w;
-    }
-    const uint32_t meta = rec[18ull * n + li];
-    const bool own = valid && !(meta & kPrepFallback) && p == 0u;
-    uint32_t f;
-    if (tail) f = verify_pair_prepped<WA, CB>(p, pkw, rw, rec + li, n, meta, comb_b, vt);
-    else f = verify_one_prepped<WA, CB>(pkw, rw, rec + li, n, meta, comb_b, vt);
-    if (own && flags_out) flags_out[idx] = (uint8_t)f;
-    if (strict_bits) {
-      if (tail) {
-        if (own && (f & kStrictOk)) atomicOr(&strict_bits[idx >> 5], 1u << (idx & 31u));
-      } else {
-        const uint64_t mask = __ballot(own && (f & kStrictOk));
-        const uint32_t w = (base - fb_end) / 32u + lane;
-        const uint32_t part = lane ? (uint32_t)(mask >> 32) : (uint32_t)mask;
-        if (lane < 2u && w < words && part) atomicOr(&strict_bits[w], part);
-      }
-    }
-  }
-}
-
-#endif  // HSV_ALL_VARIANTS
 
 // ---- v_mad_u64_u32 issue-rate probe -------------------------------------
 // 8 independent accumulation chains, 16 mads per asm statement (the compiler
@@ -1281,13 +952,6 @@ extern "C" void hsv_ws_trim(void) {
 }
 
 extern "C" hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream) {
-#if HSV_ALL_VARIANTS  // diagnosis of DESIGN.md 6.2 only: the default pool (HSV_WS_POOL=default)
-  static const bool own = [] {
-    const char *v = std::getenv("HSV_WS_POOL");
-    return !(v && std::strcmp(v, "default") == 0);
-  }();
-  if (!own) return hipMallocAsync(p, bytes, stream);
-#endif
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
@@ -1339,70 +1003,6 @@ uint32_t next_nonce() {
   return (ctr.fetch_add(0x61c88646u) * 2654435761u) | 1u;
 }
 
-#if HSV_ALL_VARIANTS
-// Persistent-grid launch of hsv_verify_mt_kernel with a stream-ordered
-// workspace for the per-lane tables (freed on the same stream).
-template <int WA, int WB, int WAVES, bool COMB, bool PREFETCH = true, int CB = 8, bool DEFER = false>
-hipError_t launch_mt(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
-                     const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
-                     uint32_t *strict_bits, const uint32_t *comb_b, hipStream_t stream) {
-  const void *kern;
-  if constexpr (COMB) kern = reinterpret_cast<const void *>(hsv::hsv_verify_hc_kernel<WA, WAVES, PREFETCH, CB, DEFER>);
-  else kern = reinterpret_cast<const void *>(hsv::hsv_verify_mt_kernel<WA, WB, WAVES>);
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  static std::mutex mu;
-  static std::unordered_map<int, int> slots_per_dev;  // resident blocks per device for this kernel
-  int resident = 0;
-  {
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = slots_per_dev.find(dev);
-    if (it == slots_per_dev.end()) {
-      int bpc = 0, cus = 0;
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kern, hsv::kBlock, 0);
-      if (e != hipSuccess) return e;
-      e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      if (e != hipSuccess) return e;
-      it = slots_per_dev.emplace(dev, std::max(1, bpc) * std::max(1, cus)).first;
-    }
-    resident = it->second;
-  }
-  const uint32_t blocks_needed = (n + hsv::kBlock - 1) / hsv::kBlock;
-  const uint32_t grid = std::min<uint32_t>(blocks_needed, (uint32_t)resident);
-  // workspace: per-lane tables | counters (256 B) | deferred-item list (4 B per item)
-  const size_t ws_bytes = (size_t)grid * hsv::kBlock * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
-  const size_t fb_bytes = DEFER ? (size_t)n * sizeof(uint32_t) : 0;
-  void *ws = nullptr;
-  e = hsv_ws_malloc(&ws, ws_bytes + 256 + fb_bytes, stream);
-  if (e != hipSuccess) return e;
-  uint8_t *ws8 = static_cast<uint8_t *>(ws);
-  hsv::HcCounters *ctr = reinterpret_cast<hsv::HcCounters *>(ws8 + ws_bytes);
-  uint32_t *fb_list = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256);
-  uint4 *vt_ws = reinterpret_cast<uint4 *>(ws);
-  if constexpr (COMB) {
-    e = hipMemsetAsync(ctr, 0, sizeof(hsv::HcCounters), stream);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((hsv::hsv_verify_hc_kernel<WA, WAVES, PREFETCH, CB, DEFER>), dim3(grid), dim3(hsv::kBlock), 0,
-                       stream, pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, vt_ws,
-                       comb_b, ctr, fb_list);
-    e = hipGetLastError();
-    if (DEFER && e == hipSuccess) {
-      hipLaunchKernelGGL((hsv::hsv_verify_fb_kernel<WA, WAVES, CB>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
-                         pk_stride, sig, sig_stride, msg, msg_stride, flags_out, strict_bits, vt_ws, comb_b, ctr,
-                         fb_list);
-      e = hipGetLastError();
-    }
-  } else {
-    hipLaunchKernelGGL((hsv::hsv_verify_mt_kernel<WA, WB, WAVES>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
-                       pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, vt_ws);
-    e = hipGetLastError();
-  }
-  const hipError_t ef = hipFreeAsync(ws, stream);
-  return e != hipSuccess ? e : ef;
-}
-
-#endif  // HSV_ALL_VARIANTS
 
 #ifndef HSV_HP_WAVES
 #define HSV_HP_WAVES 3  // waves per SIMD of the point pass (launch bounds: 168 VGPRs)
@@ -1421,18 +1021,13 @@ struct TxPrep {
   uint8_t *records;
 };
 
-template <int WA, int WAVES, int CB, bool TAIL = false>
+template <int WA, int WAVES, int CB>
 hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, uint64_t sig_stride,
                      const uint8_t *msg, uint64_t msg_stride, uint32_t n, uint8_t *flags_out,
                      uint32_t *strict_bits, const uint32_t *comb_b, uint32_t *fault, hipStream_t stream,
                      const TxPrep *tx = nullptr, void *ws_in = nullptr, size_t ws_cap = 0,
                      size_t *ws_need = nullptr) {
   const void *kern = reinterpret_cast<const void *>(hsv::hsv_verify_hp_kernel<WA, WAVES, CB>);
-#if HSV_ALL_VARIANTS
-  if constexpr (TAIL) kern = reinterpret_cast<const void *>(hsv::hsv_verify_hpt_kernel<WA, WAVES, CB>);
-#else
-  static_assert(!TAIL, "the pair-tail point pass is built with HSV_ALL_VARIANTS only");
-#endif
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
@@ -1491,16 +1086,6 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
     e = hipGetLastError();
   }
   if (e == hipSuccess) {
-#if HSV_ALL_VARIANTS
-    if constexpr (TAIL) {
-      // about one round of the grid as pair batches; the regular range stays a multiple of 64
-      const uint32_t target = grid * (hsv::kBlock / 64u) * 32u;
-      const uint32_t n_tail = n > 2u * target ? n - ((n - target) & ~63u) : 0u;
-      hipLaunchKernelGGL((hsv::hsv_verify_hpt_kernel<WA, WAVES, CB>), dim3(grid), dim3(hsv::kBlock), 0, stream,
-                         pk, pk_stride, sig, sig_stride, msg, msg_stride, n, n_tail, flags_out, strict_bits, vt_ws,
-                         comb_b, rec, ctr, fb_list);
-    } else
-#endif
     {
       hipLaunchKernelGGL((hsv::hsv_verify_hp_kernel<WA, WAVES, CB>), dim3(grid), dim3(hsv::kBlock), 0, stream, pk,
                          pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, vt_ws, comb_b, rec,
@@ -1733,51 +1318,8 @@ extern "C" hipError_t hsv_launch_verify(int variant, const uint8_t *pk, uint64_t
                                   fault, stream);
       return launch_hp<4, HSV_HP_WAVES, 16>(pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits,
                                             comb_b, fault, stream);
-#if HSV_ALL_VARIANTS
-    default: break;
-#else
-    default: return hipErrorInvalidValue;
-#endif
-  }
-#if HSV_ALL_VARIANTS
-  const uint32_t grid = (n + hsv::kBlock - 1) / hsv::kBlock;
-#define HSV_LAUNCH(WA, WB, WV, HALF)                                                           \
-  hipLaunchKernelGGL((hsv::hsv_verify_kernel<WA, WB, WV, HALF>), dim3(grid), dim3(hsv::kBlock), 0, \
-                     stream, pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out,   \
-                     strict_bits)
-#define HSV_ARGS pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, stream
-#define HSV_ARGS_F pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out, strict_bits, comb_b, fault, stream
-  switch (variant) {
-    case 0: HSV_LAUNCH(2, 8, 2, false); break;
-    case 1: HSV_LAUNCH(3, 9, 1, false); break;
-    case 2: HSV_LAUNCH(4, 8, 1, false); break;
-    case 3: HSV_LAUNCH(3, 9, 2, false); break;
-    case 4: HSV_LAUNCH(3, 9, 2, true); break;
-    case 5: HSV_LAUNCH(3, 9, 1, true); break;
-    case 6: HSV_LAUNCH(2, 8, 2, true); break;
-    case 7: return launch_mt<3, 9, 2, false>(HSV_ARGS);
-    case 8: return launch_mt<2, 8, 2, false>(HSV_ARGS);
-    case 9: return launch_mt<4, 8, 2, false>(HSV_ARGS);
-    case 10: return launch_mt<3, 3, 2, true>(HSV_ARGS);
-    case 11: return launch_mt<4, 4, 2, true>(HSV_ARGS);
-    case 12: return launch_mt<5, 5, 2, true>(HSV_ARGS);
-    case 13: return launch_mt<4, 4, 3, true, false>(HSV_ARGS);
-    case 14: return launch_mt<4, 4, 2, true, false>(HSV_ARGS);
-    case 15: return launch_mt<4, 4, 3, true, false, 16>(HSV_ARGS);
-    case 16: return launch_mt<4, 4, 2, true, false, 16>(HSV_ARGS);
-    case 17: return launch_mt<4, 4, 3, true, false, 16, true>(HSV_ARGS);
-    case 18: return launch_mt<4, 4, 2, true, false, 16, true>(HSV_ARGS);
-    case 20: return launch_hp<4, 2, 16>(HSV_ARGS_F);
-    case 22:
-      if (n <= kPairMax) return launch_pair<4, 16>(HSV_ARGS_F);
-      return launch_hp<4, 3, 16, true>(HSV_ARGS_F);
     default: return hipErrorInvalidValue;
   }
-#undef HSV_ARGS
-#undef HSV_ARGS_F
-#undef HSV_LAUNCH
-  return hipGetLastError();
-#endif
 }
 
 extern "C" hipError_t hsv_launch_verify_tx(int variant, const uint8_t *txs, const uint64_t *offsets,
@@ -1799,13 +1341,9 @@ extern "C" hipError_t hsv_launch_verify_tx(int variant, const uint8_t *txs, cons
 
 // Variant ids compiled into this library.  The product build carries the
 // default (21: variant 19's two-pass kernels above 2^13 items, the pair-lane
-// latency form at or below) and 19 itself; the other ids are measurement
-// history, built only with HSV_ALL_VARIANTS=1 (make ALL_VARIANTS=1).
-#if HSV_ALL_VARIANTS
-static const int kVariantIds[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22};
-#else
+// latency form at or below) and 19 itself.  The other ids of earlier rounds
+// are measurement history (git history before round 5's cleanup).
 static const int kVariantIds[] = {19, 21};
-#endif
 
 extern "C" int hsvi_variant_list(int *out, int cap) {
   const int n = (int)(sizeof(kVariantIds) / sizeof(kVariantIds[0]));

@@ -17,13 +17,13 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# HSV_LIB=libhsv_all.so selects the measurement build with every kernel
-# variant (make ALL_VARIANTS=1); it must live in this directory as well.
+# HSV_LIB selects another build of the library for tools (e.g. a clock-stamp
+# build from tools/build_ab_libs.sh); it must live in this directory as well.
 LIB_PATH = os.path.join(_HERE, os.path.basename(os.environ.get("HSV_LIB", "libhsv.so")))
 # The same objects plus the exported test hooks (csrc/hsv_test_hooks.h);
 # loaded only by tests and tools through hsverify._testing.
 TEST_LIB_PATH = os.path.join(_HERE, "libhsv_test.so")
-# Exported by libhsv_test.so / libhsv_all.so only, never by libhsv.so.
+# Exported by libhsv_test.so only, never by libhsv.so.
 HOOKS = ("hsv_test_inject_fault", "hsv_test_inject_mode", "hsv_test_corrupt_auto_committee",
          "hsv_test_lanesplit_check", "hsv_set_lattice_bits", "hsv_set_variant", "hsv_variant_list",
          "hsv_variant_available", "hsv_num_variants", "hsv_set_virtual_shards", "hsv_test_pipe_nocopy",
@@ -167,8 +167,8 @@ def load(require: bool = True):
 
 def load_test():
     """libhsv_test.so: the product's objects plus the exported test hooks.  If
-    the library already loaded exports them (HSV_LIB=libhsv_test.so or
-    libhsv_all.so), that instance is returned instead of a second one."""
+    the library already loaded exports them (HSV_LIB=libhsv_test.so), that
+    instance is returned instead of a second one."""
     global _test_lib
     main = load()
     if getattr(main, "hsv_test_inject_fault", None) is not None:

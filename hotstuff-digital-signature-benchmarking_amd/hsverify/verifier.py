@@ -126,7 +126,7 @@ def measure_mad_peak() -> float:
 
 
 def set_variant(v: int) -> None:
-    """Test/measurement hook (libhsv_test.so / libhsv_all.so only)."""
+    """Test/measurement hook (libhsv_test.so only)."""
     _lib.check(_lib.hook("hsv_set_variant")(v), "hsv_set_variant")
 
 

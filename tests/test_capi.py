@@ -52,7 +52,7 @@ def test_product_library_exports_exactly_the_header():
 # The environment variables the product library reads:
 # device binding, slot count, the automatic committee cache, the pack
 # threads, and the opt-in resident latency service.  Measurement switches
-# live in libhsv_test.so's hooks or the ALL_VARIANTS build only.
+# live in libhsv_test.so's hooks only.
 PRODUCT_ENV = {"HSV_DEVICE", "HSV_SLOTS", "HSV_AUTO_COMMITTEE", "HSV_PACK_THREADS", "HSV_QC_RESIDENT"}
 
 
@@ -72,7 +72,6 @@ def test_product_library_reads_only_the_documented_environment():
     for f in os.listdir(src):
         if f.endswith((".cpp", ".hip", ".h", ".hpp")):
             text = open(os.path.join(src, f)).read()
-            text = re.sub(r"#if HSV_ALL_VARIANTS.*?#endif", "", text, flags=re.S)  # measurement build only
             read |= set(re.findall(r'(?:getenv|env_int)\("(HSV_[A-Z0-9_]+)"', text))
     assert read <= PRODUCT_ENV, sorted(read - PRODUCT_ENV)
     doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()

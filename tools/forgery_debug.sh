@@ -3,7 +3,9 @@
 # four builds/settings: the round-2 neutral-point check (a library built with
 # -DHSV_NEUTRAL_NO_Z_CHECK in abdir_oldcheck/) or the fail-closed one, with launch
 # workspaces from the default HIP memory pool (HSV_WS_POOL=default) or the library's own
-# pool.  Prints failing runs' stderr and the failure count per mode.
+# pool.  Prints failing runs' stderr and the failure count per mode.  Round-2 record
+# (DESIGN.md section 6.2): the HSV_WS_POOL switch was a measurement-build knob, removed
+# from the source in round 5, so the "default" rows need a library built from git history.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out; mkdir -p $OUT
 AB=$(pwd)/hotstuff-digital-signature-benchmarking_amd/abdir_oldcheck

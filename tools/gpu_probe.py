@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Development probe: golden parity + throughput for each kernel variant on one GPU.
-The product library ships variants 19 and 21 only; run with HSV_LIB=libhsv_all.so
-(make ALL_VARIANTS=1) for the others.
+The library ships variants 19 and 21 only; the historical variants (make
+ALL_VARIANTS=1) are in git history before round 5's cleanup.
 
 python tools/gpu_probe.py [--n 1048576] [--reps 5]
 """
