@@ -972,13 +972,23 @@ extern "C" hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream) 
       uint64_t keep = UINT64_MAX;
       e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
       if (e != hipSuccess) return e;
-      // A block freed by a launch still running on another stream is never
-      // handed out by making the new launch wait for that stream: launches on
-      // different streams (consecutive batches, pipelined chunks) must be
-      // free to overlap.  Blocks whose free has completed are reused.
+      // A block is reused only on the stream that freed it (stream order
+      // alone makes that safe).  No cross-stream reuse of any kind:
+      // - internal dependencies would make a new launch wait for another
+      //   stream, and launches on different streams (consecutive batches,
+      //   pipelined chunks) must be free to overlap;
+      // - with event-dependency and opportunistic reuse, a launch on a
+      //   stream that had waited (through a third stream) on an event of the
+      //   freeing stream got a block still in use by a running launch there:
+      //   two point passes shared one work counter and prepass records and
+      //   returned wrong flags (round 5, tools/mempool_split_probe.py,
+      //   tests/test_device_model.py::test_batches_behind_cross_stream_event_chains).
       int no = 0;
-      e = hipMemPoolSetAttribute(pool, hipMemPoolReuseAllowInternalDependencies, &no);
-      if (e != hipSuccess) return e;
+      for (hipMemPoolAttr a : {hipMemPoolReuseAllowInternalDependencies, hipMemPoolReuseFollowEventDependencies,
+                               hipMemPoolReuseAllowOpportunistic}) {
+        e = hipMemPoolSetAttribute(pool, a, &no);
+        if (e != hipSuccess) return e;
+      }
       it = pools.emplace(dev, pool).first;
     }
     pool = it->second;

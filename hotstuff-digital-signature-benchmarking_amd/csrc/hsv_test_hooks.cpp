@@ -23,5 +23,12 @@ int hsv_set_virtual_shards(int k) { return hsvi_set_virtual_shards(k); }
 int hsv_test_pipe_nocopy(int on) { return hsvi_set_pipe_nocopy(on); }
 void hsv_test_resident_counts(uint64_t *posted, uint64_t *answered) { hsvh::resident_counts(posted, answered); }
 int hsv_test_resident_post_bad(uint32_t m) { return hsvh::resident_post_bad(m); }
+int hsv_test_tx_records(const uint8_t *d_txs, const uint64_t *d_offsets, size_t tx_size, size_t n,
+                        uint8_t *d_records, void *stream) {
+  if (n > UINT32_MAX) return HSV_ERR_INVALID_ARG;
+  const hipError_t e = hsv_launch_tx_records(d_txs, d_offsets, tx_size, (uint32_t)n, d_records,
+                                             reinterpret_cast<hipStream_t>(stream));
+  return e == hipSuccess ? HSV_OK : HSV_ERR_HIP;
+}
 
 }  // extern "C"

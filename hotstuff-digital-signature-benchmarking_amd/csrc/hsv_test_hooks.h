@@ -53,6 +53,12 @@ HSV_API void hsv_test_resident_counts(uint64_t *posted, uint64_t *answered);
  * service's limit): the kernel must refuse it, so the call returns
  * HSV_ERR_DEVICE_FAULT without reading through the header. */
 HSV_API int hsv_test_resident_post_bad(uint32_t m);
+/* Measurement only (tools/mempool_split_probe.py): the 128-byte records
+ * pk || R || s || SHA-512(message)[..32] of n transactions, enqueued on
+ * `stream` (the record kernel of hsv_verify_transactions_device's small-batch
+ * form, without the verification). */
+HSV_API int hsv_test_tx_records(const uint8_t *d_txs, const uint64_t *d_offsets, size_t tx_size, size_t n,
+                                uint8_t *d_records, void *stream);
 
 #ifdef __cplusplus
 }

@@ -145,6 +145,80 @@ def test_device_batches_on_concurrent_streams(mods, golden):
     assert (f[w.accept] & o.STRICT_OK).all() and not (f[~w.accept] & o.STRICT_OK).any()
 
 
+def test_distinct_batches_on_concurrent_streams(mods):
+    """Concurrent launches on different streams over DIFFERENT inputs (the
+    form above uses one input set, which cannot show two launches sharing a
+    workspace): three large batches and their flags, alternating over two
+    streams, two rounds, each output equal to its batch's one-stream result."""
+    import torch
+    _, _, synth, verifier = mods
+    dev = torch.device("cuda", 0)
+    n = (1 << 16) + 77
+    sets, refs = [], []
+    for k in range(3):
+        w = synth.independent_triples(n, seed=300 + k, corrupt_frac=0.2)
+        t = tuple(torch.from_numpy(x).to(dev) for x in (w.pk, w.sig, w.msg))
+        r = torch.zeros(n, dtype=torch.uint8, device=dev)
+        verifier.verify_device(*t, r)
+        torch.cuda.synchronize(dev)
+        sets.append(t)
+        refs.append(r)
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    outs = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(6)]
+    for i in range(6):
+        verifier.verify_device(*sets[i % 3], outs[i], stream=streams[i % 2].cuda_stream)
+    torch.cuda.synchronize(dev)
+    for i in range(6):
+        assert torch.equal(outs[i], refs[i % 3]), (i, int((outs[i] != refs[i % 3]).sum()))
+
+
+def test_batches_behind_cross_stream_event_chains(mods):
+    """A pipeline whose streams order their work through events recorded on
+    each other (the mempool split form of tools/mempool_split_probe.py: a
+    producer stream waits for the batch that used its buffer, the consumer
+    streams wait for the producer): two launches in flight on two streams must
+    never share a workspace block.  Round 5 found them doing so through the
+    pool's event-dependency reuse (profiles/r05ar_mempool_split.txt); every
+    output must equal its batch's one-stream result."""
+    import torch
+    _, _, synth, verifier = mods
+    dev = torch.device("cuda", 0)
+    n = (1 << 16) + 77
+    sets, refs = [], []
+    for k in range(3):
+        w = synth.independent_triples(n, seed=310 + k, corrupt_frac=0.2)
+        t = tuple(torch.from_numpy(x).to(dev) for x in (w.pk, w.sig, w.msg))
+        r = torch.zeros(n, dtype=torch.uint8, device=dev)
+        verifier.verify_device(*t, r)
+        torch.cuda.synchronize(dev)
+        sets.append(t)
+        refs.append(r)
+    prod = torch.cuda.Stream(dev)
+    cons = [torch.cuda.Stream(dev) for _ in range(2)]
+    bufs = [torch.zeros(n, 128, dtype=torch.uint8, device=dev) for _ in range(3)]
+    steps = 10
+    outs = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(steps)]
+    done = []
+    verifier.device_faults(-1, clear=True)
+    for k in range(steps):
+        if k >= 3:
+            prod.wait_event(done[k - 3])
+        with torch.cuda.stream(prod):
+            bufs[k % 3].add_(1)  # the producer's work on the batch's buffer
+        ev = torch.cuda.Event()
+        ev.record(prod)
+        c = cons[k % 2]
+        c.wait_event(ev)
+        verifier.verify_device(*sets[k % 3], outs[k], stream=c.cuda_stream)
+        ev2 = torch.cuda.Event()
+        ev2.record(c)
+        done.append(ev2)
+    torch.cuda.synchronize(dev)
+    bad = [int((outs[k] != refs[k % 3]).sum()) for k in range(steps)]
+    faults = verifier.device_faults(-1, clear=True)
+    assert not any(bad) and faults == 0, (bad, faults)
+
+
 def test_committee_survives_shutdown(mods, hsv, golden):
     _, committee, _, _ = mods
     keys = golden["pk"][:8]
