@@ -993,7 +993,17 @@ extern "C" hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream) 
     }
     pool = it->second;
   }
-  return hipMallocFromPoolAsync(p, bytes, pool, stream);
+  e = hipMallocFromPoolAsync(p, bytes, pool, stream);
+  if (e == hipErrorOutOfMemory) {
+    // Blocks freed on other streams (streams since destroyed, or idle) are
+    // never reused here; when the device runs out, wait for every launch,
+    // hand the pool's idle blocks back to the driver and try once more.
+    (void)hipGetLastError();
+    if (hipDeviceSynchronize() == hipSuccess && hipMemPoolTrimTo(pool, 0) == hipSuccess)
+      e = hipMallocFromPoolAsync(p, bytes, pool, stream);
+    if (e == hipSuccess) (void)hipGetLastError();
+  }
+  return e;
 }
 
 namespace {
