@@ -997,7 +997,8 @@ extern "C" hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream) 
   if (e == hipErrorOutOfMemory) {
     // Blocks freed on other streams (streams since destroyed, or idle) are
     // never reused here; when the device runs out, wait for every launch,
-    // hand the pool's idle blocks back to the driver and try once more.
+    // hand the pool's idle blocks back to the driver and try once more (with
+    // the opt-in resident service alive, the sync waits for its idle exit).
     (void)hipGetLastError();
     if (hipDeviceSynchronize() == hipSuccess && hipMemPoolTrimTo(pool, 0) == hipSuccess)
       e = hipMallocFromPoolAsync(p, bytes, pool, stream);
