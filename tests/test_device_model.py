@@ -219,6 +219,50 @@ def test_batches_behind_cross_stream_event_chains(mods):
     assert not any(bad) and faults == 0, (bad, faults)
 
 
+def test_transaction_batches_behind_cross_stream_event_chains(mods):
+    """The same event-ordered pipeline through the transaction device call
+    (records + the fused prepass above 2^13 items, workspaces from the pool):
+    every batch's flags equal its one-stream result, with no fault."""
+    import torch
+    from hsverify import mempool
+    _, _, synth, verifier = mods
+    dev = torch.device("cuda", 0)
+    n, size = (1 << 14) + 5, 200
+    sets, refs = [], []
+    for k in range(3):
+        t = synth.transactions(n, tx_size=size, seed=320 + k, corrupt_frac=0.2)
+        d = torch.from_numpy(np.ascontiguousarray(t.txs)).to(dev).view(-1)
+        r = torch.zeros(n, dtype=torch.uint8, device=dev)
+        mempool.verify_transactions_device(d, tx_size=size, n=n, flags=r)
+        torch.cuda.synchronize(dev)
+        sets.append(d)
+        refs.append(r)
+    prod = torch.cuda.Stream(dev)
+    cons = [torch.cuda.Stream(dev) for _ in range(2)]
+    bufs = [torch.zeros(n, 128, dtype=torch.uint8, device=dev) for _ in range(3)]
+    steps = 10
+    outs = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(steps)]
+    done = []
+    verifier.device_faults(-1, clear=True)
+    for k in range(steps):
+        if k >= 3:
+            prod.wait_event(done[k - 3])
+        with torch.cuda.stream(prod):
+            bufs[k % 3].add_(1)
+        ev = torch.cuda.Event()
+        ev.record(prod)
+        c = cons[k % 2]
+        c.wait_event(ev)
+        mempool.verify_transactions_device(sets[k % 3], tx_size=size, n=n, flags=outs[k], stream=c.cuda_stream)
+        ev2 = torch.cuda.Event()
+        ev2.record(c)
+        done.append(ev2)
+    torch.cuda.synchronize(dev)
+    bad = [int((outs[k] != refs[k % 3]).sum()) for k in range(steps)]
+    faults = verifier.device_faults(-1, clear=True)
+    assert not any(bad) and faults == 0, (bad, faults)
+
+
 def test_committee_survives_shutdown(mods, hsv, golden):
     _, committee, _, _ = mods
     keys = golden["pk"][:8]
