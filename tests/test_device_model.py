@@ -172,18 +172,19 @@ def test_distinct_batches_on_concurrent_streams(mods):
         assert torch.equal(outs[i], refs[i % 3]), (i, int((outs[i] != refs[i % 3]).sum()))
 
 
-def test_batches_behind_cross_stream_event_chains(mods):
+@pytest.mark.parametrize("n", [(1 << 16) + 77, 3000, 600, 200])
+def test_batches_behind_cross_stream_event_chains(mods, n):
     """A pipeline whose streams order their work through events recorded on
     each other (the mempool split form of tools/mempool_split_probe.py: a
     producer stream waits for the batch that used its buffer, the consumer
     streams wait for the producer): two launches in flight on two streams must
     never share a workspace block.  Round 5 found them doing so through the
     pool's event-dependency reuse (profiles/r05ar_mempool_split.txt); every
-    output must equal its batch's one-stream result."""
+    output must equal its batch's one-stream result.  Sizes: the two-pass
+    kernels, the row, joint and quad latency forms."""
     import torch
     _, _, synth, verifier = mods
     dev = torch.device("cuda", 0)
-    n = (1 << 16) + 77
     sets, refs = [], []
     for k in range(3):
         w = synth.independent_triples(n, seed=310 + k, corrupt_frac=0.2)
