@@ -40,9 +40,12 @@ Reported beside it:
                    strict API and from bincode, 0 % and 5 % corrupted.
   tc_dropin_sequential  C3 TC the way the unchanged caller verifies it: 667
                    sequential hsv_verify_strict calls (TC::verify's loop).
-  resident         a child process with HSV_QC_RESIDENT=1: one verify_strict, a
-                   C1 QC and the sequential TC loop through the resident latency
-                   service, with the dalek port's single verify in the same process.
+                   Single verifies and QCs of <= 4 cached-key votes take the
+                   library's default route: the resident latency service.
+  launched         a child process with HSV_QC_RESIDENT=0: one verify_strict, a
+                   C1 QC and the sequential TC loop launched per call (the
+                   service off), with the dalek port's single verify in the same
+                   process.
   qc_cpu_baseline  one host core: the C port of dalek verify_batch (Straus /
                    Pippenger MSM) for C1-C3 QCs and the sequential TC::verify loop.
   mempool_tx       2^20 client transactions of 512 B in HBM.
@@ -353,8 +356,6 @@ def qc_latency(reps, auto=True):
         res[f"n{committee}_votes{w.n}"] = _timed_lib(call, reps)
         if auto and committee != 100:  # the same calls 1 ms apart, as consensus issues them
             gaps[f"n{committee}_votes{w.n}"] = _timed_gap(call, min(reps, 200), 1000)
-    if gaps:
-        res["idle_gap_1ms"] = gaps
     # C3 with 5 % corrupted votes (member keys): Err, every flag computed
     w = member_corrupted(synth.qc_votes, 1000, seed=1000)
     packed = np.concatenate([w.pk, w.sig], axis=1).tobytes()
@@ -370,6 +371,9 @@ def qc_latency(reps, auto=True):
     call = lambda: lib.hsv_verify_strict(d0, pk0, sig0)
     assert call() == 1
     res["single_verify_strict"] = _timed_lib(call, reps)
+    res["single_verify_strict"]["route"] = call_route()
+    if auto:
+        gaps["single"] = _timed_gap(call, min(reps, 200), 1000)
     # the C3 QC handed over as its bincode wire bytes (hsv_qc_verify_bincode:
     # parse + base64 keys + qc.digest() on the host, verification on the GPU)
     w = synth.qc_votes(1000, seed=1000)
@@ -380,7 +384,18 @@ def qc_latency(reps, auto=True):
     settle(call)
     assert call() == 1
     res["n1000_votes667_bincode"] = dict(_timed_lib(call, reps), bytes=len(buf))
+    if gaps:
+        res["idle_gap_1ms"] = gaps
     return res
+
+
+def call_route():
+    """Which path answered the calling thread's last latency call: 'resident'
+    (the resident service: the call leased no staging slot, HSV_MARK_SLOT not
+    passed, but staged its request) or 'launch'."""
+    from hsverify import _testing
+    m = _testing.host_call_marks()
+    return "resident" if (len(m) >= 3 and m[1] < 0 <= m[2]) else "launch"
 
 
 def tc_latency(reps, auto=True):
@@ -464,16 +479,18 @@ def tc_dropin_sequential(reps):
         if was:
             gc.enable()
     out = _p(ts)
-    out.update(votes=w.n, call_p50_ms=float(np.median(calls) * 1e3), call_p99_ms=float(np.percentile(calls, 99) * 1e3))
+    out.update(votes=w.n, call_p50_ms=float(np.median(calls) * 1e3), call_p99_ms=float(np.percentile(calls, 99) * 1e3),
+               route=call_route())
     return out
 
 
-def resident_child(reps, tc_reps):
-    """Runs in a child process with HSV_QC_RESIDENT=1 (the library reads it
-    once per process): one cached-key verify_strict and a C1 QC through the
-    resident latency service, the sequential TC loop through it, and the dalek
-    port's single verify_strict on one host core of the same process."""
-    from hsverify import _lib, _testing, synth
+def launched_child(reps, tc_reps):
+    """Runs in a child process with HSV_QC_RESIDENT=0 (the library reads it
+    once per process): one cached-key verify_strict, a C1 QC and the
+    sequential TC loop launched per call, as without the resident service,
+    and the dalek port's single verify_strict on one host core of the same
+    process."""
+    from hsverify import _lib, synth
     lib = _lib.load()
     lib.hsv_set_auto_committee(1)
     w = synth.qc_votes(4, seed=4)
@@ -485,8 +502,7 @@ def resident_child(reps, tc_reps):
     call = lambda: lib.hsv_verify_strict(d0, pk0, sig0)
     assert call() == 1
     res = {"single_verify_strict": _timed_lib(call, reps)}
-    marks = _testing.host_call_marks()
-    res["answered_by_service"] = bool(marks[1] < 0 <= marks[2])   # no slot lease: the service answered
+    res["single_verify_strict"]["route"] = call_route()
     call = lambda: lib.hsv_verify_batch_packed(d0, packed, w.n)
     assert call() == 1
     res["n4_votes3"] = _timed_lib(call, reps)
@@ -499,10 +515,10 @@ def resident_child(reps, tc_reps):
     return res
 
 
-def resident_leg(reps, tc_reps):
-    """resident_child in a fresh process (HSV_QC_RESIDENT=1); its JSON, or the error."""
-    env = dict(os.environ, HSV_QC_RESIDENT="1")
-    cmd = [sys.executable, os.path.abspath(__file__), "--resident-child", "--qc-reps", str(reps),
+def launched_leg(reps, tc_reps):
+    """launched_child in a fresh process (HSV_QC_RESIDENT=0); its JSON, or the error."""
+    env = dict(os.environ, HSV_QC_RESIDENT="0")
+    cmd = [sys.executable, os.path.abspath(__file__), "--launched-child", "--qc-reps", str(reps),
            "--tc-seq-reps", str(tc_reps)]
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
@@ -785,7 +801,8 @@ def compact(out):
                                     "cpu_p50": cpu("n1000_votes667_corrupt5pct_p50_ms")}
         lat["qc_c3_bincode"] = {"gpu": _pp(ql["n1000_votes667_bincode"], True)}
         lat["verify_strict_single"] = {"gpu": _pp(ql["single_verify_strict"], True),
-                                       "cpu_p50": cpu("single_verify_strict_p50_ms")}
+                                       "cpu_p50": cpu("single_verify_strict_p50_ms"),
+                                       "route": ql["single_verify_strict"].get("route")}
         if qg:
             lat["cold_cache_off"] = {"c1": _pp(qg["n4_votes3"]), "c2": _pp(qg["n100_votes67"]),
                                      "c3": _pp(qg["n1000_votes667"]), "single": _pp(qg["single_verify_strict"])}
@@ -794,26 +811,26 @@ def compact(out):
                                            "cpu_p50": cpu("tc_n1000_votes667_clean_p50_ms")}
             lat["tc_c3_corrupt5pct_bincode"] = {"gpu": _pp(tl["n1000_votes667_corrupt5pct_bincode"], True),
                                                 "cpu_p50": cpu("tc_n1000_votes667_corrupt5pct_p50_ms")}
-        rs = out.get("resident", {})
-        if "single_verify_strict" in rs:
-            lat["resident_service"] = {
-                "verify_strict_single": _pp(rs["single_verify_strict"], True),
-                "qc_c1_3votes": _pp(rs["n4_votes3"], True),
-                "tc_c3_dropin_sequential": _pp(rs["tc_dropin_sequential"]),
-                "cpu_p50_same_process": _r(rs["cpu_port_single_verify_strict_p50_ms"]),
-                "answered_by_service": rs["answered_by_service"],
-                "what": "HSV_QC_RESIDENT=1 child process: requests to a resident block, no launch"}
-        elif rs:
-            lat["resident_service"] = {"error": str(rs.get("error"))[:200]}
         seq = out.get("tc_dropin_sequential")
         if seq:
             lat["tc_c3_dropin_sequential"] = {"gpu": _pp(seq), "gpu_call_p50": _r(seq["call_p50_ms"]),
-                                              "cpu_p50": cpu("tc_n1000_votes667_clean_p50_ms"),
+                                              "cpu_p50": cpu("tc_n1000_votes667_clean_p50_ms"), "route": seq.get("route"),
                                               "what": "667 sequential verify_strict calls, as TC::verify"}
+        rs = out.get("launched", {})
+        if "single_verify_strict" in rs:
+            lat["launched_service_off"] = {
+                "verify_strict_single": _pp(rs["single_verify_strict"], True),
+                "qc_c1_3votes": _pp(rs["n4_votes3"], True),
+                "tc_c3_dropin_sequential": _pp(rs["tc_dropin_sequential"]),
+                "single_gap_1ms": _r(rs.get("single_verify_strict_gap_1ms", {}).get("p50_ms")),
+                "cpu_p50_same_process": _r(rs["cpu_port_single_verify_strict_p50_ms"]),
+                "what": "HSV_QC_RESIDENT=0 child process: one launch per call"}
+        elif rs:
+            lat["launched_service_off"] = {"error": str(rs.get("error"))[:200]}
         gq = (out.get("qc_latency") or {}).get("idle_gap_1ms")
         if gq:
             lat["idle_gap_1ms"] = {"c1": _r(gq["n4_votes3"]["p50_ms"]), "c3": _r(gq["n1000_votes667"]["p50_ms"]),
-                                   "resident_single": _r(rs.get("single_verify_strict_gap_1ms", {}).get("p50_ms")),
+                                   "single": _r(gq.get("single", {}).get("p50_ms")),
                                    "what": "p50 with 1 ms of host idle before each call (consensus pacing)"}
         cc = out.get("committee_cache", {})
         if cc:
@@ -861,8 +878,8 @@ def parse_args(argv=None):
                     help="file for the full record (every rep's phases, tails, probes); stdout gets the compact line")
     ap.add_argument("--tc-seq-reps", type=int, default=30,
                     help="repetitions of the 667-call sequential TC loop (tc_dropin_sequential)")
-    ap.add_argument("--resident-child", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--no-resident", action="store_true", help="skip the resident-service child leg")
+    ap.add_argument("--launched-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-launched", action="store_true", help="skip the service-off (launched) child leg")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only: launcher, shards, timing and gather without a GPU or verification")
     return ap.parse_args(argv)
@@ -925,8 +942,8 @@ def dry_run(a, world, rank, dist):
 
 def main():
     a = parse_args()
-    if a.resident_child:  # bench.py's own child (resident_leg): no ranks, one JSON line
-        print(json.dumps(resident_child(a.qc_reps, a.tc_seq_reps)), flush=True)
+    if a.launched_child:  # bench.py's own child (launched_leg): no ranks, one JSON line
+        print(json.dumps(launched_child(a.qc_reps, a.tc_seq_reps)), flush=True)
         return
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and a.gpus is not None and a.gpus > 1:
@@ -1126,8 +1143,8 @@ def main():
         out["qc_latency_generic"] = qc_latency(a.qc_reps, auto=False)
         out["tc_latency"] = tc_latency(a.qc_reps, auto=True)
         out["tc_dropin_sequential"] = tc_dropin_sequential(a.tc_seq_reps)
-        if not a.no_resident:
-            out["resident"] = resident_leg(a.qc_reps, a.tc_seq_reps)
+        if not a.no_launched:
+            out["launched"] = launched_leg(a.qc_reps, a.tc_seq_reps)
         _lib.load().hsv_set_auto_committee(1)
         out["committee_cache"] = committee_bench(a.qc_reps, dev)
         # two streams: the record kernels (message hash + prepass, 2.3x the C4

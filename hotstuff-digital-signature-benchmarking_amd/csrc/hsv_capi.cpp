@@ -208,7 +208,8 @@ int slot_prepare(Slot &s, size_t dev_bytes, size_t host_bytes) {
     e = pipe_stream_create(&s.stream);
     if (e != hipSuccess) return hip_fail("hipStreamCreate", e);
   }
-  if ((dev_bytes > s.d_cap && s.d_buf) || (host_bytes > s.h_cap && s.h_buf)) resident_quiesce();
+  std::unique_ptr<ResidentPause> pause;  // hipFree / hipHostFree wait for every grid on the device
+  if ((dev_bytes > s.d_cap && s.d_buf) || (host_bytes > s.h_cap && s.h_buf)) pause.reset(new ResidentPause());
   if (dev_bytes > s.d_cap) {
     if (s.d_buf) (void)hipFree(s.d_buf);
     s.d_buf = nullptr;
@@ -236,7 +237,7 @@ int slot_prepare(Slot &s, size_t dev_bytes, size_t host_bytes) {
 int slot_sync_region(Slot &s, size_t bytes) {
   if (bytes <= s.h_sync_cap) return HSV_OK;
   if (s.h_sync) {
-    resident_quiesce();
+    ResidentPause pause;  // hipHostFree waits for every grid on the device
     (void)hipHostFree(s.h_sync);
   }
   s.h_sync = s.h_sync_dev = nullptr;
@@ -247,6 +248,7 @@ int slot_sync_region(Slot &s, size_t bytes) {
   void *hd = nullptr;
   e = hipHostGetDevicePointer(&hd, s.h_sync, 0);
   if (e != hipSuccess || !hd) {
+    ResidentPause pause;
     (void)hipHostFree(s.h_sync);
     s.h_sync = nullptr;
     return hip_fail("hipHostGetDevicePointer (coherent sync region)", e);
@@ -303,6 +305,7 @@ int ensure_btable(DevCtx &c) {
   int rc = e == hipSuccess ? HSV_OK : hip_fail("allocating the B comb table", e);
   if (rc == HSV_OK)
     rc = build_on_private_stream([&](hipStream_t st) { return hsv_launch_comb_build(d_enc, 1, 0, d_tab, d_tmp, nullptr, st); });
+  ResidentPause pause;  // hipFree waits for every grid on the device
   if (d_enc) (void)hipFree(d_enc);
   if (d_tmp) (void)hipFree(d_tmp);
   if (rc != HSV_OK) {
@@ -321,6 +324,7 @@ int ensure_btable16(DevCtx &c) {
   if (e == hipSuccess) e = hipMalloc(&d_tmp, hsv_comb16_tmp_bytes());
   int rc = e == hipSuccess ? HSV_OK : hip_fail("allocating the wide B comb table", e);
   if (rc == HSV_OK) rc = build_on_private_stream([&](hipStream_t st) { return hsv_launch_comb16_build(d_tab, d_tmp, st); });
+  ResidentPause pause;  // hipFree waits for every grid on the device
   if (d_tmp) (void)hipFree(d_tmp);
   if (rc != HSV_OK) {
     if (d_tab) (void)hipFree(d_tab);
@@ -515,7 +519,10 @@ int device_fault_words(DevCtx &c, uint32_t **out) {
     hipError_t e = hipMalloc(&p, 256);
     if (e == hipSuccess) e = hipMemset(p, 0, 256);
     if (e != hipSuccess) {
-      if (p) (void)hipFree(p);
+      if (p) {
+        ResidentPause pause;
+        (void)hipFree(p);
+      }
       return hip_fail("allocating the device self-check words", e);
     }
     c.d_fault = p;
@@ -601,7 +608,8 @@ int slot_workspaces(Slot &s, size_t need, int count) {
   if (need <= s.ws_cap && count <= have) return HSV_OK;
   const size_t cap = std::max(need, s.ws_cap);
   const int n = std::max(count, have);
-  if (have) resident_quiesce();
+  std::unique_ptr<ResidentPause> pause;  // hipFree waits for every grid on the device
+  if (have) pause.reset(new ResidentPause());
   for (uint8_t *&w : s.d_ws) {
     if (w) (void)hipFree(w);
     w = nullptr;
@@ -953,6 +961,7 @@ int hsvi_set_pipe_nocopy(int on) { return hsvh::g_pipe_nocopy.exchange(on != 0) 
 // drained, the device idle -- before it frees the tables those calls read.
 void hsv_shutdown(void) {
   auto_committee_shutdown();
+  ResidentPause pause;  // no relaunch while the buffers go
   Global &g = G();
   std::lock_guard<std::mutex> lk(g.mu);
   for (DevCtx *c : g.ctx) {

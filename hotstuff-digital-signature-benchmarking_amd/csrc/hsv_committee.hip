@@ -609,6 +609,10 @@ extern "C" hipError_t hsv_launch_comb16_build(uint32_t *table, uint32_t *tmp, hi
 // device over `rows` host inputs of 16 words; 0 or a hipError_t.
 extern "C" int hsvi_lanesplit_check(const uint32_t *in, uint32_t rows, uint32_t *out) {
   if (rows == 0) return 0;
+  struct Pause {  // a device-wide wait and frees below
+    Pause() { hsvi_resident_pause(1); }
+    ~Pause() { hsvi_resident_pause(0); }
+  } pause;
   uint32_t *d_in = nullptr, *d_out = nullptr;
   hipError_t e = hipMalloc(&d_in, (size_t)rows * 64);
   if (e == hipSuccess) e = hipMalloc(&d_out, (size_t)rows * 4);

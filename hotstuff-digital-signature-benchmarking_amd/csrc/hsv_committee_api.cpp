@@ -130,25 +130,28 @@ struct CommitteeDev {
   const uint32_t *const *d_tabptr = nullptr;
 };
 
-// ---- resident latency service (HSV_QC_RESIDENT=1, opt-in) --------------------------
+// ---- resident latency service (on by default; HSV_QC_RESIDENT=0 turns it off) ------
 // One block of hsv_comb_resident_kernel stays on a CU of the home device and
 // answers requests of at most hsv_comb_resident_votes() votes posted in
 // coherent pinned memory (QcResidentReq): 2.2 us round trip for a block of its
 // shape against 5.8 us for a launch with marker sync
-// (profiles/r05a_aql_latency.txt).  It holds that CU while it runs, hence
-// opt-in.  The kernel leaves on the stop word (hsv_shutdown, an atexit
-// handler registered at the first start, and resident_quiesce() before the
-// library frees device or pinned memory: on ROCm hipFree / hipHostFree wait
-// for every grid on the device, the resident one included) or after
-// kResidentIdle without a request; the next request relaunches it.  A request
-// unanswered within kResidentWait ends the service for the process, and the
-// call takes the launch path, so the service can cost latency but never a
-// verdict.  An application that synchronises the whole device
-// (hipDeviceSynchronize, torch.cuda.synchronize) waits for the idle exit, up to
-// kResidentIdle after the last request.
-constexpr uint64_t kResidentIdleTicks = 100000000ull;  // 1 s of the 100 MHz clock
+// (profiles/r05a_aql_latency.txt), so one verify_strict of a cached key costs
+// 0.034 ms instead of 0.039 ms launched (0.037 ms for the dalek port on one
+// host core).  It holds that one CU while it runs.  The kernel leaves on the
+// stop word -- hsv_shutdown, hsv_set_resident_service(0), an atexit handler,
+// and every ResidentPause: the library pauses the service around each of its
+// own hipFree / hipHostFree (on ROCm they wait for every grid on the device)
+// and before each launch of the persistent point pass, whose grid is sized to
+// fill every CU -- or after the idle time (HSV_QC_RESIDENT_IDLE_MS, default
+// 50 ms) without a request; the next request relaunches it.  A request
+// unanswered within kResidentWait, or a relaunch that does not start, takes
+// the call to the launch path and keeps the service off for a backoff, so the
+// service can cost latency but never a verdict.  An application that
+// synchronises the whole device (hipDeviceSynchronize, torch.cuda.synchronize)
+// waits at most the idle time after the last request.
 constexpr auto kResidentWait = std::chrono::milliseconds(50);
 constexpr int kResidentUnavailable = 1;
+constexpr int kResidentMaxFailures = 4;  // then the service stays off for the process
 
 struct ResidentQc {
   std::mutex mu;
@@ -157,8 +160,14 @@ struct ResidentQc {
   QcResidentReq *d = nullptr;  // its device address
   hipStream_t stream = nullptr;
   uint32_t seq = 0;
-  bool broken = false;
+  int failures = 0;                                   // relaunch / answer failures so far
+  std::chrono::steady_clock::time_point retry_after;  // backoff after a failure
+  int paused = 0;   // live ResidentPause scopes: no request, no relaunch
+  // 1 on, 0 off (hsv_set_resident_service); -1: HSV_QC_RESIDENT on first use.
+  // Read without the lock: a call that finds it on and the lock busy launches.
+  std::atomic<int> mode{-1};
   bool atexit_registered = false;
+  std::atomic<bool> started{false};   // its block has run in this process (hsvi_resident_started)
   uint64_t posted = 0, answered = 0;  // requests posted / answered (hsvi_resident_counts)
 };
 
@@ -167,12 +176,25 @@ ResidentQc &RQ() {
   return r;
 }
 
-bool resident_enabled() {
-  static const bool on = [] {
+bool resident_on(ResidentQc &r) {
+  int m = r.mode.load(std::memory_order_relaxed);
+  if (m < 0) {
     const char *v = std::getenv("HSV_QC_RESIDENT");
-    return v && v[0] == '1';
+    int want = (v && v[0] == '0') ? 0 : 1;
+    r.mode.compare_exchange_strong(m, want);  // a concurrent hsv_set_resident_service wins
+    m = r.mode.load(std::memory_order_relaxed);
+  }
+  return m == 1;
+}
+
+uint64_t resident_idle_ticks() {
+  static const uint64_t t = [] {
+    long ms = 50;
+    if (const char *v = std::getenv("HSV_QC_RESIDENT_IDLE_MS")) ms = std::atol(v);
+    ms = std::max(1L, std::min(ms, 10000L));
+    return (uint64_t)ms * 100000ull;  // the kernel's 100 MHz clock
   }();
-  return on;
+  return t;
 }
 
 // stop the kernel and wait for its grid (mu held)
@@ -184,6 +206,13 @@ void resident_stop_locked(ResidentQc &r) {
   __atomic_store_n(&r.h->stop, 0u, __ATOMIC_RELEASE);
 }
 
+// a failed relaunch or an unanswered request (mu held): off for a growing
+// backoff, for good after kResidentMaxFailures
+void resident_failed_locked(ResidentQc &r) {
+  ++r.failures;
+  r.retry_after = std::chrono::steady_clock::now() + std::chrono::milliseconds(250 << std::min(r.failures, 6));
+}
+
 void resident_atexit() {
   ResidentQc &r = RQ();
   std::lock_guard<std::mutex> lk(r.mu);
@@ -192,7 +221,8 @@ void resident_atexit() {
 
 // the kernel running on `device` (mu held): HSV_OK or kResidentUnavailable
 int resident_ensure_locked(ResidentQc &r, int device) {
-  if (r.broken) return kResidentUnavailable;
+  if (r.paused || !resident_on(r) || r.failures >= kResidentMaxFailures) return kResidentUnavailable;
+  if (r.failures && std::chrono::steady_clock::now() < r.retry_after) return kResidentUnavailable;
   if (r.h && r.device != device) return kResidentUnavailable;  // one device per process
   if (!r.h) {
     void *h = nullptr, *d = nullptr;
@@ -200,13 +230,13 @@ int resident_ensure_locked(ResidentQc &r, int device) {
     // after it started (a non-coherent area let it read a stale request
     // header and fault, profiles/r04res_pytest_sub2.txt)
     if (hipHostMalloc(&h, sizeof(QcResidentReq), hipHostMallocCoherent) != hipSuccess) {
-      r.broken = true;
+      r.failures = kResidentMaxFailures;
       return kResidentUnavailable;
     }
     if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d ||
         hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking) != hipSuccess) {
-      (void)hipHostFree(h);
-      r.broken = true;
+      (void)hipHostFree(h);  // the kernel never ran: nothing to wait for
+      r.failures = kResidentMaxFailures;
       return kResidentUnavailable;
     }
     std::memset(h, 0, sizeof(QcResidentReq));
@@ -216,22 +246,27 @@ int resident_ensure_locked(ResidentQc &r, int device) {
     r.seq = 0;
   }
   if (__atomic_load_n(&r.h->alive, __ATOMIC_ACQUIRE) == 1u) return HSV_OK;
-  // not running (first use, or it left after an idle second): relaunch
+  // not running (first use, or it left after its idle time): relaunch
   (void)hipStreamSynchronize(r.stream);  // the previous grid has fully ended
   __atomic_store_n(&r.h->stop, 0u, __ATOMIC_RELEASE);
-  if (hsv_launch_comb_resident(r.d, kResidentIdleTicks, r.stream) != hipSuccess) {
-    r.broken = true;
+  if (hsv_launch_comb_resident(r.d, resident_idle_ticks(), r.stream) != hipSuccess) {
+    resident_failed_locked(r);
     return kResidentUnavailable;
   }
+  r.started.store(true);
   if (!r.atexit_registered) {  // after HIP's own: runs before the runtime tears down
     std::atexit(resident_atexit);
     r.atexit_registered = true;
   }
+  // The block announces itself once it holds a CU.  A device busy with other
+  // grids may not give it one soon: then this call launches instead, the
+  // stop word makes the block leave as soon as it starts, and the service
+  // backs off.
   const auto t0 = std::chrono::steady_clock::now();
   while (__atomic_load_n(&r.h->alive, __ATOMIC_ACQUIRE) != 1u)
-    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+    if (std::chrono::steady_clock::now() - t0 > kResidentWait) {
       resident_stop_locked(r);
-      r.broken = true;
+      resident_failed_locked(r);
       return kResidentUnavailable;
     }
   return HSV_OK;
@@ -243,7 +278,10 @@ int resident_ensure_locked(ResidentQc &r, int device) {
 int resident_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t *sig, size_t sig_stride,
                  const uint8_t *msg, size_t msg_stride, size_t m, uint8_t *flags_out, const uint32_t *btable) {
   ResidentQc &r = RQ();
-  std::lock_guard<std::mutex> lk(r.mu);
+  // one request at a time: a concurrent caller launches instead of queueing
+  // behind this one (the launch path takes 0.039 ms, a queue could take more)
+  std::unique_lock<std::mutex> lk(r.mu, std::try_to_lock);
+  if (!lk.owns_lock()) return kResidentUnavailable;
   if (resident_ensure_locked(r, cd.device) != HSV_OK) return kResidentUnavailable;
   QcResidentReq &q = *r.h;
   QcResidentBody b{};  // the payload, chunked into the request area at each post
@@ -266,17 +304,26 @@ int resident_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t 
   uint32_t words[kResidentChunks * 3];
   std::memcpy(words, &b, sizeof(b));
   call_mark(HSV_MARK_STAGED);
-  // Each chunk's payload words, then its seq (a release store: the compiler
-  // keeps the order, and x86 makes stores visible in program order), so a
-  // chunk read with the new seq holds the new payload.
+  // Each chunk {seq, three payload words} in ONE aligned 16-byte store, the
+  // width of the kernel's read of it: a read can then never pair a new seq
+  // with an older payload word (16-byte aligned SSE stores are single
+  // accesses on x86-64 processors with AVX).  The compiler fence keeps the
+  // chunks' stores in program order; x86 makes them visible in that order.
   auto post = [&](uint32_t sq) {
+    std::atomic_signal_fence(std::memory_order_release);
     for (int c = 0; c < kResidentChunks; ++c) {
-      QcResidentChunk &ch = q.chunk[c];
-      ch.w[0] = words[3 * c];
-      ch.w[1] = words[3 * c + 1];
-      ch.w[2] = words[3 * c + 2];
-      __atomic_store_n(&ch.seq, sq, __ATOMIC_RELEASE);
+      QcResidentChunk *ch = &q.chunk[c];
+#if defined(__SSE2__)
+      _mm_store_si128(reinterpret_cast<__m128i *>(ch),
+                      _mm_set_epi32((int)words[3 * c + 2], (int)words[3 * c + 1], (int)words[3 * c], (int)sq));
+#else
+      ch->w[0] = words[3 * c];
+      ch->w[1] = words[3 * c + 1];
+      ch->w[2] = words[3 * c + 2];
+      __atomic_store_n(&ch->seq, sq, __ATOMIC_RELEASE);
+#endif
     }
+    std::atomic_signal_fence(std::memory_order_release);
   };
   // One retry: the kernel may leave on its idle timer just as a request is
   // posted (it read the doorbell before the store); then it is relaunched
@@ -302,10 +349,10 @@ int resident_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t 
     if (attempt == 0 && __atomic_load_n(&q.alive, __ATOMIC_ACQUIRE) == 0u &&
         resident_ensure_locked(r, cd.device) == HSV_OK)
       continue;
-    // no answer from a running kernel: end the service for this process,
-    // the launch path answers
+    // no answer from a running kernel: stop it and back off, the launch
+    // path answers
     resident_stop_locked(r);
-    r.broken = true;
+    resident_failed_locked(r);
     return kResidentUnavailable;
   }
   ++r.answered;
@@ -321,17 +368,32 @@ int resident_run(const CommitteeDev &cd, const uint32_t *key_idx, const uint8_t 
   return HSV_OK;
 }
 
+bool resident_enabled() { return resident_on(RQ()); }
+
 }  // namespace
 
-// Stop the resident kernel before the library frees device or pinned memory
-// (hipFree / hipHostFree wait for every grid on the device); the next request
-// relaunches it.  A no-op when the service never ran.
-void resident_quiesce() {
+// A scope in which the resident kernel does not run: the constructor stops it
+// (when it runs) and, until the destructor, no request is posted and no
+// relaunch happens -- a concurrent small call takes the launch path.  Around
+// every hipFree / hipHostFree of the library (they wait for every grid on the
+// device, and would otherwise wait for the service's idle exit, or forever
+// under steady requests) and before each launch of the persistent point pass.
+ResidentPause::ResidentPause() {
   ResidentQc &r = RQ();
-  if (!r.h) return;  // unlocked peek: the service is only ever started, never unset
   std::lock_guard<std::mutex> lk(r.mu);
-  if (__atomic_load_n(&r.h->alive, __ATOMIC_ACQUIRE) == 1u) resident_stop_locked(r);
+  ++r.paused;
+  if (r.h && __atomic_load_n(&r.h->alive, __ATOMIC_ACQUIRE) == 1u) resident_stop_locked(r);
 }
+
+ResidentPause::~ResidentPause() {
+  ResidentQc &r = RQ();
+  std::lock_guard<std::mutex> lk(r.mu);
+  --r.paused;
+}
+
+// Stop the resident kernel now, without keeping it paused (the next request
+// relaunches it).  A no-op when it does not run.
+void resident_quiesce() { ResidentPause p; }
 
 void resident_counts(uint64_t *posted, uint64_t *answered) {
   ResidentQc &r = RQ();
@@ -340,19 +402,52 @@ void resident_counts(uint64_t *posted, uint64_t *answered) {
   if (answered) *answered = r.answered;
 }
 
+// hsv_set_resident_service: 1 on, 0 off (the kernel stops now); the previous mode
+int resident_set_mode(int on) {
+  ResidentQc &r = RQ();
+  std::lock_guard<std::mutex> lk(r.mu);
+  const int prev = resident_on(r) ? 1 : 0;
+  r.mode.store(on ? 1 : 0);
+  if (!on) resident_stop_locked(r);
+  if (on) r.failures = 0;  // an explicit re-enable clears the backoff
+  return prev;
+}
+
+}  // namespace hsvh
+
+extern "C" void hsvi_resident_pause(int on) {
+  using namespace hsvh;
+  ResidentQc &r = RQ();
+  std::lock_guard<std::mutex> lk(r.mu);
+  if (on) {
+    ++r.paused;
+    if (r.h && __atomic_load_n(&r.h->alive, __ATOMIC_ACQUIRE) == 1u) resident_stop_locked(r);
+  } else if (r.paused > 0) {
+    --r.paused;
+  }
+}
+
+extern "C" int hsvi_resident_started(void) {
+  hsvh::ResidentQc &r = hsvh::RQ();
+  return r.started.load() && hsvh::resident_on(r) ? 1 : 0;
+}
+
+namespace hsvh {
+
 // Test hook: one resident request whose header claims m votes (0 or above
 // the limit: the kernel must refuse it with HSV_ERR_DEVICE_FAULT, never read
 // through it); needs the automatic cache's committee (nkeys, tables).
 int resident_post_bad(uint32_t m) {
-  if (!resident_enabled()) return fail(HSV_ERR_INVALID_ARG, "HSV_QC_RESIDENT is off");
+  if (!resident_enabled()) return fail(HSV_ERR_INVALID_ARG, "the resident service is off");
   int rc = ensure_init();
   if (rc != HSV_OK) return rc;
   DevCtx &c = ctx(home_device());
   DeviceGuard guard(c.device);
   rc = ensure_btable(c);
   if (rc != HSV_OK) return rc;
-  const uint32_t idx[1] = {0};
-  uint8_t sig[64] = {0}, msg[32] = {0}, flags[16];
+  // resident_run copies min(m, kResidentVotes) votes: arrays of that size
+  const uint32_t idx[kResidentVotes] = {};
+  uint8_t sig[kResidentVotes * 64] = {}, msg[32] = {}, flags[16];
   CommitteeDev cd;
   cd.device = c.device;
   cd.n = 1;
@@ -555,7 +650,10 @@ int hsv_committee_create(const uint8_t *pks, size_t n, hsv_committee **out) {
       e = build_tables(cm->d_pks, (uint32_t)n, ptrs.data(), cm->d_kflags, d_tmp, std::min<uint32_t>((uint32_t)n, 1024), st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (st) (void)hipStreamDestroy(st);
-    if (d_tmp) (void)hipFree(d_tmp);
+    if (d_tmp) {
+      ResidentPause pause;  // hipFree waits for every grid on the device
+      (void)hipFree(d_tmp);
+    }
     if (e != hipSuccess) {
       hsv_committee_destroy(cm.release());
       return hip_fail("building committee tables", e);
@@ -570,7 +668,7 @@ int hsv_committee_create(const uint8_t *pks, size_t n, hsv_committee **out) {
 
 void hsv_committee_destroy(hsv_committee *cm) {
   if (!cm) return;
-  resident_quiesce();
+  ResidentPause pause;  // hipFree waits for every grid on the device
   DeviceGuard guard(cm->dev.device);
   if (cm->d_pks) (void)hipFree(cm->d_pks);
   if (cm->d_kflags) (void)hipFree(cm->d_kflags);
@@ -666,6 +764,7 @@ namespace {
 constexpr uint32_t kAutoMaxKeys = 8192;      // 3 GiB of tables at most
 constexpr uint32_t kBlockKeys = 64;          // tables allocated 64 keys (24 MiB) at a time
 constexpr size_t kCommitteeTryMax = 4096;    // hsv_verify / verify_strict batches that try the cache
+constexpr size_t kLearnStrictMax = 16;       // ... and that teach it their keys (votes, single verifies)
 constexpr uint32_t kResetAfterMisses = 256;  // missing batches against a full cache before a relearn
 constexpr int kMaxBuildFailures = 3;         // then the cache stays off until hsv_set_auto_committee(1)
 
@@ -681,7 +780,7 @@ struct AutoStore {  // append-only device storage, freed with the last view usin
   // pointer into it stays valid as later builds append)
   std::unique_ptr<uint8_t[]> h_pks{new uint8_t[(size_t)kAutoMaxKeys * 32]};
   ~AutoStore() {
-    resident_quiesce();
+    ResidentPause pause;  // hipFree waits for every grid on the device
     DeviceGuard guard(device);
     if (stream) (void)hipStreamDestroy(stream);
     for (uint32_t *b : blocks) (void)hipFree(b);
@@ -936,11 +1035,15 @@ void auto_reset(bool enable) {
 int auto_committee_try(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, size_t msg_stride, size_t n,
                        uint8_t *flags_out) {
   // only the latency range (a vote, a TC); large batches of fresh keys would
-  // pay a hash lookup per item for nothing
+  // pay a hash lookup per item for nothing.  Calls of a few signatures --
+  // Vote::verify on every incoming vote (consensus/src/core.rs:240), the
+  // proposer's Block::verify -- count their keys as sightings too, so a
+  // committee whose votes arrive before its first QCs is learnt from them;
+  // larger strict batches only read the cache (their keys need not recur).
   if (n > kCommitteeTryMax || !auto_enabled()) return 1;
   thread_local std::vector<uint32_t> idx;  // per-call scratch kept by the thread
   idx.resize(n);
-  std::shared_ptr<const AutoView> v = auto_lookup(pk, 32, n, idx.data(), false);
+  std::shared_ptr<const AutoView> v = auto_lookup(pk, 32, n, idx.data(), n <= kLearnStrictMax);
   call_mark(HSV_MARK_LOOKUP);
   if (!v || v->dev.device != home_device()) return 1;
   return auto_run(v, idx.data(), sig, 64, msg, msg_stride, n, flags_out);
@@ -996,6 +1099,8 @@ int hsv_verify_batch_packed(const uint8_t digest[32], const uint8_t *votes, size
   rc = run_host(votes, 96, votes + 32, 96, digest, 0, n, flags.data());
   return rc != HSV_OK ? rc : batch_verdict(flags.data(), n);
 }
+
+int hsv_set_resident_service(int mode) { return resident_set_mode(mode != 0); }
 
 int hsv_set_auto_committee(int enable) {
   auto_reset(enable != 0);

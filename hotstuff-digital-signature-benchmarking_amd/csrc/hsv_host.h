@@ -218,10 +218,22 @@ int auto_committee_corrupt_tables();  // zero the cached tables of the automatic
 int auto_committee_try(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, size_t msg_stride, size_t n,
                        uint8_t *flags_out);
 void auto_committee_shutdown();
-// resident latency service (HSV_QC_RESIDENT=1, hsv_committee_api.cpp)
-void resident_quiesce();  // stop its kernel before a hipFree / hipHostFree
+// resident latency service (on by default, hsv_committee_api.cpp)
+// A scope in which its kernel does not run: stopped at construction, and no
+// request or relaunch until destruction (small calls launch meanwhile).  Held
+// around every hipFree / hipHostFree of the library -- they wait for every
+// grid on the device -- and around device-wide waits.
+class ResidentPause {
+ public:
+  ResidentPause();
+  ~ResidentPause();
+  ResidentPause(const ResidentPause &) = delete;
+  ResidentPause &operator=(const ResidentPause &) = delete;
+};
+void resident_quiesce();  // stop its kernel now (the next request relaunches it)
 void resident_counts(uint64_t *posted, uint64_t *answered);
 int resident_post_bad(uint32_t m);  // test hook: a request the kernel must refuse
+int resident_set_mode(int on);      // hsv_set_resident_service
 
 // The generic host-buffer path (hsv_capi.cpp): records at the given strides.
 int run_host(const uint8_t *pk, size_t pk_stride, const uint8_t *sig, size_t sig_stride, const uint8_t *msg,

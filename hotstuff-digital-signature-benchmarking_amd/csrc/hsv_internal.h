@@ -20,6 +20,15 @@ extern "C" {
 hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream);
 void hsv_ws_trim(void);  // hsv_shutdown: release the pools' free blocks
 
+// The resident latency service (hsv_committee_api.cpp) from the kernel
+// launchers: pause (on = 1) / resume (on = 0) it around a device-wide wait,
+// as hsvh::ResidentPause; hsvi_resident_started() is 1 once its block has run
+// in this process with the service on -- the persistent point pass then
+// leaves one CU's worth of blocks out of its grid, so every block of that
+// grid finds a place while the resident block holds its CU.
+void hsvi_resident_pause(int on);
+int hsvi_resident_started(void);
+
 // Everything declared here is internal: the library is built with
 // -fvisibility=hidden, so none of it is exported from libhsv.so (only the
 // HSV_API functions of include/hsv.h are).  The test and measurement hooks of

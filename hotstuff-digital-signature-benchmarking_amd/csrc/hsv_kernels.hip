@@ -951,6 +951,23 @@ extern "C" void hsv_ws_trim(void) {
   for (auto &kv : wp.pools) (void)hipMemPoolTrimTo(kv.second, 0);
 }
 
+// Free memory the pool keeps between calls (HSV_WS_POOL_KEEP_MB, default 4096
+// MiB; 0 returns every block at each synchronisation): a freed block is reused
+// only by later launches on the same stream, so an application that spreads
+// batches over many streams would otherwise keep one workspace per stream
+// (about 0.5 GB for a 2^20-item batch) out of its own allocator's reach.  Above
+// the threshold the pool hands idle blocks back to the driver whenever a
+// stream or event synchronisation observes their frees.
+static uint64_t ws_pool_keep_bytes() {
+  static const uint64_t b = [] {
+    long long mb = 4096;
+    if (const char *v = std::getenv("HSV_WS_POOL_KEEP_MB")) mb = std::atoll(v);
+    if (mb < 0) mb = 0;
+    return (uint64_t)mb << 20;
+  }();
+  return b;
+}
+
 extern "C" hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -969,7 +986,7 @@ extern "C" hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream) 
       props.location.id = dev;
       e = hipMemPoolCreate(&pool, &props);
       if (e != hipSuccess) return e;
-      uint64_t keep = UINT64_MAX;
+      uint64_t keep = ws_pool_keep_bytes();
       e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
       if (e != hipSuccess) return e;
       // A block is reused only on the stream that freed it (stream order
@@ -995,13 +1012,18 @@ extern "C" hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream) 
   }
   e = hipMallocFromPoolAsync(p, bytes, pool, stream);
   if (e == hipErrorOutOfMemory) {
-    // Blocks freed on other streams (streams since destroyed, or idle) are
-    // never reused here; when the device runs out, wait for every launch,
-    // hand the pool's idle blocks back to the driver and try once more (with
-    // the opt-in resident service alive, the sync waits for its idle exit).
+    // Blocks freed on other streams are never reused here.  When the device
+    // runs out: wait for the calling stream (its own frees complete), hand
+    // every idle block of the pool back to the driver -- blocks freed on
+    // idle or destroyed streams among them -- and try once more; otherwise
+    // the caller gets the out-of-memory error.  No device-wide wait: that
+    // would stall every stream of the application, and blocks still held by
+    // launches running on other streams stay theirs.
     (void)hipGetLastError();
-    if (hipDeviceSynchronize() == hipSuccess && hipMemPoolTrimTo(pool, 0) == hipSuccess)
+    hsvi_resident_pause(1);
+    if (hipStreamSynchronize(stream) == hipSuccess && hipMemPoolTrimTo(pool, 0) == hipSuccess)
       e = hipMallocFromPoolAsync(p, bytes, pool, stream);
+    hsvi_resident_pause(0);
     if (e == hipSuccess) (void)hipGetLastError();
   }
   return e;
@@ -1053,21 +1075,29 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
   static std::mutex mu;
-  static std::unordered_map<int, int> slots_per_dev;
-  int resident = 0;
+  static std::unordered_map<int, std::pair<int, int>> slots_per_dev;  // device -> (blocks per CU, CUs)
+  int bpc = 1, cus = 1;
   {
     std::lock_guard<std::mutex> lk(mu);
     auto it = slots_per_dev.find(dev);
     if (it == slots_per_dev.end()) {
-      int bpc = 0, cus = 0;
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kern, hsv::kBlock, 0);
+      int b = 0, c = 0;
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, hsv::kBlock, 0);
       if (e != hipSuccess) return e;
-      e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      e = hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
       if (e != hipSuccess) return e;
-      it = slots_per_dev.emplace(dev, std::max(1, bpc) * std::max(1, cus)).first;
+      it = slots_per_dev.emplace(dev, std::make_pair(std::max(1, b), std::max(1, c))).first;
     }
-    resident = it->second;
+    bpc = it->second.first;
+    cus = it->second.second;
   }
+  // A persistent grid must fit the device at once: its blocks leave when the
+  // work counter runs out, and a block still waiting for a place would hold
+  // the launch open.  Once the resident latency service has run in this
+  // process its block may sit on one CU (and a request from another thread
+  // may relaunch it while this grid is dispatched), so the grid then leaves
+  // one CU's worth of blocks out (1/256 of the slots).
+  const int resident = bpc * (hsvi_resident_started() && cus > 1 ? cus - 1 : cus);
   const uint32_t blocks_needed = (n + hsv::kBlock - 1) / hsv::kBlock;
   const uint32_t grid = std::min<uint32_t>(blocks_needed, (uint32_t)resident);
   const size_t ws_bytes = (size_t)grid * hsv::kBlock * hsv::vt_lane_uint4<WA>() * sizeof(uint4);
@@ -1379,6 +1409,11 @@ extern "C" int hsvi_variant_available(int variant) {
 }
 
 extern "C" double hsv_launch_mad_peak(int device_cus) {
+  // device-wide waits and a free below: the resident service is paused
+  struct Pause {
+    Pause() { hsvi_resident_pause(1); }
+    ~Pause() { hsvi_resident_pause(0); }
+  } pause;
   uint32_t *sink = nullptr;
   if (hipMalloc(&sink, 64) != hipSuccess) return -1.0;
   hipEvent_t e0, e1;

@@ -97,6 +97,7 @@ def _declare(lib):
         "hsv_qc_verify_bincode": (ctypes.c_int, [c_u8p, sz, ctypes.POINTER(ctypes.c_size_t), c_u8p]),
         "hsv_tc_verify_bincode": (ctypes.c_int, [c_u8p, sz, ctypes.POINTER(ctypes.c_size_t), c_u8p]),
         "hsv_set_auto_committee": (ctypes.c_int, [ctypes.c_int]),
+        "hsv_set_resident_service": (ctypes.c_int, [ctypes.c_int]),
         "hsv_auto_committee_size": (sz, []),
         "hsv_public_key": (ctypes.c_int, [c_u8p, c_u8p]),
         "hsv_sign": (ctypes.c_int, [c_u8p, c_u8p, sz, c_u8p]),

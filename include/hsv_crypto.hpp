@@ -105,15 +105,16 @@ inline std::atomic<uint64_t> &host_route_uses() {
 inline void set_host_route(HostRoute r) { host_route() = std::move(r); }
 
 // The single-verify routing default (the Rust
-// shim's hsv_single_on_host): a lone signature stays on the host unless
-// libhsv's resident latency service is on (HSV_QC_RESIDENT=1: one cached-key
-// verify_strict 0.0357 ms against 0.0371 ms for the dalek port on one host
-// core, profiles/r05d_resident_ab.txt; launched 0.0395 ms).  HSV_ROUTE_SINGLE
-// = "gpu" / "host" overrides it.
+// shim's hsv_single_on_host): a lone signature goes to libhsv, whose resident
+// latency service is on by default (one cached-key verify_strict 0.034 ms
+// against 0.036-0.037 ms for the dalek port on one host core,
+// profiles/r05ah_bench.json).  It stays on the host only when the service is
+// turned off (HSV_QC_RESIDENT=0: launched, 0.039 ms).  HSV_ROUTE_SINGLE =
+// "gpu" / "host" overrides it.
 inline bool single_verify_on_host_default() {
   if (const char *v = std::getenv("HSV_ROUTE_SINGLE")) return std::strcmp(v, "gpu") != 0;
   const char *r = std::getenv("HSV_QC_RESIDENT");
-  return !(r && r[0] == '1');
+  return r && r[0] == '0';
 }
 
 // ed25519::Error: opaque.

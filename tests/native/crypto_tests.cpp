@@ -202,8 +202,8 @@ static void install_oracle_fallback() {
 }
 
 // --route: QCs of at most 2 votes on the host verifier (the C oracle stands
-// in for dalek), larger QCs on libhsv; single verifies on the host unless the
-// resident latency service is on (crypto::single_verify_on_host_default)
+// in for dalek), larger QCs on libhsv; single verifies on libhsv unless its
+// resident latency service is off (crypto::single_verify_on_host_default)
 static void install_host_route() {
   HostRoute r;
   r.single = single_verify_on_host_default();

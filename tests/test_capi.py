@@ -51,9 +51,11 @@ def test_product_library_exports_exactly_the_header():
 
 # The environment variables the product library reads:
 # device binding, slot count, the automatic committee cache, the pack
-# threads, and the opt-in resident latency service.  Measurement switches
-# live in libhsv_test.so's hooks only.
-PRODUCT_ENV = {"HSV_DEVICE", "HSV_SLOTS", "HSV_AUTO_COMMITTEE", "HSV_PACK_THREADS", "HSV_QC_RESIDENT"}
+# threads, the resident latency service (on by default) and its idle time,
+# and the workspace pool's kept memory.  Measurement switches live in
+# libhsv_test.so's hooks only.
+PRODUCT_ENV = {"HSV_DEVICE", "HSV_SLOTS", "HSV_AUTO_COMMITTEE", "HSV_PACK_THREADS", "HSV_QC_RESIDENT",
+               "HSV_QC_RESIDENT_IDLE_MS", "HSV_WS_POOL_KEEP_MB"}
 
 
 def test_product_library_reads_only_the_documented_environment():

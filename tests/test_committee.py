@@ -261,8 +261,9 @@ with _testing.test_library() as lib:   # the hooks count the service's answers
     for m in (0, 5, 0xffffffff):
         assert lib.hsv_test_resident_post_bad(m) == ERR_FAULT, lib.hsv_last_error()
     assert resident_call(lambda: lib.hsv_verify_strict(d, pk, sg)) == 1   # the service goes on
-    # after an idle exit (1 s) the next request relaunches the kernel and is answered by it
-    time.sleep(1.5)
+    # after an idle exit (HSV_QC_RESIDENT_IDLE_MS, 50 ms) the next request relaunches the kernel
+    # and is answered by it
+    time.sleep(0.3)
     assert resident_call(lambda: lib.hsv_verify_strict(d, pk, sg)) == 1
     # corrupted cached tables under the service: its self-check fails, the view is dropped,
     # and the generic kernels answer with the right verdict
@@ -288,8 +289,8 @@ with _testing.test_library() as lib:   # the hooks count the service's answers
 
 
 def test_resident_service_in_a_child_process():
-    """The opt-in resident latency service (HSV_QC_RESIDENT=1, read once per
-    process), through libhsv_test.so's request counters: every 1-4-vote
+    """The resident latency service (HSV_QC_RESIDENT=1 here; on by default),
+    through libhsv_test.so's request counters: every 1-4-vote
     batch of cached keys is answered by the service (one request posted and
     answered per call), flag for flag against the oracle over the corruption
     kinds of synth.CORRUPTIONS, shared and per-vote digests; back-to-back
@@ -305,3 +306,90 @@ def test_resident_service_in_a_child_process():
     r = subprocess.run([sys.executable, "-c", RESIDENT_CHILD.format(tests=here, pkg=PKG)], capture_output=True,
                        text=True, timeout=300, env=dict(os.environ, HSV_QC_RESIDENT="1"))
     assert r.returncode == 0 and "resident ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
+
+
+DEFAULT_CHILD = r"""
+import ctypes, os, sys, threading, time
+sys.path.insert(0, {tests!r}); sys.path.insert(0, {pkg!r})
+import numpy as np
+from hsverify import _lib, _testing, synth, verifier
+with _testing.test_library() as lib:
+    def counts():
+        p, a = ctypes.c_uint64(), ctypes.c_uint64()
+        lib.hsv_test_resident_counts(ctypes.byref(p), ctypes.byref(a))
+        return p.value, a.value
+
+    lib.hsv_set_auto_committee(1)
+    w = synth.qc_votes(4, seed=91)
+    d, pk, sg = bytes(w.msg), bytes(w.pk[0]), bytes(w.sig[0])
+    # Vote::verify alone teaches the cache: two sightings of the key, then the background build
+    assert lib.hsv_verify_strict(d, pk, sg) == 1 and lib.hsv_verify_strict(d, pk, sg) == 1
+    assert lib.hsv_auto_committee_wait(30000) == 1
+    assert lib.hsv_auto_committee_size() >= 1, "single verifies did not teach the cache"
+    p0, a0 = counts()
+    assert lib.hsv_verify_strict(d, pk, sg) == 1
+    p1, a1 = counts()
+    expect_service = os.environ.get("HSV_QC_RESIDENT") != "0"
+    assert (p1 - p0, a1 - a0) == ((1, 1) if expect_service else (0, 0)), (p1 - p0, a1 - a0)
+    if not expect_service:
+        print("default ok (service off)")
+        sys.exit(0)
+    # hsv_set_resident_service(0): stopped at once, calls launch; (1): answered again
+    assert lib.hsv_set_resident_service(0) == 1
+    assert lib.hsv_verify_strict(d, pk, sg) == 1 and counts() == (p1, a1)
+    assert lib.hsv_set_resident_service(1) == 0
+    assert lib.hsv_verify_strict(d, pk, sg) == 1 and counts()[1] == a1 + 1
+    # Frees while another thread keeps the service busy (round-5 advice): committee create /
+    # destroy free device memory, and hipFree waits for every grid on the device; the pause
+    # keeps the service stopped until each free has returned, so they never wait for it.
+    s_bad = bytearray(sg); s_bad[40] ^= 1; s_bad = bytes(s_bad)
+    stop, errors, done = threading.Event(), [], [0]
+    def votes():
+        while not stop.is_set():
+            if lib.hsv_verify_strict(d, pk, sg) != 1 or lib.hsv_verify_strict(d, pk, s_bad) != 0:
+                errors.append("wrong verdict")
+            done[0] += 2
+    t = threading.Thread(target=votes)
+    t.start()
+    time.sleep(0.2)
+    q0 = counts()
+    worst = 0.0
+    try:
+        for i in range(5):
+            t0 = time.perf_counter()
+            c = ctypes.c_void_p()
+            assert lib.hsv_committee_create(np.ascontiguousarray(w.pk).ctypes.data, w.n, ctypes.byref(c)) == 0
+            lib.hsv_committee_destroy(c)
+            worst = max(worst, time.perf_counter() - t0)
+            time.sleep(0.05)
+    finally:
+        stop.set()
+        t.join(30)
+    q1 = counts()
+    assert not errors, errors[:3]
+    assert worst < 0.5, ("a committee create/destroy waited for the busy service", worst)
+    assert q1[1] - q0[1] > 0, "the service answered nothing while the other thread ran"
+    print("default ok", done[0], worst, q1)
+"""
+
+
+@pytest.mark.parametrize("setting", ["default", "off"])
+def test_resident_service_is_the_default(setting):
+    """The resident latency service is on without any setting (the drop-in's
+    default route for Vote::verify), single verifies teach the committee cache
+    their keys, hsv_set_resident_service switches it at run time, and
+    HSV_QC_RESIDENT=0 keeps every call on the launch path.  Committee creation
+    and destruction (device frees) while a second thread keeps the service
+    busy return promptly: the library's frees pause the service until they
+    have returned (round-5 advice)."""
+    import os
+    import subprocess
+    import sys
+    from conftest import PKG
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = {k: v for k, v in os.environ.items() if k != "HSV_QC_RESIDENT"}
+    if setting == "off":
+        env["HSV_QC_RESIDENT"] = "0"
+    r = subprocess.run([sys.executable, "-c", DEFAULT_CHILD.format(tests=here, pkg=PKG)], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "default ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])

@@ -65,39 +65,60 @@ def test_cpp_mirror_infrastructure_fallback_policy(crypto_tests_bin):
     assert uses >= 6, r.stdout  # every verify / verify_batch call of the port
 
 
+def _route_env(**kv):
+    env = {k: v for k, v in os.environ.items() if k not in ("HSV_ROUTE_SINGLE", "HSV_QC_RESIDENT")}
+    env.update(kv)
+    return env
+
+
 def test_cpp_mirror_host_route_policy(crypto_tests_bin):
-    """Latency routing: single verifies and QCs of at
-    most two votes go to the host verifier before libhsv is called; the 3-vote
-    QCs do not.  The port has 3 single verifies and one empty QC -> 4 routed
-    calls; without a GPU the four 3-vote QCs then take the fallback."""
+    """Latency routing, the default: single verifies
+    go to libhsv (its resident latency service is on by default), QCs of at
+    most two votes to the host verifier before libhsv is called.  The port has
+    3 single verifies and one empty QC -> 1 routed call; without a GPU the 3
+    single verifies and the four 3-vote QCs then take the fallback."""
     from hsverify import _lib
     if _lib.device_count() > 0:
         pytest.skip("a GPU is visible")
-    r = subprocess.run([crypto_tests_bin, "--route", "--fallback"], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([crypto_tests_bin, "--route", "--fallback"], capture_output=True, text=True, timeout=300,
+                       env=_route_env())
     assert r.returncode == 0, r.stderr
-    assert "host-routed calls: 4" in r.stdout
-    assert "infrastructure fallbacks: 4" in r.stdout
+    assert "host-routed calls: 1" in r.stdout
+    assert "infrastructure fallbacks: 7" in r.stdout
+
+
+def test_cpp_mirror_host_route_with_the_service_off(crypto_tests_bin):
+    """HSV_QC_RESIDENT=0 (no resident service: a launched single verify is
+    slower than the host core) or HSV_ROUTE_SINGLE=host puts the 3 single
+    verifies back on the host: 4 routed calls, the four 3-vote QCs fall back."""
+    from hsverify import _lib
+    if _lib.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    for env in (_route_env(HSV_QC_RESIDENT="0"), _route_env(HSV_ROUTE_SINGLE="host")):
+        r = subprocess.run([crypto_tests_bin, "--route", "--fallback"], capture_output=True, text=True, timeout=300,
+                           env=env)
+        assert r.returncode == 0, r.stderr
+        assert "host-routed calls: 4" in r.stdout and "infrastructure fallbacks: 4" in r.stdout, r.stdout
 
 
 @pytest.mark.gpu
 def test_cpp_mirror_host_route_on_gpu(crypto_tests_bin, hsv):
-    """With a device: the routed calls never reach libhsv, the QCs do, and no
-    fallback is consulted."""
-    r = subprocess.run([crypto_tests_bin, "--route", "--fallback"], capture_output=True, text=True, timeout=300)
+    """With a device and the service off: the routed calls never reach libhsv,
+    the QCs do, and no fallback is consulted."""
+    r = subprocess.run([crypto_tests_bin, "--route", "--fallback"], capture_output=True, text=True, timeout=300,
+                       env=_route_env(HSV_QC_RESIDENT="0"))
     assert r.returncode == 0, r.stderr
     assert "host-routed calls: 4" in r.stdout and "infrastructure fallbacks: 0" in r.stdout
 
 
 @pytest.mark.gpu
 def test_cpp_mirror_routes_singles_to_the_resident_service(crypto_tests_bin, hsv):
-    """With the resident latency service on (HSV_QC_RESIDENT=1) the routing
-    default sends single verifies to libhsv (0.0357 against 0.0371 ms for the
-    dalek port): only the empty QC stays on the host, and the
-    reference's tests pass without a fallback."""
-    env = dict(os.environ, HSV_QC_RESIDENT="1")
-    env.pop("HSV_ROUTE_SINGLE", None)
+    """The default route: the resident latency service is on, so single
+    verifies go to libhsv (0.034 against 0.036 ms for the dalek port, DESIGN.md
+    4a): only the empty QC stays on the host, and the reference's tests pass
+    without a fallback."""
     r = subprocess.run([crypto_tests_bin, "--route", "--fallback"], capture_output=True, text=True, timeout=300,
-                       env=env)
+                       env=_route_env())
     assert r.returncode == 0, r.stderr
     assert "all passed" in r.stdout
     assert "host-routed calls: 1" in r.stdout and "infrastructure fallbacks: 0" in r.stdout
