@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -347,16 +348,31 @@ int comb_table_for(DevCtx &c, int v, const uint32_t **out) {
 // ---- persistent host threads for the staging copies ----------------------------
 // A host-buffer batch must be packed into pinned memory before the DMA engine
 // can read it (128 MiB for 2^20 triples).  One thread copies ~10 GB/s, which
-// made the pack -- not PCIe -- the bound of the drop-in path in round 2.  The
-// pool's threads and the caller split every pack; a caller that finds the
-// pool busy (another thread's pack) copies its parts itself.
+// made the pack -- not PCIe -- the bound of the drop-in path in round 2.  Each
+// device has a pool of helper threads, pinned to the CPUs of that GPU's NUMA
+// node (hsv_numa.cpp), which split every pack with the caller; a caller that
+// finds its device's pool busy (another thread's pack) copies its parts
+// itself.  With one pool per device, the shards of a multi-GPU batch pack
+// side by side, each on its GPU's socket (round 5 had one process-wide pool,
+// so at eight shards one shard had the helpers and seven packed alone).
 namespace {
 
 class PackPool {
  public:
-  static PackPool &get() {
-    static PackPool p;
-    return p;
+  PackPool(int nthreads, std::vector<int> cpus) {
+    for (int i = 0; i < nthreads; ++i)
+      workers_.emplace_back([this, cpus] {
+        pin_current_thread(cpus);  // no-op for an empty set
+        loop();
+      });
+  }
+  ~PackPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : workers_) t.join();
   }
   int threads() const { return (int)workers_.size(); }
   // fn(part) for part in [0, nparts), spread over the pool and the caller
@@ -390,23 +406,6 @@ class PackPool {
     std::atomic<int> next{0};
   };
 
-  PackPool() {
-    // default: 11 helpers + the caller, capped by the CPUs this process may
-    // run on (the GPU box's cgroup gives a job 16); at 12 copying threads the
-    // pack of 2^20 triples takes ~1.3 ms (tools/host_pipeline_probe.py)
-    int n = std::min(11, (int)std::thread::hardware_concurrency() - 1);
-    if (const char *v = std::getenv("HSV_PACK_THREADS")) n = std::atoi(v);
-    n = std::max(0, std::min(n, 32));
-    for (int i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
-  }
-  ~PackPool() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto &t : workers_) t.join();
-  }
   void work(Job &j) {
     int mine = 0;
     for (int p; (p = j.next.fetch_add(1)) < j.nparts;) {
@@ -437,6 +436,119 @@ class PackPool {
   bool stop_ = false;
   std::vector<std::thread> workers_;
 };
+
+// The pack pool of `device` (created on first use with that device's
+// placement; -1: an unpinned pool for a caller without a device).  Pools live
+// for the process.
+PackPool &pack_pool(int device) {
+  static std::mutex mu;
+  static std::map<int, std::unique_ptr<PackPool>> pools;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = pools.find(device);
+  if (it == pools.end()) {
+    const HostPlace &p = device_place(device);
+    it = pools.emplace(device, std::unique_ptr<PackPool>(new PackPool(p.pack_threads, p.cpus))).first;
+  }
+  return *it->second;
+}
+
+PackPool &pack_pool_current() {
+  int d = -1;
+  if (hipGetDevice(&d) != hipSuccess) d = -1;
+  return pack_pool(d);
+}
+
+// ---- shard workers ----------------------------------------------------------------
+// One persistent thread per shard index of a multi-GPU host batch: shard i
+// runs on GPU i (run_host, run_tx_host), so its worker is pinned to that GPU's
+// NUMA node, and the slot buffers it allocates there (pinned staging, first
+// touched by this thread) sit on that node too.  Round 5 started one
+// unpinned std::thread per shard per call.
+class ShardWorker {
+ public:
+  ShardWorker() : th_([this] { loop(); }) {}
+  ~ShardWorker() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  void post(int device, std::function<void()> fn) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      q_.push_back({device, std::move(fn)});
+    }
+    cv_.notify_all();
+  }
+
+ private:
+  void loop() {
+    int placed = -2;  // the device this thread is pinned for
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+      if (q_.empty()) return;  // stop_ with nothing left
+      auto job = std::move(q_.front());
+      q_.erase(q_.begin());
+      lk.unlock();
+      if (job.first != placed) {
+        const HostPlace &p = device_place(job.first);
+        if (!pin_current_thread(p.cpus)) pin_current_thread(current_affinity_at_start_);
+        placed = job.first;
+      }
+      job.second();
+      lk.lock();
+    }
+  }
+  std::vector<int> current_affinity_at_start_ = current_affinity();
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<std::pair<int, std::function<void()>>> q_;
+  bool stop_ = false;
+  std::thread th_;  // last: starts once the members above exist
+};
+
+ShardWorker &shard_worker(int shard) {
+  static std::mutex mu;
+  static std::vector<std::unique_ptr<ShardWorker>> workers;
+  std::lock_guard<std::mutex> lk(mu);
+  while ((int)workers.size() <= shard) workers.emplace_back(new ShardWorker());
+  return *workers[shard];
+}
+
+}  // namespace
+
+int run_sharded(int k, const std::function<int(int, int)> &fn) {
+  struct Join {
+    std::mutex mu;
+    std::condition_variable cv;
+    int left = 0;
+  } join;
+  join.left = k;
+  std::vector<int> rcs(k, HSV_OK);
+  std::vector<std::string> errs(k);
+  const int inject = hsvi_inject_mode();  // the caller's (test) injection reaches its shards
+  for (int d = 0; d < k; ++d) {
+    const int dev = shard_device(d, k);
+    shard_worker(d).post(dev, [&, d, dev, inject] {
+      const int prev = hsvi_set_inject(inject);
+      rcs[d] = fn(d, dev);
+      if (rcs[d] != HSV_OK) errs[d] = t_last_error;
+      (void)hsvi_set_inject(prev < 0 ? 0 : prev);
+      std::lock_guard<std::mutex> lk(join.mu);
+      if (--join.left == 0) join.cv.notify_all();
+    });
+  }
+  std::unique_lock<std::mutex> lk(join.mu);
+  join.cv.wait(lk, [&] { return join.left == 0; });
+  for (int d = 0; d < k; ++d)
+    if (rcs[d] != HSV_OK) return fail(rcs[d], "shard " + std::to_string(d) + ": " + errs[d]);
+  return HSV_OK;
+}
+
+namespace {
 
 constexpr size_t kPackPart = size_t(1) << 20;  // bytes per part of a split copy
 
@@ -494,7 +606,7 @@ void stage_copy(uint8_t *dst, const uint8_t *src, size_t bytes) {
     nt_copy(dst, src, bytes);
     return;
   }
-  PackPool::get().run(nparts, [&](int p) {
+  pack_pool_current().run(nparts, [&](int p) {
     const size_t lo = bytes * p / nparts & ~size_t(63), hi = p + 1 == nparts ? bytes : bytes * (p + 1) / nparts & ~size_t(63);
     nt_copy(dst + lo, src + lo, hi - lo);
   });
@@ -623,18 +735,35 @@ int slot_workspaces(Slot &s, size_t need, int count) {
   return HSV_OK;
 }
 
-// Chunk sizes of a pipelined call over n items (n >= 2 kPipeChunk).
-// Nothing hides the first chunk's pack and copy, so it is half a chunk
-// (2^16 items: 10.73 ms per 2^20 against 10.99 for a full first chunk sent
-// in four pieces and 11.01 for 2^15, profiles/r03m_host_pipeline_probe.txt;
-// eight schedules measured within 10.02-10.12 ms,
-// profiles/r03y_host_pipeline_schedules.txt).
+// Launch chunks of a pipelined call over n items (n >= 2 kPipeChunk).  The
+// inputs cross PCIe in pieces of at most kPipeChunk items (57 GB/s: 0.29 ms
+// per piece), four times as fast as the kernels verify them (1.1 ms per
+// piece), so a launch need not wait for one piece each: every chunk is three
+// times all the chunks before it -- 2^16, 3 x 2^16, 12 x 2^16 items for 2^20
+// -- and the next chunk's pieces have landed before the previous chunk's
+// launch ends.  Three launches instead of one per piece: each launch boundary
+// costs a grid end and a prepass the point pass waits for (round 5's
+// schedule of nine 2^17-item chunks took 9.85 ms per 2^20 against 8.91 ms for
+// one launch alone, BENCH r06a).  Only the first piece (2^16 items, 8 MiB:
+// 0.08 ms pack + 0.15 ms copy) is exposed.  hsv_test_pipe_schedule (test
+// library) substitutes a schedule for measurement.
+constexpr size_t kPipeFirst = size_t(1) << 16;
+std::mutex g_pipe_sched_mu;
+std::vector<size_t> g_pipe_sched;  // hsv_test_pipe_schedule; empty: the default
+
 std::vector<size_t> pipe_schedule(size_t n) {
+  std::vector<size_t> want;
+  {
+    std::lock_guard<std::mutex> lk(g_pipe_sched_mu);
+    want = g_pipe_sched;
+  }
   std::vector<size_t> sizes;
-  for (size_t base = 0, k = 0; base < n; ++k) {
-    const size_t want = k == 0 ? kPipeChunk / 2 : kPipeChunk;
-    sizes.push_back(std::min(want, n - base));
-    base += sizes.back();
+  for (size_t done = 0, k = 0; done < n; ++k) {
+    size_t w;
+    if (!want.empty()) w = want[std::min(k, want.size() - 1)];  // the last size repeats
+    else w = done == 0 ? kPipeFirst : 3 * done;
+    sizes.push_back(std::min(std::max<size_t>(w, 1), n - done));
+    done += sizes.back();
   }
   return sizes;
 }
@@ -676,20 +805,17 @@ int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, siz
   const size_t d_flag = d_dig + kAlign;
   const size_t d_fault = d_flag + round_up(n, kAlign);
   const size_t d_total = d_fault + kAlign;
-  // host: two staging buffers of the largest chunk | flags n | self-check words
-  const size_t h_stage = round_up(maxm * rec, kAlign);
+  // host: two staging buffers of one piece | flags n | self-check words
+  const size_t h_stage = round_up(kPipeChunk * rec, kAlign);
   const size_t h_flag = 2 * h_stage;
   const size_t h_fault = h_flag + round_up(n, kAlign);
   const size_t h_total = h_fault + kAlign;
   int rc = slot_prepare(s, d_total, h_total);
   if (rc != HSV_OK) return rc;
-  // Launches alternate over two compute streams.  A chunk's memset and
-  // prepass (~0.1 ms) run beside only the other stream's point pass, a 2^17
-  // grid that fills two thirds of the GPU's lanes (rocprofv3 kernel trace,
-  // profiles/r04l_host_kernel_trace_summary.txt); a third stream fills that
-  // gap but measured slower: 10.27 against 10.04 ms per 2^20, and 9.62
-  // against 9.32 ms with the copies skipped (profiles/r04m_host_streams_ab.txt,
-  // r04i_host_nocopy.txt).
+  // Launches alternate over two compute streams, so a chunk's memset and
+  // prepass can run in the previous chunk's grid end (a third stream measured
+  // slower with round 4's schedule: 10.27 against 10.04 ms per 2^20,
+  // profiles/r04m_host_streams_ab.txt).
   constexpr int nstreams = 2;
   rc = slot_pipeline(s);
   if (rc != HSV_OK) return rc;
@@ -719,43 +845,54 @@ int run_pipelined(Slot &s, int v, const uint32_t *comb_b, const uint8_t *pk, siz
   // alone, for the same inputs called again
   const bool nocopy = g_pipe_nocopy.load(std::memory_order_relaxed) && s.pipe_warm_n == n;
   s.pipe_warm_n = 0;
-  t_clock.marks.clear();  // four marks per chunk instead of the HSV_MARK_* points
+  t_clock.marks.clear();  // four marks per piece instead of the HSV_MARK_* points
+  size_t piece = 0;
   for (size_t base = 0, k = 0, m = 0; k < sizes.size(); base += m, ++k) {
     m = sizes[k];
-    const int b = (int)(k & 1);
-    uint8_t *h = s.h_buf + (size_t)b * h_stage;
-    if (used[b]) {  // the copy that last read this staging buffer has finished
-      e = hipEventSynchronize(staged[b]);
-      if (e != hipSuccess) return drain(hip_fail("hipEventSynchronize", e));
-    }
-    call_chunk_mark();
-    uint8_t *dc = d + base * rec;  // chunk k's records in HBM
+    int last = 0;  // staging buffer of the chunk's last piece
     // Items as records pk | R || s (| digest), so any item range is one
-    // contiguous copy.  (Sending the first chunk in four pieces, each copied
-    // as soon as it was packed, measured no faster: 10.59 against 10.52 ms
-    // per 2^20, profiles/r04o_host_pieces_ab.txt.)
-    if (!nocopy) {
-      const auto t_pack = std::chrono::steady_clock::now();
-      const int nparts = (int)std::min<size_t>(64, (m * rec + kPackPart - 1) / kPackPart);
-      auto part = [&](int p) {
-        const size_t lo = m * p / nparts, hi = m * (p + 1) / nparts;
-        pack_records(h, rec, pk + base * pk_stride, pk_stride, sig + base * sig_stride, sig_stride,
-                     msg + base * msg_stride, msg_stride, lo, hi);
-      };
-      if (nparts < 2) part(0);
-      else PackPool::get().run(nparts, part);
-      t_pack_ms += ms_since(t_pack);
-      e = hipMemcpyAsync(dc, h, m * rec, hipMemcpyHostToDevice, s.copy);
-      if (e != hipSuccess) return drain(hip_fail("hipMemcpyAsync H2D", e));
+    // contiguous copy.  The pieces of a chunk go out one by one, each as
+    // soon as it is packed; the chunk's launch waits for its last piece
+    // (copies run in order on the copy stream).
+    for (size_t pb = 0; pb < m; pb += kPipeChunk, ++piece) {
+      const size_t pm = std::min(kPipeChunk, m - pb);
+      const int b = (int)(piece & 1);
+      last = b;
+      uint8_t *h = s.h_buf + (size_t)b * h_stage;
+      if (used[b]) {  // the copy that last read this staging buffer has finished
+        e = hipEventSynchronize(staged[b]);
+        if (e != hipSuccess) return drain(hip_fail("hipEventSynchronize", e));
+      }
+      call_chunk_mark();
+      const size_t ib = base + pb;  // first item of the piece
+      if (!nocopy) {
+        const auto t_pack = std::chrono::steady_clock::now();
+        const int nparts = (int)std::min<size_t>(64, (pm * rec + kPackPart - 1) / kPackPart);
+        auto part = [&](int p) {
+          const size_t lo = pm * p / nparts, hi = pm * (p + 1) / nparts;
+          pack_records(h, rec, pk + ib * pk_stride, pk_stride, sig + ib * sig_stride, sig_stride,
+                       msg + ib * msg_stride, msg_stride, lo, hi);
+        };
+        if (nparts < 2) part(0);
+        else pack_pool_current().run(nparts, part);
+        t_pack_ms += ms_since(t_pack);
+        call_chunk_mark();
+        e = hipMemcpyAsync(d + ib * rec, h, pm * rec, hipMemcpyHostToDevice, s.copy);
+        if (e != hipSuccess) return drain(hip_fail("hipMemcpyAsync H2D", e));
+        t_h2d_bytes += pm * rec;
+      } else {
+        call_chunk_mark();
+      }
+      e = hipEventRecord(staged[b], s.copy);
+      if (e != hipSuccess) return drain(hip_fail("staging a piece", e));
+      used[b] = true;
+      call_chunk_mark();
+      if (pb + pm < m) call_chunk_mark();  // not the chunk's last piece: no launch behind it
     }
-    call_chunk_mark();
     const int cs = (int)(k % (size_t)nstreams);  // this chunk's compute stream and workspace
-    e = hipEventRecord(staged[b], s.copy);
-    if (e == hipSuccess) e = hipStreamWaitEvent(comp[cs], staged[b], 0);
+    uint8_t *dc = d + base * rec;                // chunk k's records in HBM
+    e = hipStreamWaitEvent(comp[cs], staged[last], 0);
     if (e != hipSuccess) return drain(hip_fail("staging a chunk", e));
-    used[b] = true;
-    call_chunk_mark();
-    t_h2d_bytes += m * rec;
     e = hsv_launch_verify_ws(v, dc, rec, dc + 32, rec, msg_stride ? dc + 96 : d + d_dig, msg_stride ? rec : 0,
                              (uint32_t)m, d + d_flag + base, nullptr, comb_b,
                              reinterpret_cast<uint32_t *>(d + d_fault), s.d_ws[cs], s.ws_cap, comp[cs]);
@@ -837,7 +974,7 @@ int run_on_device(DevCtx &c, const uint8_t *pk, size_t pk_stride, const uint8_t 
       stage_fence();
     };
     if (nparts < 2) part(0);
-    else PackPool::get().run(nparts, part);
+    else pack_pool(c.device).run(nparts, part);
     if (msg_stride == 0) std::memcpy(h + msg_off, msg, 32);
     // a flag the kernels failed to write reads as a rejection, never as an
     // earlier call's verdict; the self-check words start at zero
@@ -894,26 +1031,13 @@ int run_host(const uint8_t *pk, size_t pk_stride, const uint8_t *sig, size_t sig
   if (rc != HSV_OK) return rc;
   const int k = shard_count(n);
   if (k <= 1) return run_on_device(ctx(home_device()), pk, pk_stride, sig, sig_stride, msg, msg_stride, n, flags_out);
-  // contiguous shards, one host thread each
-  std::vector<int> rcs(k, HSV_OK);
-  std::vector<std::string> errs(k);
-  std::vector<std::thread> th;
-  const int inject = hsvi_inject_mode();  // the caller's (test) injection reaches its shards
-  for (int d = 0; d < k; ++d) {
+  // contiguous shards, each on the shard worker of its GPU's node
+  return run_sharded(k, [&](int d, int dev) {
     const size_t lo = n * d / k, hi = n * (d + 1) / k;
-    const int dev = shard_device(d, k);
-    th.emplace_back([&, d, lo, hi, dev, inject]() {
-      (void)hsvi_set_inject(inject);
-      if (hi > lo)
-        rcs[d] = run_on_device(ctx(dev), pk + lo * pk_stride, pk_stride, sig + lo * sig_stride, sig_stride,
-                               msg + lo * msg_stride, msg_stride, hi - lo, flags_out + lo);
-      if (rcs[d] != HSV_OK) errs[d] = t_last_error;
-    });
-  }
-  for (auto &t : th) t.join();
-  for (int d = 0; d < k; ++d)
-    if (rcs[d] != HSV_OK) return fail(rcs[d], "shard " + std::to_string(d) + ": " + errs[d]);
-  return HSV_OK;
+    if (hi <= lo) return HSV_OK;
+    return run_on_device(ctx(dev), pk + lo * pk_stride, pk_stride, sig + lo * sig_stride, sig_stride,
+                         msg + lo * msg_stride, msg_stride, hi - lo, flags_out + lo);
+  });
 }
 
 int batch_verdict(const uint8_t *flags, size_t n) {
@@ -955,6 +1079,13 @@ int hsvi_set_virtual_shards(int k) {
 }
 
 int hsvi_set_pipe_nocopy(int on) { return hsvh::g_pipe_nocopy.exchange(on != 0) ? 1 : 0; }
+
+int hsvi_set_pipe_schedule(const uint64_t *sizes, int count) {
+  if (count < 0 || count > 64 || (count > 0 && !sizes)) return fail(HSV_ERR_INVALID_ARG, "schedule of 0..64 sizes");
+  std::lock_guard<std::mutex> lk(hsvh::g_pipe_sched_mu);
+  hsvh::g_pipe_sched.assign(sizes, sizes + count);
+  return HSV_OK;
+}
 
 // Lifecycle call: must not run concurrently with verify calls (hsv.h).  It
 // still quiesces first -- every slot locked and drained, every side stream
@@ -1186,7 +1317,10 @@ void hsv_host_call_stats(double *pack_ms, double *h2d_bytes, double *call_ms) {
   if (call_ms) *call_ms = t_call_ms;
 }
 
-int hsv_pack_threads(void) { return PackPool::get().threads(); }
+int hsv_pack_threads(void) {
+  const int d = ensure_init() == HSV_OK ? home_device() : -1;
+  return pack_pool(d).threads();
+}
 
 // The host timeline of the calling thread's last call (hsv.h HSV_MARK_*, or
 // four marks per chunk of a pipelined call); returns the count.

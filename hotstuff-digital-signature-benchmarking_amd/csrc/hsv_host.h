@@ -16,6 +16,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -199,8 +200,34 @@ int ensure_btable(DevCtx &c);
 int ensure_btable16(DevCtx &c);
 int comb_table_for(DevCtx &c, int variant, const uint32_t **out);
 
-// memcpy into pinned staging; large copies split over a few host threads
+// memcpy into pinned staging; large copies split over the pack pool of the
+// current device (its helpers run on the GPU's NUMA node)
 void stage_copy(uint8_t *dst, const uint8_t *src, size_t bytes);
+
+// ---- host placement (hsv_numa.cpp) -------------------------------------------
+struct HostPlace {
+  int node = -1;          // NUMA node of the GPU's PCIe function (-1: unknown / single node)
+  std::vector<int> cpus;  // that node's CPUs the process may use (empty: threads stay unpinned)
+  int pack_threads = 0;   // helpers of the device's pack pool
+};
+bool parse_cpulist(const std::string &text, std::vector<int> &out);
+std::vector<int> current_affinity();
+bool pin_current_thread(const std::vector<int> &cpus);
+int default_pack_threads();
+// For PCI functions `bdfs` under the sysfs tree `root`: each one's node, the
+// node's CPUs within `allowed` (sorted), and the pack-pool size (the node's
+// CPUs split among its GPUs, at most pack_default)
+std::vector<HostPlace> plan_host_places(const std::string &root, const std::vector<std::string> &bdfs,
+                                        const std::vector<int> &allowed, int pack_default);
+// The placement of a visible device (sysfs under /sys, the process affinity
+// at first use); a device without NUMA information gets an unpinned place.
+const HostPlace &device_place(int device);
+
+// Run fn(shard, device) for shards [0, k) of a host batch, each on the
+// persistent shard worker of its index, pinned to the NUMA node of its
+// device; returns HSV_OK or the first shard's error.  The caller's fault
+// injection mode (tests) reaches the workers.
+int run_sharded(int k, const std::function<int(int shard, int device)> &fn);
 
 // Device owning a device pointer (hipPointerGetAttributes); -1 if unknown.
 int pointer_device(const void *p);

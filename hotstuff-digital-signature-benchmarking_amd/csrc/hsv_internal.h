@@ -184,6 +184,7 @@ int hsvi_set_error(int code, const char *msg);
 // test hooks of hsv_capi.cpp (exported as hsv_set_* by libhsv_test.so only)
 int hsvi_set_virtual_shards(int k);
 int hsvi_set_pipe_nocopy(int on);  // hsv_test_pipe_nocopy (libhsv_test.so only)
+int hsvi_set_pipe_schedule(const uint64_t *sizes, int count);  // hsv_test_pipe_schedule
 int hsvi_set_variant(int v);
 #ifdef __cplusplus
 }

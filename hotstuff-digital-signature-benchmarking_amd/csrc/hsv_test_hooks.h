@@ -46,6 +46,21 @@ HSV_API int hsv_set_virtual_shards(int k);
  * flags are the previous inputs' flags, so it never belongs in a product
  * library.  Returns the previous setting. */
 HSV_API int hsv_test_pipe_nocopy(int on);
+/* Measurement only (tools/host_sched_ab.py): the launch-chunk sizes of the
+ * pipelined host call (items; the last size repeats; count 0 restores the
+ * default schedule).  Returns HSV_OK or HSV_ERR_INVALID_ARG. */
+HSV_API int hsv_test_pipe_schedule(const uint64_t *sizes, int count);
+/* Host placement plan (csrc/hsv_numa.cpp) for the PCI functions in bdfs_csv
+ * ("0000:0d:00.0,...") under a sysfs tree at sysfs_root, within the CPUs of
+ * allowed_cpulist ("0-7"): per function its NUMA node (-1 unknown), the
+ * number of that node's allowed CPUs its threads are pinned to, and its
+ * pack-pool size.  Returns the number of functions or HSV_ERR_INVALID_ARG. */
+HSV_API int hsv_test_numa_plan(const char *sysfs_root, const char *bdfs_csv, const char *allowed_cpulist,
+                               int pack_default, int *node_out, int *ncpus_out, int *pack_out, int cap);
+/* A thread pinned the way the library pins its shard workers and pack
+ * helpers, to the CPUs of `cpulist`: the affinity it then reports (count, CPUs
+ * written to cpus_out), or HSV_ERR_INVALID_ARG. */
+HSV_API int hsv_test_pinned_thread_cpus(const char *cpulist, int *cpus_out, int cap);
 /* The resident latency service (HSV_QC_RESIDENT=1): requests posted to it and
  * answered by it in this process so far (either pointer may be NULL). */
 HSV_API void hsv_test_resident_counts(uint64_t *posted, uint64_t *answered);

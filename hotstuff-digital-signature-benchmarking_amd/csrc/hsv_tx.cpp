@@ -127,21 +127,11 @@ int run_tx_host(const uint8_t *txs, const uint64_t *offsets, size_t tx_size, siz
   if (rc != HSV_OK) return rc;
   const int k = shard_count(n);
   if (k <= 1) return run_tx_on_device(ctx(home_device()), txs, offsets, tx_size, 0, n, flags_out);
-  std::vector<int> rcs(k, HSV_OK);
-  std::vector<std::string> errs(k);
-  std::vector<std::thread> th;
-  for (int d = 0; d < k; ++d) {
+  // contiguous shards, each on the shard worker of its GPU's node
+  return run_sharded(k, [&](int d, int dev) {
     const size_t lo = n * d / k, hi = n * (d + 1) / k;
-    const int dev = shard_device(d, k);
-    th.emplace_back([&, d, lo, hi, dev]() {
-      if (hi > lo) rcs[d] = run_tx_on_device(ctx(dev), txs, offsets, tx_size, lo, hi, flags_out + lo);
-      if (rcs[d] != HSV_OK) errs[d] = last_error();
-    });
-  }
-  for (auto &t : th) t.join();
-  for (int d = 0; d < k; ++d)
-    if (rcs[d] != HSV_OK) return fail(rcs[d], "shard " + std::to_string(d) + ": " + errs[d]);
-  return HSV_OK;
+    return hi > lo ? run_tx_on_device(ctx(dev), txs, offsets, tx_size, lo, hi, flags_out + lo) : HSV_OK;
+  });
 }
 
 }  // namespace

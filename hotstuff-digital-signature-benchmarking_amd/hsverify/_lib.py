@@ -27,7 +27,8 @@ TEST_LIB_PATH = os.path.join(_HERE, "libhsv_test.so")
 HOOKS = ("hsv_test_inject_fault", "hsv_test_inject_mode", "hsv_test_corrupt_auto_committee",
          "hsv_test_lanesplit_check", "hsv_set_lattice_bits", "hsv_set_variant", "hsv_variant_list",
          "hsv_variant_available", "hsv_num_variants", "hsv_set_virtual_shards", "hsv_test_pipe_nocopy",
-         "hsv_test_resident_counts", "hsv_test_resident_post_bad", "hsv_test_tx_records")
+         "hsv_test_resident_counts", "hsv_test_resident_post_bad", "hsv_test_tx_records",
+         "hsv_test_pipe_schedule", "hsv_test_numa_plan", "hsv_test_pinned_thread_cpus")
 
 # flag bits (include/hsv.h)
 STRICT_OK = 0x01
@@ -70,6 +71,10 @@ def _declare(lib):
         "hsv_bound_device": (ctypes.c_int, []),
         "hsv_set_virtual_shards": (ctypes.c_int, [ctypes.c_int]),
         "hsv_test_pipe_nocopy": (ctypes.c_int, [ctypes.c_int]),
+        "hsv_test_pipe_schedule": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+        "hsv_test_numa_plan": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+        "hsv_test_pinned_thread_cpus": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int]),
         "hsv_test_resident_counts": (None, [ctypes.POINTER(ctypes.c_uint64)] * 2),
         "hsv_test_resident_post_bad": (ctypes.c_int, [ctypes.c_uint32]),
         "hsv_test_tx_records": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,

@@ -47,10 +47,13 @@ def test_init_binds_and_reports_device(mods, hsv):
         hsv.hsv_init(-1)
 
 
-@pytest.mark.parametrize("shards", [2, 3, 5])
+@pytest.mark.parametrize("shards", [2, 3, 5, 8])
 def test_virtual_shards_gather_matches_unsharded_and_oracle(mods, oracle_lib, shards):
-    """run_host's multi-device path: contiguous shards, one host thread and
-    slot each, flags written into the caller's buffer at the shard offsets."""
+    """run_host's multi-device path: contiguous shards, each on the persistent
+    shard worker of its index (pinned to its GPU's NUMA node, run_sharded) with
+    a slot and the device's pack pool, flags written into the caller's buffer
+    at the shard offsets; k = 8 as on an 8-GPU node (more shards than slots:
+    they queue for the device's four slots)."""
     _, _, synth, verifier = mods
     from hsverify import _testing
     n = (1 << 16) + 12345

@@ -457,9 +457,10 @@ def test_c4_full_size_properties(api, oracle_lib):
 
 
 def test_host_api_pipelined_chunks_match_device_api(api, oracle_lib):
-    """Host batches of >= 2^18 items run as one streamed launch over pieces of
-    2^14 items (hsv_capi.cpp run_streamed): an uneven last piece, every flag
-    equal to the device-resident launch, and an oracle-checked sample."""
+    """Host batches of >= 2^18 items run the copy pipeline (hsv_capi.cpp
+    run_pipelined: launch chunks of 2^16, 3 x 2^16, then the rest, copied in
+    pieces of 2^17 items): an uneven last piece, every flag equal to the
+    device-resident launch, and an oracle-checked sample."""
     import torch
     _, verifier, synth = api
     n = (1 << 19) + (1 << 18) + 12345
@@ -477,8 +478,8 @@ def test_host_api_pipelined_chunks_match_device_api(api, oracle_lib):
 
 
 def test_host_api_pipeline_shared_digest_and_packed_votes(api, oracle_lib):
-    """The streamed host path (hsv_capi.cpp run_streamed: 96-byte records and
-    one shared digest, read through the pinned staging's device mapping) with
+    """The pipelined host path (hsv_capi.cpp run_pipelined: 96-byte records
+    and one shared digest staged once) with
     one shared digest (a huge QC) and with packed 96-byte votes
     (hsv_verify_batch_packed's strided records): flags equal the
     device-resident launch and an oracle sample."""
@@ -510,3 +511,29 @@ def test_host_api_pipeline_shared_digest_and_packed_votes(api, oracle_lib):
         assert lib.hsv_verify_batch_packed(digest.tobytes(), packed.tobytes(), n) == 1
     finally:
         lib.hsv_set_auto_committee(1)
+
+
+@pytest.mark.parametrize("sched", [[1000, 70000, 3], [1 << 18], [12345, 1 << 17, 5 << 16]])
+def test_host_api_pipeline_schedules(api, sched):
+    """Any launch schedule of the pipelined host call (hsv_test_pipe_schedule,
+    test library: ragged chunks, chunks of several copy pieces, a chunk of one
+    item) gives the device-resident launch's flags."""
+    import ctypes
+    import torch
+    from hsverify import _testing
+    _, verifier, synth = api
+    n = (1 << 18) + 4321
+    w = synth.independent_triples(n, seed=78, corrupt_frac=0.05)
+    dev = torch.device("cuda:0")
+    flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+    verifier.verify_device(*(torch.from_numpy(a).to(dev) for a in (w.pk, w.sig, w.msg)), flags)
+    torch.cuda.synchronize()
+    want = flags.cpu().numpy()
+    with _testing.test_library() as lib:
+        arr = (ctypes.c_uint64 * len(sched))(*sched)
+        assert lib.hsv_test_pipe_schedule(arr, len(sched)) == 0
+        try:
+            got = verifier.verify_flags(w.pk, w.sig, w.msg)
+        finally:
+            lib.hsv_test_pipe_schedule(None, 0)
+    assert (got == want).all()
