@@ -5,7 +5,9 @@
 //   26 (default)  hsv_fe26x10.hpp: 10 limbs of 26/25 bits (radix 2^25.5);
 //                 column sums accumulate in place on v_mad_u64_u32 with the
 //                 mod-p fold pre-applied (19x / 2x operand scaling).
-//   32            hsv_fe32x8.hpp: 8 limbs of 32 bits, operand scanning.
+//   32            hsv_fe32x8.hpp: 8 limbs of 32 bits, operand scanning -- a
+//                 measured alternative kept for the host test build only
+//                 (tests/native/, built with -I tests/native).
 // API: fe, fe_small, fe_from_words_masked, fe_pack (canonical 8 words),
 // fe_add, fe_sub, fe_neg, fe_mul, fe_sq, fe_carry, fe_canon, fe_is_zero,
 // fe_select, fe_d / fe_d2 / fe_sqrtm1, plus the generic chains below.

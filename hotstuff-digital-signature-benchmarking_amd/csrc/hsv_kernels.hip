@@ -903,34 +903,17 @@ __global__ void __launch_bounds__(256) hsv_mad_peak_kernel(uint32_t *sink, uint3
 
 }  // namespace hsv
 
-// Kernel variants, selectable for measurement (hsv_set_variant / HSV_VARIANT).
-//   0: WA=2 WB=8  2 waves/SIMD (table of 2 cached points in registers)
-//   1: WA=3 WB=9  1 wave/SIMD
-//   2: WA=4 WB=8  1 wave/SIMD
-//   3: WA=3 WB=9  2 waves/SIMD (register-capped; spills if it does not fit)
-//   4: half-size scalars, WA=3 WB=9, 2 waves/SIMD
-//   5: half-size scalars, WA=3 WB=9, 1 wave/SIMD
-//   6: half-size scalars, WA=2 WB=8, 2 waves/SIMD
-//   7: half-size scalars, memory-resident variable-base tables, WA=3 WB=9, 2 waves/SIMD
-//   8: as 7 with WA=2 WB=8
-//   9: as 7 with WA=4 WB=8
-//  10: half-size scalars + comb table for B, memory tables, WA=3, 2 waves/SIMD
-//  11: as 10 with WA=4
-//  12: as 10 with WA=5
-//  13: as 11, 3 waves/SIMD, table entries loaded at their addition (no prefetch)
-//  14: as 11, 2 waves/SIMD, no prefetch
-//  15: as 13 with the wide (16-bit digit, 48 MiB) comb table of B
-//  16: as 14 with the wide comb table
-//  17: as 15, full-length fallback items deferred to a second launch
-//  18: as 16, fallback deferred
-//  19: two passes: scalar prepass, then the point pass with the fallback
-//      items dealt out first (WA 4, 3 waves/SIMD, wide comb)
-//  20: as 19, 2 waves/SIMD
-//  21: as 19 for batches above 2^13 items; at or below, the latency form:
-//      prepass, then two lanes per item (hsv_verify_pair_kernel)
-//  22: as 21 with a pair-lane tail in the large-batch point pass (hsv_verify_hpt_kernel)
-// id space of the variants (hsv_variant_list gives the ids built into this library)
-extern "C" int hsvi_num_variants(void) { return 23; }
+// Kernel variant ids (hsv_set_variant, test library).  The library builds two
+// (kVariantIds below):
+//  19: two passes -- scalar prepass (hsv_prep_kernel), then the persistent
+//      point pass with the fallback items dealt out first (WA 4, 3 waves/SIMD,
+//      wide comb of B)
+//  21: the default: 19's kernels above 2^13 items; at or below, the latency
+//      forms (quad / joint / row / pair)
+// Ids 0-18, 20 and 22 were rounds 1-4's measured alternatives; they left the
+// source in round 5 (git history before that cleanup).  The id space stays
+// [0, 22) so old measurement records keep their meaning.
+extern "C" int hsvi_num_variants(void) { return 22; }
 
 namespace {
 struct WsPools {
@@ -1006,6 +989,17 @@ extern "C" hipError_t hsv_ws_malloc(void **p, size_t bytes, hipStream_t stream) 
         e = hipMemPoolSetAttribute(pool, a, &no);
         if (e != hipSuccess) return e;
       }
+#ifdef HSV_WS_POOL_PROBE
+      // Measurement builds only (tools/build_ab_libs.sh): one
+      // cross-stream reuse policy back on -- 1 event dependencies, 2
+      // opportunistic -- to pin which one handed a running launch's block on.
+      {
+        int yes = 1;
+        e = hipMemPoolSetAttribute(pool, HSV_WS_POOL_PROBE == 1 ? hipMemPoolReuseFollowEventDependencies
+                                                                : hipMemPoolReuseAllowOpportunistic, &yes);
+        if (e != hipSuccess) return e;
+      }
+#endif
       it = pools.emplace(dev, pool).first;
     }
     pool = it->second;

@@ -130,30 +130,4 @@ HSV_INL sc sc_muladd(const sc &a, const sc &b, const sc &c) {
   return sc_reduce512(t);
 }
 
-// k + C3, C3 = sum_{i<85} 4 * 8^i  (window 3, digits in [-4, 3]); result < 2^255
-HSV_INL void sc_recode_w3(const sc &k, uint32_t out[8]) {
-  const uint32_t c3[8] = {0x24924924u, 0x49249249u, 0x92492492u, 0x24924924u,
-                          0x49249249u, 0x92492492u, 0x24924924u, 0x49249249u};
-  uint64_t t = 0;
-  HSV_UNROLL
-  for (int i = 0; i < 8; ++i) {
-    t += (uint64_t)k.v[i] + c3[i];
-    out[i] = (uint32_t)t;
-    t >>= 32;
-  }
-}
-
-// s + C9, C9 = sum_{j<29} 256 * 512^j  (window 9, digits in [-256, 255]); result < 2^261
-HSV_INL void sc_recode_w9(const sc &s, uint32_t out[9]) {
-  const uint32_t c9[9] = {0x04020100u, 0x40201008u, 0x02010080u, 0x20100804u, 0x01008040u,
-                          0x10080402u, 0x00804020u, 0x08040201u, 0x00000010u};
-  uint64_t t = 0;
-  HSV_UNROLL
-  for (int i = 0; i < 9; ++i) {
-    t += (uint64_t)(i < 8 ? s.v[i] : 0u) + c9[i];
-    out[i] = (uint32_t)t;
-    t >>= 32;
-  }
-}
-
 }  // namespace hsv

@@ -84,7 +84,7 @@ def test_challenge_scalar_matches_python(core_host):
 @pytest.fixture(scope="module")
 def core_host32():
     """The alternative radix-2^32 field representation (HSV_FE_RADIX=32)."""
-    return _build(BIN + "32", "-DHSV_FE_RADIX=32")
+    return _build(BIN + "32", "-DHSV_FE_RADIX=32", "-I", os.path.join(ROOT, "tests", "native"))
 
 
 @pytest.mark.parametrize("variant", [0, 1, 10, 11, 12, 14, 16, 18, 20, 21])

@@ -23,8 +23,9 @@ sys.path.insert(0, os.path.join(ROOT, "hotstuff-digital-signature-benchmarking_a
 SCHEDULES = {
     "default": [],                                   # 2^16, then 3x everything before
     "r05_pieces": [1 << 16, 1 << 17],                # round 5: 2^16, then 2^17 per launch
-    "two": [1 << 17, 1 << 20],                       # 2^17, then the rest
-    "geo4_14": [1 << 14, 5 << 14, 25 << 14, 1 << 20],  # first launch from 2 MiB, x5 growth
+    "full1": [3 << 16, 3 << 16, 1 << 20],            # one 64-item batch per wave of the grid first
+    "full1b": [3 << 16, 1 << 20],
+    "half_full": [3 << 15, 3 << 16, 1 << 20],
     "geo_15": [1 << 15, 3 << 15, 12 << 15, 1 << 20],
 }
 
