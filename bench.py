@@ -668,20 +668,28 @@ def mempool_bench(dev, n=1 << 20, tx_size=512, cpu_sample=1 << 17, nstreams=2, s
            "outputs_identical_across_streams": all(bool(torch.equal(outs[0], o)) for o in outs[1:]),
            "honest_all_accepted": bool((f[w.accept] & 1).all()),
            "corrupted_all_rejected": bool(not (f[~w.accept] & 1).any())}
-    if cpu_sample <= 0:
-        return res
+    sample = 1 << 17
+    res["_check"] = (np.ascontiguousarray(w.txs[:sample]), tx_size, f[:sample].copy())  # for mempool_cpu
+    if cpu_sample > 0:
+        res["cpu_baseline"] = mempool_cpu(res.pop("_check"), cpu_sample)
+    return res
+
+
+def mempool_cpu(check, cpu_sample=1 << 17):
+    """The C port on host threads over the first transactions of the mempool
+    line's batch, flag-for-flag against the GPU's flags for them."""
+    txs, tx_size, gpu = check
     lib = _oracle()
-    m = min(cpu_sample, n)
+    m = min(cpu_sample, len(txs))
     threads, _ = host_cores()
-    buf = np.ascontiguousarray(w.txs[:m])
+    buf = np.ascontiguousarray(txs[:m])
     out = np.zeros(m, np.uint8)
     t0 = time.perf_counter()
     with all_host_cpus():
         lib.oracle_verify_tx_many(buf.ctypes.data, None, tx_size, m, out.ctypes.data, threads)
     dt = time.perf_counter() - t0
-    res["cpu_baseline"] = {"value": m / dt, "unit": "tx/s", "cores": threads, "kind": "port",
-                           "sample": f"first {m} transactions", "sample_parity_vs_gpu": bool((out == f[:m]).all())}
-    return res
+    return {"value": m / dt, "unit": "tx/s", "cores": threads, "kind": "port",
+            "sample": f"first {m} transactions", "sample_parity_vs_gpu": bool((out == gpu[:m]).all())}
 
 
 def host_api_bench(w, dev, reps=5):
@@ -1129,9 +1137,20 @@ def main():
                    "expected_accept": "honest items and the mixed-order-A items with k = 0 mod 8"},
     }
     if not a.no_qc:
-        # the drop-in boundary from host buffers, measured next to the C4 line it
-        # is compared with (after the other benchmarks it read 11.62 against
-        # 11.21 ms on the same box, profiles/r03p_bench.json)
+        # The two lines compared with the C4 line run right after it, in the same
+        # conditions: the mempool line (the same point pass behind a message-hash
+        # record kernel) first, then the drop-in boundary from host buffers.
+        # After the latency legs -- a minute of other GPU work, and the resident
+        # latency service's block on one CU -- the same mempool line read 7 %
+        # slower than C4 (BENCH r05, r06a) against 4 % beside it
+        # (profiles/r06/r06e_mp.txt); the host call read 11.62 against 11.21 ms
+        # (profiles/r03p_bench.json).
+        # two streams: the record kernels (message hash + prepass, 2.3x the C4
+        # prepass's work) fill the point passes' grid ends better with one
+        # batch in flight beside the next than with two (9.57 against 9.77 ms
+        # per 2^20, profiles/r04z_mempool_streams2.txt)
+        out["mempool_tx"] = mempool_bench(dev, nstreams=2, streams=streams[:2] if nst >= 2 else None,
+                                          cpu_sample=0)
         out["host_api"] = host_api_bench(w, dev)
         if early_host_api is not None:
             out["host_api_early"] = early_host_api
@@ -1147,13 +1166,11 @@ def main():
             out["launched"] = launched_leg(a.qc_reps, a.tc_seq_reps)
         _lib.load().hsv_set_auto_committee(1)
         out["committee_cache"] = committee_bench(a.qc_reps, dev)
-        # two streams: the record kernels (message hash + prepass, 2.3x the C4
-        # prepass's work) fill the point passes' grid ends better with one
-        # batch in flight beside the next than with two (9.57 against 9.77 ms
-        # per 2^20, profiles/r04z_mempool_streams2.txt)
-        out["mempool_tx"] = mempool_bench(dev, nstreams=2, streams=streams[:2] if nst >= 2 else None)
+        chk = out["mempool_tx"].pop("_check", None)
         if world == 1 and not a.no_cpu_baseline:
             with all_host_cpus():
+                if chk is not None:
+                    out["mempool_tx"]["cpu_baseline"] = mempool_cpu(chk)
                 out["qc_cpu_baseline"] = qc_cpu()
     if a.detail:
         try:
