@@ -82,7 +82,9 @@ int fail(int code, const std::string &msg) {
 }
 
 int hip_fail(const char *where, hipError_t e) {
-  return fail(HSV_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+  // out of device memory (after hsv_ws_malloc's trim and retry) is the
+  // allocation error of include/hsv.h, every other HIP failure HSV_ERR_HIP
+  return fail(e == hipErrorOutOfMemory ? HSV_ERR_ALLOC : HSV_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
 }
 
 const std::string &last_error() { return t_last_error; }
@@ -534,8 +536,13 @@ int run_sharded(int k, const std::function<int(int, int)> &fn) {
     const int dev = shard_device(d, k);
     shard_worker(d).post(dev, [&, d, dev, inject] {
       const int prev = hsvi_set_inject(inject);
-      rcs[d] = fn(d, dev);
-      if (rcs[d] != HSV_OK) errs[d] = t_last_error;
+      try {
+        rcs[d] = fn(d, dev);
+        if (rcs[d] != HSV_OK) errs[d] = t_last_error;
+      } catch (const std::exception &e) {  // a host allocation failed: the shard's error, not the worker's end
+        rcs[d] = HSV_ERR_ALLOC;
+        errs[d] = e.what();
+      }
       (void)hsvi_set_inject(prev < 0 ? 0 : prev);
       std::lock_guard<std::mutex> lk(join.mu);
       if (--join.left == 0) join.cv.notify_all();
