@@ -1143,13 +1143,14 @@ def main():
         # After the latency legs -- a minute of other GPU work, and the resident
         # latency service's block on one CU -- the same mempool line read 7 %
         # slower than C4 (BENCH r05, r06a) against 4 % beside it
-        # (profiles/r06/r06e_mp.txt); the host call read 11.62 against 11.21 ms
-        # (profiles/r03p_bench.json).
-        # two streams: the record kernels (message hash + prepass, 2.3x the C4
-        # prepass's work) fill the point passes' grid ends better with one
-        # batch in flight beside the next than with two (9.57 against 9.77 ms
-        # per 2^20, profiles/r04z_mempool_streams2.txt)
-        out["mempool_tx"] = mempool_bench(dev, nstreams=2, streams=streams[:2] if nst >= 2 else None,
+        # (profiles/r06/r06e_mp_analysis.json); the host call read 11.62 against
+        # 11.21 ms (profiles/r03p_bench.json).
+        # All three of the C4 line's streams: with the round-6 record kernel
+        # (0.82 ms per 2^20, bitop3 message hash) three streams beat two, 9.61
+        # against 9.66 ms (profiles/r06/r06l_nstreams_b3f.txt); round 4's
+        # record kernel, 2.3x the C4 prepass's work, had been faster on two
+        # (9.57 against 9.77 ms, profiles/r04z_mempool_streams2.txt).
+        out["mempool_tx"] = mempool_bench(dev, nstreams=3, streams=streams if nst >= 2 else None,
                                           cpu_sample=0)
         out["host_api"] = host_api_bench(w, dev)
         if early_host_api is not None:

@@ -15,6 +15,14 @@
 // (about 4 x 80 rounds) against ~2,300 field operations for the signature.
 #include <hip/hip_runtime.h>
 
+// The message hash in this file runs gfx950's v_bitop3_b32 for the sigma XOR
+// triples, the majority and the choice (hsv_sha512.hpp): with the bitop3
+// results kept as opaque 64-bit pairs that is 754 instead of 991 instructions
+// per 16 rounds, and the record kernel went from 0.99 to 0.82 ms per 2^20
+// transactions together with the full-block fast path below
+// (profiles/r06/r06k_*).  The latency kernels keep the XOR form (their lone
+// waves measured no faster with it).
+#define HSV_SHA_BITOP3 1
 #include "hsv_internal.h"
 #include "hsv_txhash.hpp"
 #include "hsv_verify_hc.hpp"
@@ -111,14 +119,6 @@ __global__ void __launch_bounds__(kTxBlock) hsv_tx_record_kernel(const uint8_t *
   const uint64_t start = (uint64_t)(base & 15u) + lo;
   const uint64_t mlen = ok ? hi - lo - 96 : 0;
   const uint64_t q_last = ok ? (start + (hi - lo) - 1) >> 4 : kNoChunk;
-  uint32_t r[32];
-  // pk || R || s: the last 96 bytes (7 chunks at any offset)
-  {
-    const uint64_t tail = start + mlen;
-    uint32_t raw[4 * 7 + 1];
-    tx_stage_chunks<7>(q, stage, lane, tail >> 4, q_last, raw);
-    tx_realign<24>(raw, (uint32_t)(tail & 15u), r);
-  }
   // SHA-512 of the message, block by block
   uint64_t h[8];
   sha512_init(h);
@@ -127,15 +127,35 @@ __global__ void __launch_bounds__(kTxBlock) hsv_tx_record_kernel(const uint8_t *
   HSV_UNROLL
   for (int m = 1; m < 64; m <<= 1) wave_blocks = max(wave_blocks, (uint32_t)__shfl_xor((int)wave_blocks, m, 64));
   const uint32_t sh16 = (uint32_t)(start & 15u);
+  // wave-uniform fast paths: every transaction of the wave starts on a 16-byte
+  // boundary (no realignment), and block b lies wholly inside every message
+  // (no padding selects) -- the common case of equal-sized transactions
+  const bool wave_aligned = __all(sh16 == 0u);
   HSV_NOUNROLL
   for (uint32_t b = 0; b < wave_blocks; ++b) {
     uint32_t raw[4 * kTxQ + 1];
     tx_stage_chunks<kTxQ>(q, stage, lane, (start >> 4) + 8ull * b, q_last, raw);
+    const bool wave_full = __all((uint64_t)(b + 1u) * 128u <= mlen);
     if (b < nblocks) {
       uint32_t words[32];
-      tx_realign<32>(raw, sh16, words);
-      tx_compress_block(h, words, mlen, b, nblocks);
+      if (wave_aligned) {
+        HSV_UNROLL
+        for (int j = 0; j < 32; ++j) words[j] = raw[j];
+      } else {
+        tx_realign<32>(raw, sh16, words);
+      }
+      if (wave_full) tx_compress_full_block(h, words);
+      else tx_compress_block(h, words, mlen, b, nblocks);
     }
+  }
+  // pk || R || s: the last 96 bytes (7 chunks at any offset), staged after
+  // the hash so that its 24 words are not live across the message loop
+  uint32_t r[32];
+  {
+    const uint64_t tail = start + mlen;
+    uint32_t raw[4 * 7 + 1];
+    tx_stage_chunks<7>(q, stage, lane, tail >> 4, q_last, raw);
+    tx_realign<24>(raw, (uint32_t)(tail & 15u), r);
   }
   tx_digest_words(h, r + 24);
   if (i >= n) return;

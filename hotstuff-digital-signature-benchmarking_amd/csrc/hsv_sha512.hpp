@@ -76,7 +76,9 @@ HSV_SHA_INL void sha512_init(uint64_t h[8]) {
 // over A = 0xf0, B = 0xcc, C = 0xaa): x ^ y ^ z is 0x96, maj 0xe8, ch 0xca.
 // Without it the compiler forms v_bfi_b32 for ch but keeps the XOR pairs of
 // the four sigma functions and the majority as two or three instructions.
-// HSV_SHA_BITOP3=1 selects the v_bitop3 form.
+// HSV_SHA_BITOP3=1 selects the v_bitop3 form: the mempool
+// kernels define it (csrc/hsv_mempool.hip); the other translation units keep
+// the XOR form.
 #ifndef HSV_SHA_BITOP3
 #define HSV_SHA_BITOP3 0
 #endif
@@ -85,7 +87,12 @@ HSV_SHA_INL uint64_t sha_bitop3(uint64_t x, uint64_t y, uint64_t z) {
 #if defined(__HIP_DEVICE_COMPILE__) && HSV_SHA_BITOP3
   const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)x, (uint32_t)y, (uint32_t)z, IMM);
   const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(x >> 32), (uint32_t)(y >> 32), (uint32_t)(z >> 32), IMM);
-  return ((uint64_t)hi << 32) | lo;
+  uint64_t r = ((uint64_t)hi << 32) | lo;
+  // opaque pair: otherwise the compiler splits the 64-bit adds that consume
+  // r into a low add, a separate high-half add and a v_mov (more instructions
+  // than the XORs the bitop3 saves)
+  asm("" : "+v"(r));
+  return r;
 #else
   if constexpr (IMM == 0x96) return x ^ y ^ z;
   if constexpr (IMM == 0xe8) return (x & y) ^ (x & z) ^ (y & z);

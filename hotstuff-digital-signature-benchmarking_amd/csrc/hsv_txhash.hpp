@@ -106,6 +106,17 @@ HSV_INL void tx_compress_block(uint64_t h[8], const uint32_t words[32], uint64_t
   sha512_compress(h, w);
 }
 
+// The same for a block wholly inside the message ((b + 1) * 128 <= mlen): no
+// padding word, no length field.  The kernel takes it when every lane of the
+// wave is in that case (wave-uniform branch), which is all but the last block
+// of equal-sized transactions.
+HSV_INL void tx_compress_full_block(uint64_t h[8], const uint32_t words[32]) {
+  uint64_t w[16];
+  HSV_UNROLL
+  for (int j = 0; j < 16; ++j) w[j] = be64_from_le32(words[2 * j], words[2 * j + 1]);
+  sha512_compress(h, w);
+}
+
 // First 32 digest bytes as 8 little-endian words.
 HSV_INL void tx_digest_words(const uint64_t h[8], uint32_t out[8]) {
   HSV_UNROLL
