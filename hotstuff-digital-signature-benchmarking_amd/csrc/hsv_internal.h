@@ -162,6 +162,17 @@ hipError_t hsv_launch_tx_records(const uint8_t *txs, const uint64_t *offsets, ui
 hipError_t hsv_launch_tx_prep(const uint8_t *txs, const uint64_t *offsets, uint64_t tx_size, uint32_t n,
                               uint8_t *records, uint32_t *prep, uint32_t *fb_count, uint32_t *fb_list,
                               int lat_bits, hipStream_t stream);
+// Records, prepass and point pass in ONE persistent launch (hsv_mempool.hip,
+// hsv_verify_tx_fused_kernel): grid = the point pass's persistent grid
+// (hsv_tx_fused_blocks_per_cu blocks per CU), ctr = the zeroed HcCounters,
+// ready = nbatch = ceil(n / 64) zeroed words, vt_ws / canary as
+// hsv_verify_hp_kernel's.  n * 128 must stay below 2^32.
+int hsv_tx_fused_blocks_per_cu(int device);
+hipError_t hsv_launch_tx_fused(uint32_t grid, const uint8_t *txs, const uint64_t *offsets, uint64_t tx_size,
+                               uint32_t n, uint8_t *records, uint32_t *rec, void *ctr, uint32_t *fb_list,
+                               uint32_t *ready, int lat_bits, uint8_t *flags_out, uint32_t *strict_bits, void *vt_ws,
+                               const uint32_t *comb_b, uint32_t *canary, uint32_t nonce, uint32_t inject,
+                               uint32_t *fault, hipStream_t stream);
 // Transactions end to end: records (128 B per item, caller's buffer) and
 // verification, fused as above for large batches of the product variants;
 // otherwise hsv_launch_tx_records + hsv_launch_verify.

@@ -20,91 +20,9 @@
 #include "hsv_verify_core.hpp"
 #include "hsv_verify_hc.hpp"
 #include "hsv_rowpoint.hpp"
+#include "hsv_pointpass.hpp"
 
 namespace hsv {
-
-constexpr int kBlock = 256;
-
-
-// Per-lane variable-base tables in global memory (hsv_verify_core.hpp, VT):
-// lane region = 2 tables x (ENT - 1) entries x 128 B, entry = 8 x uint4.
-// Entry 0 of every table is the identity: it is not stored per lane; a zero
-// digit reads this one shared line (L2-resident) instead.  Loose encoding of
-// (Y+X, Y-X, 2Z, 2dT) = (1, 1, 2, 0).
-__device__ const uint4 kVtIdentity[8] = {{1u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {1u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u},
-                                         {2u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
-
-// Fault injection (hsv_test_inject_fault, tests only; uniform kernel argument,
-// kInject* in hsv_verify_core.hpp): the table stores of every lane are
-// replaced, between the table build and the window loop, by what a corrupted
-// workspace would hold.
-template <int ENT>
-struct GlobalVarTab {
-  static constexpr int kStored = ENT - 1;  // entries 1 .. ENT-1 per table
-  uint4 *base;
-  uint32_t inject = kInjectNone;
-  __device__ __forceinline__ void put(int t, int m, const uint32_t w[32]) const {
-    if (m == 0) return;
-    uint4 *e = base + (t * kStored + m - 1) * 8;
-    if (__builtin_expect(inject == kInjectZeroTables || (inject == kInjectFlipTables && t == 0), 0)) {
-      HSV_UNROLL
-      for (int q = 0; q < 8; ++q)
-        e[q] = inject == kInjectZeroTables ? make_uint4(0u, 0u, 0u, 0u)
-                                           : make_uint4(w[4 * q] ^ (q == 0 ? 1u : 0u), w[4 * q + 1], w[4 * q + 2],
-                                                        w[4 * q + 3]);
-      return;
-    }
-    HSV_UNROLL
-    for (int q = 0; q < 8; ++q) {
-#ifdef HSV_TIMING_STUB_TABLE_STORES  // timing probe only: entries computed, never stored
-      asm volatile("" ::"v"(w[4 * q]), "v"(w[4 * q + 1]), "v"(w[4 * q + 2]), "v"(w[4 * q + 3]));
-#else
-      e[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-#endif
-    }
-  }
-  __device__ __forceinline__ void get(int t, uint32_t m, uint32_t w[32]) const {
-    const uint4 *e = m ? base + (t * kStored + (int)m - 1) * 8 : kVtIdentity;
-    HSV_UNROLL
-    for (int q = 0; q < 8; ++q) {
-      const uint4 v = e[q];
-      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
-    }
-  }
-};
-
-template <int WA>
-constexpr int vt_lane_uint4() { return 2 * (1 << (WA - 1)) * 8; }
-
-
-// one (pk, sig, msg) record into words
-__device__ __forceinline__ void load_triple(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig,
-                                            uint64_t sig_stride, const uint8_t *msg, uint64_t msg_stride,
-                                            uint64_t i, uint32_t pkw[8], uint32_t sigw[16], uint32_t msgw[8]) {
-  const uint4 *p = reinterpret_cast<const uint4 *>(pk + i * pk_stride);
-  const uint4 *s = reinterpret_cast<const uint4 *>(sig + i * sig_stride);
-  const uint4 *m = reinterpret_cast<const uint4 *>(msg + i * msg_stride);
-  const uint4 p0 = p[0], p1 = p[1];
-  const uint4 s0 = s[0], s1 = s[1], s2 = s[2], s3 = s[3];
-  const uint4 m0 = m[0], m1 = m[1];
-  pkw[0] = p0.x; pkw[1] = p0.y; pkw[2] = p0.z; pkw[3] = p0.w;
-  pkw[4] = p1.x; pkw[5] = p1.y; pkw[6] = p1.z; pkw[7] = p1.w;
-  sigw[0] = s0.x; sigw[1] = s0.y; sigw[2] = s0.z; sigw[3] = s0.w;
-  sigw[4] = s1.x; sigw[5] = s1.y; sigw[6] = s1.z; sigw[7] = s1.w;
-  sigw[8] = s2.x; sigw[9] = s2.y; sigw[10] = s2.z; sigw[11] = s2.w;
-  sigw[12] = s3.x; sigw[13] = s3.y; sigw[14] = s3.z; sigw[15] = s3.w;
-  msgw[0] = m0.x; msgw[1] = m0.y; msgw[2] = m0.z; msgw[3] = m0.w;
-  msgw[4] = m1.x; msgw[5] = m1.y; msgw[6] = m1.z; msgw[7] = m1.w;
-}
-
-// Work counters of the comb kernels, zeroed before the launch (16 bytes).
-struct HcCounters {
-  uint32_t next;      // main pass: next item handed out
-  uint32_t fb_count;  // deferred full-length items appended to fb_list
-  uint32_t fb_next;   // fallback pass: next fb_list entry handed out
-  uint32_t pad;
-};
-
 
 #ifdef HSV_PHASE_CLOCKS  // tools/phase_clock_probe.py only: 8 words per 64-item batch of the point pass
 constexpr uint32_t kPhaseCap = 1u << 16;
@@ -130,20 +48,6 @@ hsv_prep_kernel(const uint8_t *__restrict__ pk, uint64_t pk_stride, const uint8_
   uint32_t pkw[8], sigw[16], msgw[8];
   load_triple(pk, pk_stride, sig, sig_stride, msg, msg_stride, idx, pkw, sigw, msgw);
   if (prep_scalars<WA>(pkw, sigw, msgw, rec + idx, n, lat_bits)) fb_list[atomicAdd(&ctr->fb_count, 1u)] = idx;
-}
-
-// Device self-checks of the product kernels (a device failure must
-// never become a silent reject).  Each launch gets
-//   fault[2]  two words the host zeroed: fault[0] <- 1 when an item's final
-//             point fails ge_is_sane (kFault), fault[1] <- 1 when a lane's
-//             canary changed; written with plain stores once the work loop
-//             is done (no atomics, so the words may live in pinned host memory);
-//   canary    one word per lane slot of the workspace, set to the launch's
-//             nonce when the lane starts and compared after every batch.
-// The host turns a non-zero word into HSV_ERR_DEVICE_FAULT.
-__device__ __forceinline__ void report_faults(uint32_t *fault, uint32_t bad) {
-  if (bad & 1u) fault[0] = 1u;
-  if (bad & 2u) fault[1] = 1u;
 }
 
 // Pass 2: persistent grid, 64-item batches from ctr->next over a virtual
@@ -1034,6 +938,16 @@ std::atomic<int> g_lat_bits{hsv::kLatCombBits};
 // test that injects on one thread leaves every other thread's calls alone.
 thread_local uint32_t t_inject = hsv::kInjectNone;
 
+// HSV_TX_FUSED=0: transactions as the record kernel + point pass pair (the
+// round-5 form), for A/B runs; read once per process.
+bool tx_fused_enabled() {
+  static const bool on = [] {
+    const char *v = std::getenv("HSV_TX_FUSED");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 // Per-launch canary nonce: odd, so never 0 (zeroed memory) or all-ones.
 uint32_t next_nonce() {
   static std::atomic<uint32_t> ctr{0x9e3779b9u};
@@ -1041,9 +955,6 @@ uint32_t next_nonce() {
 }
 
 
-#ifndef HSV_HP_WAVES
-#define HSV_HP_WAVES 3  // waves per SIMD of the point pass (launch bounds: 168 VGPRs)
-#endif
 
 // Two-pass launch (variants 19/20): prepass over all items, then the
 // persistent point pass.  Workspace: per-lane tables | counters (256 B) |
@@ -1091,6 +1002,12 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
   // process its block may sit on one CU (and a request from another thread
   // may relaunch it while this grid is dispatched), so the grid then leaves
   // one CU's worth of blocks out (1/256 of the slots).
+  // Transactions of the product form run as ONE fused launch (records,
+  // prepass and point pass; hsv_mempool.hip) unless HSV_TX_FUSED=0 selects
+  // the record kernel + point pass pair; its grid follows its own occupancy.
+  const bool fused = tx && WA == 4 && WAVES == HSV_HP_WAVES && CB == 16 && tx_fused_enabled() &&
+                     (uint64_t)n * 128u <= 0xffffffffull && hsv_tx_fused_blocks_per_cu(dev) > 0;
+  if (fused) bpc = std::min(bpc, hsv_tx_fused_blocks_per_cu(dev));
   const int resident = bpc * (hsvi_resident_started() && cus > 1 ? cus - 1 : cus);
   const uint32_t blocks_needed = (n + hsv::kBlock - 1) / hsv::kBlock;
   const uint32_t grid = std::min<uint32_t>(blocks_needed, (uint32_t)resident);
@@ -1098,7 +1015,8 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
   const size_t canary_bytes = ((size_t)grid * hsv::kBlock * sizeof(uint32_t) + 255) & ~(size_t)255;
   const size_t fb_bytes = (size_t)n * sizeof(uint32_t);
   const size_t rec_bytes = (size_t)n * hsv::kPrepWords * sizeof(uint32_t);
-  const size_t need = ws_bytes + 256 + canary_bytes + fb_bytes + rec_bytes;
+  const size_t ready_bytes = fused ? (((size_t)(n + 63u) / 64u) * sizeof(uint32_t) + 255) & ~(size_t)255 : 0;
+  const size_t need = ws_bytes + 256 + canary_bytes + fb_bytes + rec_bytes + ready_bytes;
   if (ws_need) {  // size query only
     *ws_need = need;
     return hipSuccess;
@@ -1115,8 +1033,18 @@ hipError_t launch_hp(const uint8_t *pk, uint64_t pk_stride, const uint8_t *sig, 
   uint32_t *canary = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256);
   uint32_t *fb_list = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256 + canary_bytes);
   uint32_t *rec = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256 + canary_bytes + fb_bytes);
+  uint32_t *ready = reinterpret_cast<uint32_t *>(ws8 + ws_bytes + 256 + canary_bytes + fb_bytes + rec_bytes);
   e = hipMemsetAsync(ctr, 0, sizeof(hsv::HcCounters), stream);
   if (e == hipSuccess && strict_bits) e = hipMemsetAsync(strict_bits, 0, (size_t)((n + 31u) / 32u) * 4u, stream);
+  if (e == hipSuccess && fused) {
+    e = hipMemsetAsync(ready, 0, ready_bytes, stream);
+    if (e == hipSuccess)
+      e = hsv_launch_tx_fused(grid, tx->txs, tx->offsets, tx->tx_size, n, tx->records, rec, ctr, fb_list, ready,
+                              g_lat_bits.load(), flags_out, strict_bits, vt_ws, comb_b, canary, next_nonce(), t_inject,
+                              fault, stream);
+    const hipError_t ef = own ? hipFreeAsync(ws, stream) : hipSuccess;
+    return e != hipSuccess ? e : ef;
+  }
   if (e == hipSuccess && tx) {
     static_assert(WA == 4, "hsv_launch_tx_prep writes the WA = 4 prepass record");
     e = hsv_launch_tx_prep(tx->txs, tx->offsets, tx->tx_size, n, tx->records, rec, &ctr->fb_count, fb_list,

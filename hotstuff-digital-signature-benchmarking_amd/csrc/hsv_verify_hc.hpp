@@ -226,9 +226,16 @@ HSV_INL uint32_t verify_one_half_comb(const uint32_t pk[8], const uint32_t sig[1
 constexpr int kPrepWords = 19;  // d(c1)[5] | d(|c0|)[5] | b[8] | meta
 enum : uint32_t { kPrepSOk = 1u, kPrepC0Neg = 2u, kPrepFallback = 4u };
 
+// How prep_scalars stores its record words: plain stores here; the fused
+// transaction launch (hsv_mempool.hip) passes write-through stores, because
+// other workgroups of the same launch read the records.
+struct PutPlain {
+  static HSV_MEMBER void u32(uint32_t *p, uint32_t v) { *p = v; }
+};
+
 // lat_bits: the lattice bound (kLatCombBits; lower values only to exercise the
 // full-length path in tests, hsvi_set_lattice_bits).
-template <int WA>
+template <int WA, class Put = PutPlain>
 HSV_INL bool prep_scalars(const uint32_t pk[8], const uint32_t sig[16], const uint32_t msg[8], uint32_t *rec,
                           uint64_t stride, int lat_bits = kLatCombBits) {
   using G = HalfCombWindows<WA>;
@@ -240,14 +247,15 @@ HSV_INL bool prep_scalars(const uint32_t pk[8], const uint32_t sig[16], const ui
   uint32_t d[5];
   recode_top5<WA, G::NW>(lat.c1, d);
   HSV_UNROLL
-  for (int i = 0; i < 5; ++i) rec[i * stride] = d[i];
+  for (int i = 0; i < 5; ++i) Put::u32(rec + i * stride, d[i]);
   recode_top5<WA, G::NW>(lat.c0, d);
   HSV_UNROLL
-  for (int i = 0; i < 5; ++i) rec[(5 + i) * stride] = d[i];
+  for (int i = 0; i < 5; ++i) Put::u32(rec + (5 + i) * stride, d[i]);
   const sc b = sc_mul_small(lat.c1, sig + 8);
   HSV_UNROLL
-  for (int i = 0; i < 8; ++i) rec[(10 + i) * stride] = b.v[i];
-  rec[18 * stride] = (s_ok ? kPrepSOk : 0u) | (lat.c0_neg ? kPrepC0Neg : 0u) | (lat.ok ? 0u : kPrepFallback);
+  for (int i = 0; i < 8; ++i) Put::u32(rec + (10 + i) * stride, b.v[i]);
+  Put::u32(rec + 18 * stride,
+           (s_ok ? kPrepSOk : 0u) | (lat.c0_neg ? kPrepC0Neg : 0u) | (lat.ok ? 0u : kPrepFallback));
   return !lat.ok;
 }
 

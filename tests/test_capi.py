@@ -55,7 +55,7 @@ def test_product_library_exports_exactly_the_header():
 # and the workspace pool's kept memory.  Measurement switches live in
 # libhsv_test.so's hooks only.
 PRODUCT_ENV = {"HSV_DEVICE", "HSV_SLOTS", "HSV_AUTO_COMMITTEE", "HSV_PACK_THREADS", "HSV_QC_RESIDENT",
-               "HSV_QC_RESIDENT_IDLE_MS", "HSV_WS_POOL_KEEP_MB"}
+               "HSV_QC_RESIDENT_IDLE_MS", "HSV_WS_POOL_KEEP_MB", "HSV_TX_FUSED"}
 
 
 def test_product_library_reads_only_the_documented_environment():

@@ -8,6 +8,8 @@ expected flags from oracle/ed25519_ref.py, cross-checked with libsodium) and
 the host-side argument checks; GPU tests compare the HIP path (record kernel +
 verification kernels, through the C ABI) with the oracle bit-exactly.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -196,3 +198,89 @@ def test_tx_device_fixed_2p16_vs_oracle(hsv, oracle_lib):
     mempool.verify_transactions_device(d, None, tx_size=512, n=w.n, flags=flags2)
     torch.cuda.synchronize()
     assert torch.equal(flags, flags2)
+
+
+def _ragged_txs(seed, n, max_msg):
+    import hashlib
+    from hsverify import verifier
+    rnd = np.random.default_rng(seed)
+    lens = rnd.integers(0, max_msg, n)
+    msgs = [rnd.integers(0, 256, int(m), dtype=np.uint8).tobytes() for m in lens]
+    seeds = rnd.integers(0, 256, (n, 32), dtype=np.uint8)
+    dig = np.stack([np.frombuffer(hashlib.sha512(m).digest()[:32], np.uint8) for m in msgs])
+    pk, sig = verifier.sign_many(seeds, dig)
+    sig[::13, 7] ^= 2                      # bad R
+    sig[5::29, 40] ^= 1                    # bad s
+    return [m + pk[i].tobytes() + sig[i].tobytes() for i, m in enumerate(msgs)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [0, 128])
+def test_tx_fused_launch_ragged_unaligned_vs_oracle(hsv, oracle_lib, bits):
+    """Above 2^13 transactions the device path is ONE launch: record batches,
+    then point batches behind per-batch ready words, then the fallback list
+    (hsv_verify_tx_fused_kernel).  Ragged lengths at an odd base
+    address, short transactions, flags and STRICT_OK bits, against the C
+    oracle; with the lattice bound lowered to 128 (test library) items without
+    a short pair go down the fallback list the launch runs last.  Run twice:
+    the outputs must not depend on which wave published which batch."""
+    import torch
+    from hsverify import _testing, mempool
+    n = 12000
+    txs = _ragged_txs(31 + bits, n, 700)
+    for i in (100, 8191, 11999):
+        txs[i] = txs[i][:50]               # short transactions: flags 0
+    buf, offsets = mempool.pack(txs)
+    exp = oracle_tx_flags(oracle_lib, buf, offsets)
+    assert exp[100] == 0 and exp[11999] == 0 and (exp & o.STRICT_OK).sum() > n // 2
+    dev = torch.device("cuda:0")
+    backing = torch.zeros(buf.size + 64, dtype=torch.uint8, device=dev)
+    d_txs = backing[5:5 + buf.size]
+    d_txs.copy_(torch.from_numpy(buf))
+    d_off = torch.from_numpy(offsets.view(np.int64)).to(dev)
+    with _testing.test_library():
+        prev = _testing.set_lattice_bits(bits)
+        try:
+            for _ in range(2):
+                flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+                bits_out = torch.zeros((n + 31) // 32, dtype=torch.int32, device=dev)
+                fault = torch.zeros(2, dtype=torch.int32, device=dev)
+                mempool.verify_transactions_device(d_txs, d_off, n=n, flags=flags, strict_bits=bits_out, fault=fault)
+                torch.cuda.synchronize()
+                got = flags.cpu().numpy()
+                assert (got == exp).all(), np.nonzero(got != exp)[0][:8]
+                b = bits_out.cpu().numpy().view(np.uint32)
+                unpacked = (b[np.arange(n) // 32] >> (np.arange(n) % 32)) & 1
+                assert (unpacked == (exp & o.STRICT_OK)).all()
+                assert not fault.cpu().numpy().any()
+        finally:
+            _testing.set_lattice_bits(prev)
+
+
+@pytest.mark.gpu
+def test_tx_fused_and_two_launch_forms_agree():
+    """HSV_TX_FUSED=0 (record kernel + point pass, the round-5 form) and the
+    fused launch give the same flags on 2^15 fixed-size transactions with
+    corruptions (a child process per form: the switch is read once)."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    child = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, %r); sys.path.insert(0, %r + "/hotstuff-digital-signature-benchmarking_amd")
+from hsverify import mempool, synth
+w = synth.transactions(1 << 15, tx_size=333, seed=77, corrupt_frac=0.05)
+d = torch.from_numpy(w.txs.reshape(-1)).to("cuda:0")
+f = torch.zeros(w.n, dtype=torch.uint8, device="cuda:0")
+mempool.verify_transactions_device(d, None, tx_size=333, n=w.n, flags=f)
+torch.cuda.synchronize()
+sys.stdout.buffer.write(f.cpu().numpy().tobytes())
+""" % (ROOT, ROOT)
+    outs = []
+    for fused in ("1", "0"):
+        env = dict(os.environ, HSV_TX_FUSED=fused)
+        r = subprocess.run([sys.executable, "-c", child], capture_output=True, timeout=180, env=env)
+        assert r.returncode == 0, r.stderr.decode()[-2000:]
+        outs.append(np.frombuffer(r.stdout, np.uint8))
+    assert outs[0].size == 1 << 15 and (outs[0] == outs[1]).all()
+    assert (outs[0] & o.STRICT_OK).sum() > (1 << 14)

@@ -3,7 +3,8 @@
 (HSV_LIB), alternating fresh processes: prints, per run, the C4 line, the
 mempool line and its ratio to C4, the host-buffer call and the cached C3 QC
 p50, then the medians per library.
-python tools/bench_lib_ab.py [--rounds 2] LIB [LIB ...]"""
+python tools/bench_lib_ab.py [--rounds 2] LIB[@VAR=VALUE] [LIB[@VAR=VALUE] ...]
+(LIB@VAR=VALUE runs that library with one more environment variable)"""
 import argparse
 import json
 import os
@@ -22,8 +23,13 @@ def main():
     res = {lib: [] for lib in a.libs}
     for _ in range(a.rounds):
         for lib in a.libs:
+            name, _, kv = lib.partition("@")
+            env = dict(os.environ, HSV_LIB=name)
+            if kv:
+                k, _, v = kv.partition("=")
+                env[k] = v
             r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--no-launched"],
-                               capture_output=True, text=True, timeout=600, env=dict(os.environ, HSV_LIB=lib))
+                               capture_output=True, text=True, timeout=600, env=env)
             if r.returncode != 0:
                 print(lib, "failed", r.stderr[-2000:])
                 return r.returncode

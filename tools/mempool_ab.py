@@ -3,7 +3,9 @@
 in HBM, record + prepass + point pass) between library builds, alternating
 fresh processes; HSV_LIB selects each build (files in hsverify/).
 
-python tools/mempool_ab.py [--rounds 3] LIB [LIB ...]
+python tools/mempool_ab.py [--rounds 3] LIB[@VAR=VALUE] [LIB[@VAR=VALUE] ...]
+(LIB@VAR=VALUE runs that library with one more environment variable, e.g.
+libhsv.so@HSV_TX_FUSED=0)
 """
 import argparse
 import json
@@ -30,8 +32,13 @@ def main():
     res = {lib: [] for lib in a.libs}
     for _ in range(a.rounds):
         for lib in a.libs:
+            name, _, kv = lib.partition("@")
+            env = dict(os.environ, HSV_LIB=name)
+            if kv:
+                k, _, v = kv.partition("=")
+                env[k] = v
             r = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT)], capture_output=True, text=True,
-                               timeout=300, env=dict(os.environ, HSV_LIB=lib))
+                               timeout=300, env=env)
             if r.returncode != 0:
                 print(r.stdout, r.stderr[-2000:])
                 return r.returncode
