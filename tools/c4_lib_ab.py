@@ -2,7 +2,8 @@
 """Same-box A/B of the C4 line (bench.py --no-qc --no-cpu-baseline) between
 library builds in hsverify/ (HSV_LIB), alternating fresh processes; prints
 each run's verif/s, ms per step and one-launch time, then the medians.
-python tools/c4_lib_ab.py [--rounds 3] LIB [LIB ...]"""
+python tools/c4_lib_ab.py [--rounds 3] LIB[@VAR=VALUE] [LIB[@VAR=VALUE] ...]
+(LIB@VAR=VALUE runs that library with one more environment variable)"""
 import argparse
 import json
 import os
@@ -21,8 +22,13 @@ def main():
     res = {lib: [] for lib in a.libs}
     for _ in range(a.rounds):
         for lib in a.libs:
+            name, _, kv = lib.partition("@")
+            env = dict(os.environ, HSV_LIB=name)
+            if kv:
+                k, _, v = kv.partition("=")
+                env[k] = v
             r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-qc", "--no-cpu-baseline"],
-                               capture_output=True, text=True, timeout=300, env=dict(os.environ, HSV_LIB=lib))
+                               capture_output=True, text=True, timeout=300, env=env)
             if r.returncode != 0:
                 print(lib, "rc", r.returncode, r.stderr[-1500:])
                 return r.returncode
