@@ -343,6 +343,13 @@ with _testing.test_library() as lib:
     # destroy free device memory, and hipFree waits for every grid on the device; the pause
     # keeps the service stopped until each free has returned, so they never wait for it.
     s_bad = bytearray(sg); s_bad[40] ^= 1; s_bad = bytes(s_bad)
+    def create_destroy():
+        t0 = time.perf_counter()
+        c = ctypes.c_void_p()
+        assert lib.hsv_committee_create(np.ascontiguousarray(w.pk).ctypes.data, w.n, ctypes.byref(c)) == 0
+        lib.hsv_committee_destroy(c)
+        return time.perf_counter() - t0
+    base = [create_destroy() for _ in range(3)]  # the same calls with the service idle
     stop, errors, done = threading.Event(), [], [0]
     def votes():
         while not stop.is_set():
@@ -353,23 +360,25 @@ with _testing.test_library() as lib:
     t.start()
     time.sleep(0.2)
     q0 = counts()
-    worst = 0.0
+    busy = []
     try:
         for i in range(5):
-            t0 = time.perf_counter()
-            c = ctypes.c_void_p()
-            assert lib.hsv_committee_create(np.ascontiguousarray(w.pk).ctypes.data, w.n, ctypes.byref(c)) == 0
-            lib.hsv_committee_destroy(c)
-            worst = max(worst, time.perf_counter() - t0)
+            busy.append(create_destroy())
             time.sleep(0.05)
     finally:
         stop.set()
         t.join(30)
     q1 = counts()
     assert not errors, errors[:3]
-    assert worst < 0.5, ("a committee create/destroy waited for the busy service", worst)
+    # A free that waited for the busy service would not return until the other
+    # thread stops: every call would stall.  The median must stay within the
+    # idle calls' time several times over (at least 0.5 s; ~10 ms measured,
+    # profiles/r06/r06q_resident_default.txt), and no call may take seconds
+    # (one call of 0.87 s was seen once on a loaded box, r06z).
+    assert sorted(busy)[len(busy) // 2] < max(0.5, 4 * max(base)), ("create/destroy waited for the busy service", busy, base)
+    assert max(busy) < 5.0, ("a create/destroy stalled", busy, base)
     assert q1[1] - q0[1] > 0, "the service answered nothing while the other thread ran"
-    print("default ok", done[0], worst, q1)
+    print("default ok", done[0], [round(x, 4) for x in busy], [round(x, 4) for x in base], q1)
 """
 
 
@@ -393,3 +402,4 @@ def test_resident_service_is_the_default(setting):
     r = subprocess.run([sys.executable, "-c", DEFAULT_CHILD.format(tests=here, pkg=PKG)], capture_output=True,
                        text=True, timeout=300, env=env)
     assert r.returncode == 0 and "default ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
+    print(r.stdout.strip())
