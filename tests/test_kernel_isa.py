@@ -117,3 +117,26 @@ def test_product_work_loops_are_uniform(hipcc, src):
             assert not divergent, f"{name}: work loop {h} compiled as a divergent loop"
     if src == "hsv_kernels.hip":
         assert any("hsv_verify_hp_kernel" in k and work_loops(v) for k, v in ks.items()), "point pass loop not found"
+
+
+def test_fused_transaction_launch_hands_off_write_through(hipcc):
+    """The fused transaction launch (hsv_verify_fused... in hsv_mempool.hip,
+    DESIGN.md 4b) hands records from the waves that build them to other
+    workgroups of the same launch.  Per-XCD L2s are not coherent, so in the
+    record phase (between s_setprio 3 and s_setprio 0) every global or buffer
+    store must be write-through (sc1) -- scratch spills are the lane's own --
+    each record batch must be published by an atomic after an
+    s_waitcnt vmcnt(0), and the point phase must acquire (buffer_inv sc1)."""
+    ks = _kernels(_compile(os.path.join(PKG, "csrc", "hsv_mempool.hip"), "hsv_mempool_handoff.s", []))
+    fused = [(k, v) for k, v in ks.items() if "fused_kernel" in k]
+    assert fused, "fused transaction kernel not found"
+    for name, body in fused:
+        start = next(i for i, l in enumerate(body) if "s_setprio 3" in l)
+        end = next(i for i, l in enumerate(body) if "s_setprio 0" in l and i > start)
+        stores = [l.strip() for l in body[start:end] if re.search(r"\b(global|buffer|flat)_store", l)]
+        assert stores and all(" sc1" in l for l in stores), [l for l in stores if " sc1" not in l][:4]
+        assert any("buffer_store_dwordx4" in l for l in stores), "records not stored 16 B at a time"
+        atomics = [i for i in range(start, end) if re.search(r"global_atomic_add\b", body[i])]
+        waits = [i for i in range(start, end) if re.match(r"\s*s_waitcnt vmcnt\(0\)", body[i])]
+        assert any(w < a for a in atomics for w in waits), "no drain before a publishing atomic"
+        assert any("buffer_inv sc1" in l for l in body[end:]), "the point phase never acquires"
