@@ -1369,10 +1369,11 @@ extern "C" int hsvi_set_lattice_bits(int bits) {
 }
 
 // Fault injection mode of the calling thread's following launches (kInject*:
-// 1 zeroed tables, 2 overwritten canary, 3 flipped table bits; 0 = off).
+// 1 zeroed tables, 2 overwritten canary, 3 flipped table bits, 4 a record
+// batch of the fused transaction launch never published; 0 = off).
 // Returns the previous mode, or -1 for an unknown one.
 extern "C" int hsvi_set_inject(int mode) {
-  if (mode < 0 || mode > (int)hsv::kInjectFlipTables) return -1;
+  if (mode < 0 || mode > (int)hsv::kInjectNoPublish) return -1;
   const int prev = (int)t_inject;
   t_inject = (uint32_t)mode;
   return prev;

@@ -54,6 +54,7 @@ enum : uint32_t {
   kInjectZeroTables = 1,  // table entries read back as zeros
   kInjectCanary = 2,      // the lane's workspace canary is overwritten mid-batch
   kInjectFlipTables = 3,  // one bit of table entries flipped
+  kInjectNoPublish = 4,   // fused transaction launch: record batch 0 is never published
 };
 
 // kFault when both points decoded (the equation is then part of the verdict)

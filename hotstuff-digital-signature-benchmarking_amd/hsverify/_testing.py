@@ -20,6 +20,7 @@ INJECT_NONE = 0
 INJECT_ZERO_TABLES = 1   # table entries read back as zeros
 INJECT_CANARY = 2        # a lane's workspace canary is overwritten mid-batch
 INJECT_FLIP_TABLES = 3   # one bit of table entries flipped
+INJECT_NO_PUBLISH = 4    # fused transaction launch: record batch 0 never published (bounded wait -> fault)
 
 
 @contextlib.contextmanager

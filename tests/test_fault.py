@@ -207,8 +207,9 @@ def test_committee_path_canary_mode_is_not_a_fault(env, tlib, generic):
 
 @pytest.mark.parametrize("mode", [1, 2, 3])
 def test_large_transaction_batch_reports_faults(env, tlib, mode):
-    """More than 2^13 transactions: the fused record + prepass kernel and the
-    point pass (hsv_launch_verify_tx), canary included."""
+    """More than 2^13 transactions: the fused launch (records, prepass and
+    point pass in one kernel, hsv_launch_verify_tx), canary included (ADVICE
+    round 3)."""
     _lib, _testing, _, synth, verifier = env
     from hsverify import mempool
     t = synth.transactions((1 << 13) + 64, tx_size=160, seed=14, corrupt_frac=0.0)
@@ -290,3 +291,34 @@ def test_concurrent_device_calls_own_their_fault_words(env, tlib):
     second = verifier.device_faults(-1, clear=True)
     assert (first | second) == 1
     assert verifier.device_faults(-1, clear=True) == 0
+
+
+def test_unpublished_transaction_batch_is_a_device_fault(env, tlib):
+    """The fused transaction launch hands record batches to point batches
+    through per-batch ready words.  With one batch never
+    published (INJECT_NO_PUBLISH), the bounded waits end (0.5 s of the wall
+    clock each): the launch finishes within seconds, its fault words report
+    it, no transaction of that batch is accepted, the host API returns
+    HSV_ERR_DEVICE_FAULT -- and without the hook the same call verifies."""
+    import time
+    import torch
+    _lib, _testing, _, synth, verifier = env
+    from hsverify import mempool
+    t = synth.transactions((1 << 13) + 512, tx_size=200, seed=21, corrupt_frac=0.0)
+    dev = torch.device("cuda:0")
+    d = torch.from_numpy(np.ascontiguousarray(t.txs)).to(dev).view(-1)
+    flags = torch.zeros(t.n, dtype=torch.uint8, device=dev)
+    words = torch.full((2,), -1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with _testing.injected_fault(_testing.INJECT_NO_PUBLISH):
+        mempool.verify_transactions_device(d, tx_size=200, n=t.n, flags=flags, fault=words)
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t0 < 20.0
+    assert verifier.fault_bits(words) & 1
+    got = flags.cpu().numpy()
+    assert not (got[:64] & 1).any()  # batch 0: never verified, never accepted
+    with _testing.injected_fault(_testing.INJECT_NO_PUBLISH):
+        with pytest.raises(_lib.HsvLibraryError, match="HSV_ERR_DEVICE_FAULT"):
+            mempool.verify_transactions_fixed(t.txs)
+    assert (mempool.verify_transactions_fixed(t.txs) & 1).all()
