@@ -6,13 +6,16 @@
 //     digest  = Digest(SHA-512(message)[..32])
 //     Signature::from_bytes(sig[..32], sig[32..64]).verify(&digest, &PublicKey(pk))
 //
-// Stage 1 (hsv_tx_record_kernel, one lane per transaction, loads staged through
-// LDS by the whole wave) hashes the message and writes the 128-byte record
-// pk || R || s || digest; stage 2 is the
-// generic verification launch over those records (strides 128, the same
-// kernels and flags as hsv_verify_device).  The record pass is a small
-// fraction of a verification: a 512-byte transaction is 4 SHA-512 blocks
-// (about 4 x 80 rounds) against ~2,300 field operations for the signature.
+// The record work (tx_record_lane, one lane per transaction, loads staged
+// through LDS by the whole wave) hashes the message and writes the 128-byte
+// record pk || R || s || digest, then runs the point pass's prepass on it.
+// Above 2^13 transactions it is phase 1 of ONE fused launch whose waves then
+// take the point batches (hsv_verify_tx_fused_kernel, below); otherwise, and
+// with HSV_TX_FUSED=0, the record kernel is followed by the generic
+// verification launch over the records (strides 128, the same kernels and
+// flags as hsv_verify_device).  The record work is a small fraction of a
+// verification: a 512-byte transaction is 4 SHA-512 blocks (about 4 x 80
+// rounds) against ~2,300 field operations for the signature.
 #include <hip/hip_runtime.h>
 
 #include <mutex>
