@@ -269,9 +269,9 @@ def _timed_lib(fn, reps, warm=10):
     from hsverify import _lib
     lib = _lib.load()
     buf = (ctypes.c_double * 8)()
+    gc.collect()  # before the warm-up: a collection between warm-up and reps left the first rep cold
     for _ in range(warm):
         fn()
-    gc.collect()
     was = gc.isenabled()
     gc.disable()
     ts, marks = [], []
@@ -463,8 +463,8 @@ def tc_dropin_sequential(reps):
                     return False
         return True
 
+    gc.collect()  # before the warm-up loop (as _timed_lib)
     assert loop()
-    gc.collect()
     was = gc.isenabled()
     gc.disable()
     ts, calls = [], []
